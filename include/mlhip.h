@@ -1,0 +1,216 @@
+/*
+ * mlhip.h -- C ABI of the MI355X (gfx950) proving backend for the hot path of
+ * fr34za/multilinear (reference @ 2025-06-20): radix-2 NTT, Reed-Solomon LDE,
+ * SHA-256 Merkle level hashing, FRI layer folding, and MLE/sumcheck round
+ * sums over the field.rs prime M = 2^128 - 45*2^40 + 1.
+ *
+ * Conventions (identical to the reference's in-memory forms):
+ *   - a field element is 16 bytes: the canonical u128 (value < M), little
+ *     endian -- Field128::as_ref (src/field.rs:33-38);
+ *   - a digest is the 32 SHA-256 output bytes (HashDigest, merkle_tree/mod.rs:5);
+ *   - a Merkle tree of L = 2^l leaves is one buffer of 2L-1 digests in level
+ *     order (leaves first, root last) -- Merkle::layers flattened
+ *     (merkle_tree/mod.rs:7-11);
+ *   - "dev" pointers are device (HBM) pointers on the context's device, e.g.
+ *     from mlh_malloc or any HIP allocator; "host" pointers are host memory.
+ *   - All work is enqueued on the context's HIP stream; functions that return
+ *     host results (roots, sums, proofs) synchronise that stream.
+ *
+ * Errors: the reference prover panics (assert!) on non-power-of-two sizes,
+ * bad lengths and the "not an RS code" check; here every entry point returns
+ * an mlh_status and mlh_last_error() gives the message.  Nothing falls back
+ * to a CPU implementation: without a usable gfx950 device every compute call
+ * returns MLH_ERR_HIP.
+ */
+#ifndef MLHIP_H
+#define MLHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum mlh_status {
+  MLH_OK = 0,
+  MLH_ERR_INVALID = 1,       /* bad argument (null pointer, size out of range)   */
+  MLH_ERR_NOT_POW2 = 2,      /* "must be a power of two" asserts                   */
+  MLH_ERR_BAD_GENERATOR = 3, /* generator is not of order exactly 2^log_n          */
+  MLH_ERR_HIP = 4,           /* HIP runtime error / no device                      */
+  MLH_ERR_OOM = 5,           /* device allocation failed                           */
+  MLH_ERR_NOT_RS_CODE = 6,   /* fri/mod.rs:119-122 "not an RS code"                */
+  MLH_ERR_VERIFY = 7         /* verifier rejected                                  */
+} mlh_status;
+
+typedef struct mlh_ctx mlh_ctx;               /* device + stream + twiddle caches */
+typedef struct mlh_transcript mlh_transcript; /* transcript.rs Transcript         */
+typedef struct mlh_fri_prover mlh_fri_prover; /* fri/mod.rs FriProverData         */
+
+#define MLH_LOG_BLOWUP 1   /* fri/mod.rs:16 */
+#define MLH_NUM_QUERIES 128 /* fri/mod.rs:17 */
+
+/* ---- context and memory ------------------------------------------------- */
+const char* mlh_version(void);
+mlh_status mlh_context_create(int device, void* hip_stream, mlh_ctx** out);
+void mlh_context_destroy(mlh_ctx* ctx);
+mlh_status mlh_set_stream(mlh_ctx* ctx, void* hip_stream);
+mlh_status mlh_synchronize(mlh_ctx* ctx);
+const char* mlh_last_error(const mlh_ctx* ctx);
+mlh_status mlh_malloc(mlh_ctx* ctx, size_t bytes, void** dev);
+mlh_status mlh_free(mlh_ctx* ctx, void* dev);
+mlh_status mlh_memcpy_h2d(mlh_ctx* ctx, void* dev, const void* host, size_t bytes);
+mlh_status mlh_memcpy_d2h(mlh_ctx* ctx, void* host, const void* dev, size_t bytes);
+mlh_status mlh_memcpy_d2d(mlh_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+/* ---- field helpers (host) ------------------------------------------------ */
+/* NttField::pow_2_generator (src/ntt/mod.rs:42-54): 3^((M-1)/2^log_size). */
+mlh_status mlh_pow_2_generator(uint32_t log_size, uint8_t gen_out[16]);
+/* NttField::pow_2_generator_powers (src/ntt/mod.rs:18-28): out[i] = g^i,
+ * i < 2^log_size, written to dev (no serial chain on the device). */
+mlh_status mlh_pow_2_generator_powers(mlh_ctx* ctx, uint32_t log_size, void* dev_out);
+
+/* ---- NTT (src/ntt/mod.rs) ------------------------------------------------ */
+/* Polynomial::ntt (ntt/mod.rs:69-110): evals[i] = sum_j coeffs[j] gen^(ij),
+ * natural order in and out.  gen must have order exactly 2^log_n.  In-place
+ * (dev_in == dev_out) is allowed. */
+mlh_status mlh_ntt(mlh_ctx* ctx, const void* dev_coeffs, void* dev_evals, uint32_t log_n,
+                   const uint8_t gen[16]);
+/* LagrangePolynomial::intt (ntt/mod.rs:132-173): gen is the forward
+ * generator (LagrangePolynomial::gen); uses gen^-1 and scales by 1/n. */
+mlh_status mlh_intt(mlh_ctx* ctx, const void* dev_evals, void* dev_coeffs, uint32_t log_n,
+                    const uint8_t gen[16]);
+/* bit_reverse_permutation (ntt/mod.rs:113-123), out of place (in != out). */
+mlh_status mlh_bit_reverse_permutation(mlh_ctx* ctx, const void* dev_in, void* dev_out,
+                                       uint32_t log_n);
+/* Vec -> Vec convenience (host buffers, includes PCIe copies). */
+mlh_status mlh_ntt_host(mlh_ctx* ctx, const uint8_t* host_in, uint8_t* host_out, uint32_t log_n,
+                        const uint8_t gen[16], int inverse);
+
+/* ---- Reed-Solomon, Merkle, FRI (src/fri, src/merkle_tree) -------------------- */
+/* reed_solomon (fri/mod.rs:19-28): zero-pad 2^log_n coeffs to 2^(log_n+1) and
+ * NTT with gen (order 2^(log_n+1)).  dev_code holds 2^(log_n+1) elements. */
+mlh_status mlh_reed_solomon(mlh_ctx* ctx, const void* dev_coeffs, uint32_t log_n,
+                            const uint8_t gen[16], void* dev_code);
+/* Bytes of a flattened tree with `leaves` leaves: (2*leaves - 1) * 32. */
+uint64_t mlh_merkle_layers_bytes(uint64_t leaves);
+/* commit_rs_code (fri/mod.rs:45-55) + Merkle::commit (merkle_tree/mod.rs:65-85):
+ * leaf i = SHA256(LE16(code[i]) ‖ LE16(code[i + n/2])), n = 2^log_code. */
+mlh_status mlh_merkle_commit_pairs(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                                   void* dev_layers, uint8_t root_out[32]);
+/* Merkle::commit over `count` (power of two) items of item_len bytes each. */
+mlh_status mlh_merkle_commit(mlh_ctx* ctx, const void* dev_items, uint64_t item_len,
+                             uint64_t count, void* dev_layers, uint8_t root_out[32]);
+/* Merkle::batch_commit (merkle_tree/mod.rs:92-131): m batches of `count`
+ * items, batch j at dev_items + j*count*item_len; leaf i hashes the m items i. */
+mlh_status mlh_merkle_batch_commit(mlh_ctx* ctx, const void* dev_items, uint64_t item_len,
+                                   uint32_t m, uint64_t count, void* dev_layers,
+                                   uint8_t root_out[32]);
+/* The fold loop of FriProverData::fold_step (fri/mod.rs:89-114): layer of
+ * 2^log_layer values (pairs i, i + n/2) -> 2^(log_layer-1) values, fold index
+ * k, original domain 2^log_domain (twiddle g^(-i 2^k)). */
+mlh_status mlh_fri_fold(mlh_ctx* ctx, const void* dev_layer, uint32_t log_layer, uint32_t k,
+                        uint32_t log_domain, const uint8_t r[16], void* dev_next);
+
+/* FriProverData (fri/mod.rs:10-175), device resident. */
+mlh_status mlh_fri_prover_init(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                               mlh_transcript* tr, mlh_fri_prover** out); /* :58-76  */
+mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
+                                    const uint8_t r[16], mlh_transcript* tr); /* :79-134 */
+mlh_status mlh_fri_prover_fold(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                               mlh_transcript* tr, mlh_fri_prover** out); /* :136-145 */
+uint32_t mlh_fri_prover_num_trees(const mlh_fri_prover* p);
+mlh_status mlh_fri_prover_roots(const mlh_fri_prover* p, uint8_t* roots_out /* [T][32] */);
+/* last_element (fri/mod.rs:13); MLH_ERR_INVALID while still None. */
+mlh_status mlh_fri_prover_last_element(const mlh_fri_prover* p, uint8_t out[16]);
+/* open_query_at (fri/mod.rs:154-175) -> one query record (layout below). */
+mlh_status mlh_fri_prover_open_query(mlh_ctx* ctx, const mlh_fri_prover* p, uint64_t index,
+                                     uint8_t* out);
+void mlh_fri_prover_destroy(mlh_fri_prover* p);
+
+/* FriProof (fri/mod.rs:239-249) as caller-allocated flat buffers.
+ * Query record for a code of 2^L elements: for tree t = 0..L-2: the opened
+ * ReedSolomonPair (32 B) then its L-1-t sibling digests leaf-to-root (32 B
+ * each); the Direction of level i is Right iff bit i of the opened index is 0
+ * (merkle_tree/mod.rs:43-47), so it is not stored. */
+typedef struct mlh_fri_proof {
+  uint32_t log_code;    /* L = log2(code length)                    */
+  uint32_t num_trees;   /* commitments: L - MLH_LOG_BLOWUP          */
+  uint32_t num_queries; /* MLH_NUM_QUERIES                          */
+  uint8_t* commitments; /* [num_trees][32]                         */
+  uint8_t last_elem[16];
+  uint8_t last_random[32];
+  uint64_t* query_indices; /* [num_queries]                         */
+  uint8_t* queries;        /* [num_queries][mlh_fri_query_bytes(L)]  */
+} mlh_fri_proof;
+uint64_t mlh_fri_query_bytes(uint32_t log_code);
+/* FriProof::prove (fri/mod.rs:261-285). */
+mlh_status mlh_fri_prove(mlh_ctx* ctx, const void* dev_code, uint32_t log_code, mlh_transcript* tr,
+                         mlh_fri_proof* proof);
+/* FriProof::verify (fri/mod.rs:287-340), host side; MLH_ERR_VERIFY if rejected. */
+mlh_status mlh_fri_verify(const mlh_fri_proof* proof);
+
+/* ---- transcript (src/transcript.rs), host side --------------------------- */
+mlh_status mlh_transcript_create(mlh_transcript** out);
+mlh_status mlh_transcript_clone(const mlh_transcript* t, mlh_transcript** out);
+void mlh_transcript_destroy(mlh_transcript* t);
+mlh_status mlh_transcript_absorb(mlh_transcript* t, const uint8_t* bytes, uint64_t len); /* :31 */
+mlh_status mlh_transcript_random(const mlh_transcript* t, uint8_t out[32]);             /* :23 */
+mlh_status mlh_transcript_next_challenge(mlh_transcript* t, uint8_t out[16]);          /* :35 */
+
+/* ---- multilinear polynomials and sumcheck -------------------------------- */
+/* MultilinearPolynomialEvals::to_coefficient (polynomials.rs:150-163), in place. */
+mlh_status mlh_mle_to_coefficient(mlh_ctx* ctx, void* dev_evals, uint32_t log_n);
+/* MultilinearPolynomial::to_evaluation (polynomials.rs:111-124), in place. */
+mlh_status mlh_mle_to_evaluation(mlh_ctx* ctx, void* dev_coeffs, uint32_t log_n);
+/* delta table of SumcheckTables::build_tables_for_pcs (sumcheck.rs:128-145,
+ * Mask::evaluate evaluation.rs:51-73): out[idx] = prod_i (bit_i(idx) ?
+ * p[n-1-i] : 1-p[n-1-i]); host_points: n elements. */
+mlh_status mlh_eq_table(mlh_ctx* ctx, const uint8_t* host_points, uint32_t n, void* dev_out);
+/* MultilinearPolynomialEvals::evaluate (polynomials.rs:165-187). */
+mlh_status mlh_mle_evaluate(mlh_ctx* ctx, const void* dev_evals, uint32_t n,
+                            const uint8_t* host_args, uint8_t out[16]);
+/* SumcheckTables::partial_sum (sumcheck.rs:204-232), composition x[0]
+ * (multilinear_pcs.rs:56), at X = 1 and X = 2: out = s1 ‖ s2.
+ * Tables have 2^log_height elements. */
+mlh_status mlh_sumcheck_partial_sums(mlh_ctx* ctx, const void* dev_matrix, const void* dev_delta,
+                                     uint32_t log_height, uint8_t out[32]);
+/* SumcheckTables::fold (sumcheck.rs:234-247), in place: height 2^log_height
+ * -> 2^(log_height-1) (first half). */
+mlh_status mlh_sumcheck_fold(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, uint32_t log_height,
+                             const uint8_t r[16]);
+/* fold followed by the next round's partial sums, one HBM pass. */
+mlh_status mlh_sumcheck_fold_and_sums(mlh_ctx* ctx, void* dev_matrix, void* dev_delta,
+                                      uint32_t log_height, const uint8_t r[16], uint8_t out[32]);
+/* SumcheckTables::compute_sumcheck_polynomials (sumcheck.rs:77-102) for the
+ * PCS composition (x[0], total degree 2): log_height rounds; per round the
+ * two nonzero coefficients (c1, c2) go to polys_out[round][2][16] and the
+ * challenge to rs_out[round][16].  Tables are folded in place. */
+mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, uint32_t log_height,
+                              const uint8_t sum[16], mlh_transcript* tr, uint8_t* polys_out,
+                              uint8_t* rs_out);
+
+/* ---- multilinear PCS (src/fri/multilinear_pcs.rs) ------------------------ */
+typedef struct mlh_pcs_proof {
+  mlh_fri_proof fri;
+  uint8_t* sumcheck_polys; /* [n_vars][2][16] nonzero coefficients c1, c2 */
+} mlh_pcs_proof;
+/* PCSProof::prove (multilinear_pcs.rs:90-136): dev_evals (2^n_vars elements)
+ * is not modified; host_inputs: n_vars points; output: the claimed value. */
+mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
+                         const uint8_t* host_inputs, const uint8_t output[16], mlh_transcript* tr,
+                         mlh_pcs_proof* proof);
+/* PCSProof::verify (multilinear_pcs.rs:138-190), host side. */
+mlh_status mlh_pcs_verify(const mlh_pcs_proof* proof, uint32_t n_vars, const uint8_t* host_inputs,
+                          const uint8_t output[16], mlh_transcript* tr);
+
+/* ---- device timing helpers (bench / profiling) --------------------------- */
+/* Time `iters` forward NTTs of 2^log_n on the context stream with HIP events
+ * (dev_buf is transformed in place); returns the mean ms per NTT. */
+mlh_status mlh_bench_ntt(mlh_ctx* ctx, void* dev_buf, uint32_t log_n, uint32_t iters,
+                         float* ms_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MLHIP_H */

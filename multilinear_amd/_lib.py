@@ -1,0 +1,132 @@
+"""ctypes binding of libmlhip.so (the C ABI declared in include/mlhip.h).
+
+The library is built in-tree (``multilinear_amd/libmlhip.so``) by
+``__graft_entry__.build()`` / ``make -C multilinear_amd/csrc``.  There is no
+fallback: if the library is missing this module raises, and every compute
+entry point returns MLH_ERR_HIP when no gfx950 device is usable.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmlhip.so")
+
+MLH_OK = 0
+STATUS_NAMES = {
+    0: "MLH_OK",
+    1: "MLH_ERR_INVALID",
+    2: "MLH_ERR_NOT_POW2",
+    3: "MLH_ERR_BAD_GENERATOR",
+    4: "MLH_ERR_HIP",
+    5: "MLH_ERR_OOM",
+    6: "MLH_ERR_NOT_RS_CODE",
+    7: "MLH_ERR_VERIFY",
+}
+LOG_BLOWUP = 1
+NUM_QUERIES = 128
+
+
+class MlhError(RuntimeError):
+    def __init__(self, status, msg=""):
+        self.status = status
+        super().__init__("%s: %s" % (STATUS_NAMES.get(status, status), msg))
+
+
+class FriProofC(ctypes.Structure):
+    _fields_ = [
+        ("log_code", ctypes.c_uint32),
+        ("num_trees", ctypes.c_uint32),
+        ("num_queries", ctypes.c_uint32),
+        ("commitments", ctypes.c_void_p),
+        ("last_elem", ctypes.c_uint8 * 16),
+        ("last_random", ctypes.c_uint8 * 32),
+        ("query_indices", ctypes.c_void_p),
+        ("queries", ctypes.c_void_p),
+    ]
+
+
+class PcsProofC(ctypes.Structure):
+    _fields_ = [("fri", FriProofC), ("sumcheck_polys", ctypes.c_void_p)]
+
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I = ctypes.c_int
+_S = ctypes.c_size_t
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "mlh_version": (ctypes.c_char_p, []),
+    "mlh_context_create": (_I, [_I, _P, ctypes.POINTER(_P)]),
+    "mlh_context_destroy": (None, [_P]),
+    "mlh_set_stream": (_I, [_P, _P]),
+    "mlh_synchronize": (_I, [_P]),
+    "mlh_last_error": (ctypes.c_char_p, [_P]),
+    "mlh_malloc": (_I, [_P, _S, ctypes.POINTER(_P)]),
+    "mlh_free": (_I, [_P, _P]),
+    "mlh_memcpy_h2d": (_I, [_P, _P, _P, _S]),
+    "mlh_memcpy_d2h": (_I, [_P, _P, _P, _S]),
+    "mlh_memcpy_d2d": (_I, [_P, _P, _P, _S]),
+    "mlh_pow_2_generator": (_I, [_U32, _P]),
+    "mlh_pow_2_generator_powers": (_I, [_P, _U32, _P]),
+    "mlh_ntt": (_I, [_P, _P, _P, _U32, _P]),
+    "mlh_intt": (_I, [_P, _P, _P, _U32, _P]),
+    "mlh_bit_reverse_permutation": (_I, [_P, _P, _P, _U32]),
+    "mlh_ntt_host": (_I, [_P, _P, _P, _U32, _P, _I]),
+    "mlh_reed_solomon": (_I, [_P, _P, _U32, _P, _P]),
+    "mlh_merkle_layers_bytes": (_U64, [_U64]),
+    "mlh_merkle_commit_pairs": (_I, [_P, _P, _U32, _P, _P]),
+    "mlh_merkle_commit": (_I, [_P, _P, _U64, _U64, _P, _P]),
+    "mlh_merkle_batch_commit": (_I, [_P, _P, _U64, _U32, _U64, _P, _P]),
+    "mlh_fri_fold": (_I, [_P, _P, _U32, _U32, _U32, _P, _P]),
+    "mlh_fri_prover_init": (_I, [_P, _P, _U32, _P, ctypes.POINTER(_P)]),
+    "mlh_fri_prover_fold_step": (_I, [_P, _P, _U32, _P, _P]),
+    "mlh_fri_prover_fold": (_I, [_P, _P, _U32, _P, ctypes.POINTER(_P)]),
+    "mlh_fri_prover_num_trees": (_U32, [_P]),
+    "mlh_fri_prover_roots": (_I, [_P, _P]),
+    "mlh_fri_prover_last_element": (_I, [_P, _P]),
+    "mlh_fri_prover_open_query": (_I, [_P, _P, _U64, _P]),
+    "mlh_fri_prover_destroy": (None, [_P]),
+    "mlh_fri_query_bytes": (_U64, [_U32]),
+    "mlh_fri_prove": (_I, [_P, _P, _U32, _P, ctypes.POINTER(FriProofC)]),
+    "mlh_fri_verify": (_I, [ctypes.POINTER(FriProofC)]),
+    "mlh_transcript_create": (_I, [ctypes.POINTER(_P)]),
+    "mlh_transcript_clone": (_I, [_P, ctypes.POINTER(_P)]),
+    "mlh_transcript_destroy": (None, [_P]),
+    "mlh_transcript_absorb": (_I, [_P, _P, _U64]),
+    "mlh_transcript_random": (_I, [_P, _P]),
+    "mlh_transcript_next_challenge": (_I, [_P, _P]),
+    "mlh_mle_to_coefficient": (_I, [_P, _P, _U32]),
+    "mlh_mle_to_evaluation": (_I, [_P, _P, _U32]),
+    "mlh_eq_table": (_I, [_P, _P, _U32, _P]),
+    "mlh_mle_evaluate": (_I, [_P, _P, _U32, _P, _P]),
+    "mlh_sumcheck_partial_sums": (_I, [_P, _P, _P, _U32, _P]),
+    "mlh_sumcheck_fold": (_I, [_P, _P, _P, _U32, _P]),
+    "mlh_sumcheck_fold_and_sums": (_I, [_P, _P, _P, _U32, _P, _P]),
+    "mlh_sumcheck_prove": (_I, [_P, _P, _P, _U32, _P, _P, _P, _P]),
+    "mlh_pcs_prove": (_I, [_P, _P, _U32, _P, _P, _P, ctypes.POINTER(PcsProofC)]),
+    "mlh_pcs_verify": (_I, [ctypes.POINTER(PcsProofC), _U32, _P, _P, _P]),
+    "mlh_bench_ntt": (_I, [_P, _P, _U32, _U32, ctypes.POINTER(ctypes.c_float)]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libmlhip.so once; raises if it is missing (no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "libmlhip.so not built at %s -- run `python -c 'import __graft_entry__ as g; g.build()'`"
+            % LIB_PATH
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

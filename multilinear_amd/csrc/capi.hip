@@ -1,0 +1,1079 @@
+// C ABI (include/mlhip.h) and the C++ host layer above the gfx950 kernels.
+//
+// This file mirrors the reference's prover-side orchestration:
+//   FriProverData::{init, fold_step, fold, open_query_at}  src/fri/mod.rs:57-175
+//   FriProof::{prove, verify, verify_queries}               src/fri/mod.rs:260-341
+//   SumcheckTables::compute_sumcheck_polynomial(s)          sumcheck.rs:77-202
+//   PCSProof::{prove, verify}                               multilinear_pcs.rs:90-190
+// with every large vector device resident; only roots (32 B), round sums
+// (32 B), the last element and the opened query paths cross PCIe.  The
+// Fiat-Shamir transcript runs on the host (it is a strict sequence of small
+// SHA-256 updates; one host round trip per round).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/mlhip.h"
+#include "field.hpp"
+#include "host_field.hpp"
+#include "host_sha256.hpp"
+#include "merkle.hpp"
+#include "ntt.hpp"
+#include "sha256.hpp"
+#include "sumcheck.hpp"
+
+using namespace mlh;
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct TableKey {
+  u128 base;
+  uint64_t count;
+  u128 scale;
+  bool operator<(const TableKey& o) const {
+    return std::tie(base, count, scale) < std::tie(o.base, o.count, o.scale);
+  }
+};
+
+struct mlh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::map<TableKey, fe*> tables;
+  std::multimap<size_t, void*> pool;  // cached free device blocks
+  std::map<void*, size_t> live;       // pool-owned live blocks
+  fe* partials = nullptr;             // 2 * kMaxRedBlocks
+  fe* small = nullptr;                // 64 elements scratch (sums, points)
+  uint8_t* pinned = nullptr;          // 4 KiB pinned host staging
+  fe* ntt_scratch = nullptr;          // NTT ping-pong buffer (grow-only)
+  size_t ntt_scratch_bytes = 0;
+};
+
+struct mlh_transcript {
+  HostSha256 sha;
+};
+
+static mlh_status fail(mlh_ctx* ctx, mlh_status st, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return st;
+}
+
+#define HIP_TRY(ctx, expr)                                                                \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail((ctx), MLH_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_));  \
+  } while (0)
+
+#define MLH_TRY(expr)              \
+  do {                             \
+    mlh_status s_ = (expr);        \
+    if (s_ != MLH_OK) return s_;   \
+  } while (0)
+
+static fe to_fe(u128 v) {
+  fe r;
+  memcpy(r.w, &v, 16);
+  return r;
+}
+static u128 from_fe(const fe& x) {
+  u128 v;
+  memcpy(&v, x.w, 16);
+  return v;
+}
+
+// pooled device allocation: large per-call buffers are reused across calls
+static mlh_status pool_alloc(mlh_ctx* ctx, size_t bytes, void** out) {
+  bytes = (bytes + 255) & ~(size_t)255;
+  auto it = ctx->pool.lower_bound(bytes);
+  if (it != ctx->pool.end() && it->first <= bytes + bytes / 4) {
+    *out = it->second;
+    ctx->live[it->second] = it->first;
+    ctx->pool.erase(it);
+    return MLH_OK;
+  }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess) {
+    // release cached blocks and retry once
+    for (auto& kv : ctx->pool) (void)hipFree(kv.second);
+    ctx->pool.clear();
+    e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return fail(ctx, MLH_ERR_OOM, "hipMalloc failed");
+  }
+  ctx->live[p] = bytes;
+  *out = p;
+  return MLH_OK;
+}
+static void pool_free(mlh_ctx* ctx, void* p) {
+  if (!p) return;
+  auto it = ctx->live.find(p);
+  if (it == ctx->live.end()) return;
+  ctx->pool.emplace(it->second, p);
+  ctx->live.erase(it);
+}
+
+// RAII helper for pooled buffers
+struct PoolBuf {
+  mlh_ctx* ctx;
+  void* p = nullptr;
+  explicit PoolBuf(mlh_ctx* c) : ctx(c) {}
+  ~PoolBuf() { pool_free(ctx, p); }
+  mlh_status alloc(size_t bytes) { return pool_alloc(ctx, bytes, &p); }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+// table[t] = base^t * scale, t < count, cached per context
+static mlh_status get_table(mlh_ctx* ctx, u128 base, uint64_t count, u128 scale, const fe** out) {
+  TableKey k{base, count, scale};
+  auto it = ctx->tables.find(k);
+  if (it != ctx->tables.end()) {
+    *out = it->second;
+    return MLH_OK;
+  }
+  fe* d = nullptr;
+  HIP_TRY(ctx, hipMalloc(&d, count * sizeof(fe)));
+  HIP_TRY(ctx, launch_pow_table(d, to_fe(base), to_fe(scale), count, ctx->stream));
+  ctx->tables[k] = d;
+  *out = d;
+  return MLH_OK;
+}
+
+static uint64_t hi_count(uint32_t log_n) {
+  const uint64_t N = 1ull << log_n;
+  return N <= 4096 ? 1 : N / 4096;
+}
+
+static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool inverse,
+                                 NttTables* tb) {
+  const uint64_t N = 1ull << log_n;
+  const u128 w = inverse ? h_inv(gen) : gen;
+  const u128 scale = inverse ? h_inv((u128)N) : (u128)1;
+  tb->log_n = log_n;
+  tb->inverse = inverse;
+  tb->scale = to_fe(scale);
+  if (log_n <= 10) {
+    MLH_TRY(get_table(ctx, w, N / 2 ? N / 2 : 1, 1, &tb->tw_small));
+    return MLH_OK;
+  }
+  ntt_plan_radices(log_n, &tb->nradix, tb->logr);
+  for (uint32_t p = 0; p < tb->nradix; ++p) {
+    const uint64_t R = 1ull << tb->logr[p];
+    MLH_TRY(get_table(ctx, h_pow(w, N / R), R / 2, 1, &tb->tw[p]));
+  }
+  MLH_TRY(get_table(ctx, w, 4096, scale, &tb->tlo0));
+  MLH_TRY(get_table(ctx, w, 4096, 1, &tb->tlo));
+  MLH_TRY(get_table(ctx, h_pow(w, 4096), hi_count(log_n), 1, &tb->thi));
+  return MLH_OK;
+}
+
+// gen must have order exactly 2^log_n
+static bool check_generator(u128 gen, uint32_t log_n) {
+  if (gen >= kModulus) return false;
+  if (log_n == 0) return gen == 1;
+  const u128 half = h_pow(gen, (u128)1 << (log_n - 1));
+  return half == kModulus - 1;  // gen^(N/2) = -1  <=>  order exactly N
+}
+
+// Core NTT on device (in may equal out; zero_top: input has N/2 elements).
+static mlh_status ntt_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, u128 gen,
+                           bool inverse, bool zero_top) {
+  NttTables tb;
+  MLH_TRY(get_ntt_tables(ctx, gen, log_n, inverse, &tb));
+  if (log_n <= 10) {
+    const uint64_t N = 1ull << log_n;
+    if (in == out && log_n > 0) {
+      // small kernel reads everything into LDS before writing; in-place is safe
+    }
+    HIP_TRY(ctx, launch_ntt_small(in, out, tb.tw_small, log_n, zero_top ? N / 2 : N, tb.scale,
+                                  inverse, ctx->stream));
+    return MLH_OK;
+  }
+  const size_t need = (size_t)16 << log_n;
+  if (ctx->ntt_scratch_bytes < need) {
+    if (ctx->ntt_scratch) {
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+      HIP_TRY(ctx, hipFree(ctx->ntt_scratch));
+      ctx->ntt_scratch = nullptr;
+      ctx->ntt_scratch_bytes = 0;
+    }
+    HIP_TRY(ctx, hipMalloc(&ctx->ntt_scratch, need));
+    ctx->ntt_scratch_bytes = need;
+  }
+  HIP_TRY(ctx, launch_ntt_passes(in, out, ctx->ntt_scratch, tb, log_n, zero_top, ctx->stream));
+  return MLH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// context / memory API
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* mlh_version(void) { return "mlhip 0.1 (gfx950)"; }
+
+mlh_status mlh_context_create(int device, void* hip_stream, mlh_ctx** out) {
+  if (!out) return MLH_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return MLH_ERR_HIP;
+  if (hipSetDevice(device) != hipSuccess) return MLH_ERR_HIP;
+  std::unique_ptr<mlh_ctx> c(new mlh_ctx());
+  c->device = device;
+  c->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  if (hipMalloc(&c->partials, 2 * kMaxRedBlocks * sizeof(fe)) != hipSuccess) return MLH_ERR_OOM;
+  if (hipMalloc(&c->small, 64 * sizeof(fe)) != hipSuccess) return MLH_ERR_OOM;
+  if (hipHostMalloc(&c->pinned, 4096, 0) != hipSuccess) return MLH_ERR_OOM;
+  *out = c.release();
+  return MLH_OK;
+}
+
+void mlh_context_destroy(mlh_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->tables) (void)hipFree(kv.second);
+  for (auto& kv : ctx->pool) (void)hipFree(kv.second);
+  for (auto& kv : ctx->live) (void)hipFree(kv.first);
+  (void)hipFree(ctx->ntt_scratch);
+  (void)hipFree(ctx->partials);
+  (void)hipFree(ctx->small);
+  (void)hipHostFree(ctx->pinned);
+  delete ctx;
+}
+
+mlh_status mlh_set_stream(mlh_ctx* ctx, void* hip_stream) {
+  if (!ctx) return MLH_ERR_INVALID;
+  ctx->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  return MLH_OK;
+}
+
+mlh_status mlh_synchronize(mlh_ctx* ctx) {
+  if (!ctx) return MLH_ERR_INVALID;
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+
+const char* mlh_last_error(const mlh_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+mlh_status mlh_malloc(mlh_ctx* ctx, size_t bytes, void** dev) {
+  if (!ctx || !dev) return MLH_ERR_INVALID;
+  HIP_TRY(ctx, hipMalloc(dev, bytes ? bytes : 16));
+  return MLH_OK;
+}
+mlh_status mlh_free(mlh_ctx* ctx, void* dev) {
+  if (!ctx) return MLH_ERR_INVALID;
+  HIP_TRY(ctx, hipFree(dev));
+  return MLH_OK;
+}
+mlh_status mlh_memcpy_h2d(mlh_ctx* ctx, void* dev, const void* host, size_t bytes) {
+  if (!ctx) return MLH_ERR_INVALID;
+  HIP_TRY(ctx, hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+mlh_status mlh_memcpy_d2h(mlh_ctx* ctx, void* host, const void* dev, size_t bytes) {
+  if (!ctx) return MLH_ERR_INVALID;
+  HIP_TRY(ctx, hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+mlh_status mlh_memcpy_d2d(mlh_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return MLH_ERR_INVALID;
+  HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  return MLH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// field helpers / NTT
+// ---------------------------------------------------------------------------
+mlh_status mlh_pow_2_generator(uint32_t log_size, uint8_t gen_out[16]) {
+  if (!gen_out || log_size > 40) return MLH_ERR_INVALID;
+  h_store(gen_out, h_pow2_generator(log_size));
+  return MLH_OK;
+}
+
+mlh_status mlh_pow_2_generator_powers(mlh_ctx* ctx, uint32_t log_size, void* dev_out) {
+  if (!ctx || !dev_out || log_size > 40) return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  const u128 g = h_pow2_generator(log_size);
+  const fe *tlo, *thi;
+  MLH_TRY(get_table(ctx, g, 4096, 1, &tlo));
+  MLH_TRY(get_table(ctx, h_pow(g, 4096), hi_count(log_size), 1, &thi));
+  HIP_TRY(ctx, launch_pow_series(reinterpret_cast<fe*>(dev_out), tlo, thi, 1ull << log_size,
+                                 ctx->stream));
+  return MLH_OK;
+}
+
+static mlh_status ntt_entry(mlh_ctx* ctx, const void* in, void* out, uint32_t log_n,
+                            const uint8_t gen[16], bool inverse) {
+  if (!ctx || !in || !out || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_n < 1 || log_n > 32) return fail(ctx, MLH_ERR_NOT_POW2, "The number of coeffs must be a power of 2 (n >= 2)");
+  const u128 g = h_load(gen);
+  if (!check_generator(g, log_n)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != n");
+  return ntt_core(ctx, reinterpret_cast<const fe*>(in), reinterpret_cast<fe*>(out), log_n, g,
+                  inverse, false);
+}
+
+mlh_status mlh_ntt(mlh_ctx* ctx, const void* dev_coeffs, void* dev_evals, uint32_t log_n,
+                   const uint8_t gen[16]) {
+  return ntt_entry(ctx, dev_coeffs, dev_evals, log_n, gen, false);
+}
+
+mlh_status mlh_intt(mlh_ctx* ctx, const void* dev_evals, void* dev_coeffs, uint32_t log_n,
+                    const uint8_t gen[16]) {
+  return ntt_entry(ctx, dev_evals, dev_coeffs, log_n, gen, true);
+}
+
+mlh_status mlh_bit_reverse_permutation(mlh_ctx* ctx, const void* dev_in, void* dev_out,
+                                       uint32_t log_n) {
+  if (!ctx || !dev_in || !dev_out || dev_in == dev_out)
+    return fail(ctx, MLH_ERR_INVALID, "bit_reverse_permutation is out of place");
+  if (log_n > 40) return fail(ctx, MLH_ERR_INVALID, "log_n too large");
+  HIP_TRY(ctx, launch_bitrev(reinterpret_cast<const fe*>(dev_in), reinterpret_cast<fe*>(dev_out),
+                             log_n, ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_ntt_host(mlh_ctx* ctx, const uint8_t* host_in, uint8_t* host_out, uint32_t log_n,
+                        const uint8_t gen[16], int inverse) {
+  if (!ctx || !host_in || !host_out) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  const size_t bytes = (size_t)16 << log_n;
+  PoolBuf buf(ctx);
+  MLH_TRY(buf.alloc(bytes));
+  HIP_TRY(ctx, hipMemcpyAsync(buf.p, host_in, bytes, hipMemcpyHostToDevice, ctx->stream));
+  MLH_TRY(ntt_entry(ctx, buf.p, buf.p, log_n, gen, inverse != 0));
+  HIP_TRY(ctx, hipMemcpyAsync(host_out, buf.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Reed-Solomon / Merkle / fold
+// ---------------------------------------------------------------------------
+mlh_status mlh_reed_solomon(mlh_ctx* ctx, const void* dev_coeffs, uint32_t log_n,
+                            const uint8_t gen[16], void* dev_code) {
+  if (!ctx || !dev_coeffs || !dev_code || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_n > 31) return fail(ctx, MLH_ERR_INVALID, "log_n too large");
+  if (dev_coeffs == dev_code) return fail(ctx, MLH_ERR_INVALID, "reed_solomon is out of place");
+  const uint32_t lc = log_n + MLH_LOG_BLOWUP;
+  const u128 g = h_load(gen);
+  if (!check_generator(g, lc)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != 2n");
+  return ntt_core(ctx, reinterpret_cast<const fe*>(dev_coeffs), reinterpret_cast<fe*>(dev_code),
+                  lc, g, false, true);
+}
+
+uint64_t mlh_merkle_layers_bytes(uint64_t leaves) { return leaves ? (2 * leaves - 1) * 32 : 0; }
+
+static mlh_status read_root(mlh_ctx* ctx, const uint8_t* layers, uint64_t leaves, uint8_t out[32]) {
+  if (!out) return MLH_OK;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, layers + (2 * leaves - 2) * 32, 32,
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(out, ctx->pinned, 32);
+  return MLH_OK;
+}
+
+static bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+mlh_status mlh_merkle_commit_pairs(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                                   void* dev_layers, uint8_t root_out[32]) {
+  if (!ctx || !dev_code || !dev_layers) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_code < 1 || log_code > 40)
+    return fail(ctx, MLH_ERR_NOT_POW2, "Data length must be a power of two");
+  const uint64_t L = 1ull << (log_code - 1);
+  uint8_t* layers = reinterpret_cast<uint8_t*>(dev_layers);
+  HIP_TRY(ctx, launch_leaf_pairs(reinterpret_cast<const fe*>(dev_code), L, layers, ctx->stream));
+  HIP_TRY(ctx, launch_merkle_levels(layers, L, ctx->stream));
+  return read_root(ctx, layers, L, root_out);
+}
+
+mlh_status mlh_merkle_commit(mlh_ctx* ctx, const void* dev_items, uint64_t item_len,
+                             uint64_t count, void* dev_layers, uint8_t root_out[32]) {
+  if (!ctx || !dev_items || !dev_layers) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (!is_pow2(count)) return fail(ctx, MLH_ERR_NOT_POW2, "Data length must be a power of two");
+  uint8_t* layers = reinterpret_cast<uint8_t*>(dev_layers);
+  HIP_TRY(ctx, launch_leaf_bytes(reinterpret_cast<const uint8_t*>(dev_items), item_len, count,
+                                 layers, ctx->stream));
+  HIP_TRY(ctx, launch_merkle_levels(layers, count, ctx->stream));
+  return read_root(ctx, layers, count, root_out);
+}
+
+mlh_status mlh_merkle_batch_commit(mlh_ctx* ctx, const void* dev_items, uint64_t item_len,
+                                   uint32_t m, uint64_t count, void* dev_layers,
+                                   uint8_t root_out[32]) {
+  if (!ctx || !dev_items || !dev_layers) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (m == 0) return fail(ctx, MLH_ERR_INVALID, "Data must not be empty");
+  if (!is_pow2(count))
+    return fail(ctx, MLH_ERR_NOT_POW2, "Each batch length must be a power of two");
+  uint8_t* layers = reinterpret_cast<uint8_t*>(dev_layers);
+  HIP_TRY(ctx, launch_leaf_batch(reinterpret_cast<const uint8_t*>(dev_items), item_len,
+                                 item_len * count, m, count, layers, ctx->stream));
+  HIP_TRY(ctx, launch_merkle_levels(layers, count, ctx->stream));
+  return read_root(ctx, layers, count, root_out);
+}
+
+static mlh_status fold_tables(mlh_ctx* ctx, uint32_t log_domain, const fe** tlo, const fe** thi) {
+  const u128 ginv = h_inv(h_pow2_generator(log_domain));
+  MLH_TRY(get_table(ctx, ginv, 4096, 1, tlo));
+  MLH_TRY(get_table(ctx, h_pow(ginv, 4096), hi_count(log_domain), 1, thi));
+  return MLH_OK;
+}
+
+mlh_status mlh_fri_fold(mlh_ctx* ctx, const void* dev_layer, uint32_t log_layer, uint32_t k,
+                        uint32_t log_domain, const uint8_t r[16], void* dev_next) {
+  if (!ctx || !dev_layer || !dev_next || !r) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_layer < 1 || log_domain > 40 || log_layer + k != log_domain)
+    return fail(ctx, MLH_ERR_INVALID, "layer size must be 2^(log_domain - k)");
+  const fe *tlo, *thi;
+  MLH_TRY(fold_tables(ctx, log_domain, &tlo, &thi));
+  HIP_TRY(ctx, launch_fri_fold(reinterpret_cast<const fe*>(dev_layer), 1ull << log_layer,
+                               reinterpret_cast<fe*>(dev_next), to_fe(h_load(r)), tlo, thi, k,
+                               1ull << log_domain, ctx->stream));
+  return MLH_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// FRI prover (FriProverData)
+// ---------------------------------------------------------------------------
+struct FriLayer {
+  const fe* values = nullptr;  // 2^log_n values (pairs i, i + n/2)
+  void* owned_values = nullptr;
+  uint8_t* tree = nullptr;  // 2L-1 digests, L = n/2
+  uint32_t log_n = 0;
+  uint8_t root[32];
+};
+
+struct mlh_fri_prover {
+  mlh_ctx* ctx;
+  uint32_t log_code;
+  std::vector<FriLayer> layers;
+  bool has_last = false;
+  uint8_t last[16];
+  ~mlh_fri_prover() {
+    for (auto& l : layers) {
+      pool_free(ctx, l.owned_values);
+      pool_free(ctx, l.tree);
+    }
+  }
+};
+
+extern "C" {
+
+mlh_status mlh_fri_prover_init(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                               mlh_transcript* tr, mlh_fri_prover** out) {
+  if (!ctx || !dev_code || !tr || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_code < 1 || log_code > 40)
+    return fail(ctx, MLH_ERR_NOT_POW2, "Input size must be a power of two");
+  std::unique_ptr<mlh_fri_prover> p(new mlh_fri_prover());
+  p->ctx = ctx;
+  p->log_code = log_code;
+  FriLayer l0;
+  l0.values = reinterpret_cast<const fe*>(dev_code);
+  l0.log_n = log_code;
+  const uint64_t L = 1ull << (log_code - 1);
+  void* tree;
+  MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
+  l0.tree = reinterpret_cast<uint8_t*>(tree);
+  p->layers.push_back(l0);
+  MLH_TRY(mlh_merkle_commit_pairs(ctx, dev_code, log_code, tree, p->layers[0].root));
+  mlh_transcript_absorb(tr, p->layers[0].root, 32);
+  *out = p.release();
+  return MLH_OK;
+}
+
+mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
+                                    const uint8_t r[16], mlh_transcript* tr) {
+  if (!ctx || !p || !r || !tr) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  const FriLayer& cur = p->layers.back();
+  const uint32_t log_n = cur.log_n;  // n = 2 * pairs
+  const uint64_t blowup = 1ull << MLH_LOG_BLOWUP;
+  if ((1ull << log_n) <= blowup) return MLH_OK;  // fri/mod.rs:83-85
+  if (p->has_last) return MLH_OK;
+  const uint64_t half_n = 1ull << (log_n - 1);
+  if (k + log_n != p->log_code) return fail(ctx, MLH_ERR_INVALID, "fold index k out of sequence");
+  const fe *tlo, *thi;
+  MLH_TRY(fold_tables(ctx, p->log_code, &tlo, &thi));
+  const fe rr = to_fe(h_load(r));
+  FriLayer nx;
+  nx.log_n = log_n - 1;
+  void* vals;
+  MLH_TRY(pool_alloc(ctx, half_n * sizeof(fe), &vals));
+  nx.owned_values = vals;
+  nx.values = reinterpret_cast<const fe*>(vals);
+  if (half_n == blowup) {  // fri/mod.rs:116-126
+    HIP_TRY(ctx, launch_fri_fold(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), rr, tlo,
+                                 thi, k, 1ull << p->log_code, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, vals, 32, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    pool_free(ctx, vals);
+    if (memcmp(ctx->pinned, ctx->pinned + 16, 16) != 0)
+      return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
+    memcpy(p->last, ctx->pinned, 16);
+    p->has_last = true;
+    mlh_transcript_absorb(tr, p->last, 16);
+    return MLH_OK;
+  }
+  const uint64_t L = half_n / 2;
+  void* tree;
+  MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
+  nx.tree = reinterpret_cast<uint8_t*>(tree);
+  HIP_TRY(ctx, launch_fri_fold_leaves(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
+                                      nx.tree, rr, tlo, thi, k, 1ull << p->log_code,
+                                      ctx->stream));
+  HIP_TRY(ctx, launch_merkle_levels(nx.tree, L, ctx->stream));
+  MLH_TRY(read_root(ctx, nx.tree, L, nx.root));
+  p->layers.push_back(nx);
+  mlh_transcript_absorb(tr, p->layers.back().root, 32);
+  return MLH_OK;
+}
+
+mlh_status mlh_fri_prover_fold(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                               mlh_transcript* tr, mlh_fri_prover** out) {
+  mlh_fri_prover* p = nullptr;
+  MLH_TRY(mlh_fri_prover_init(ctx, dev_code, log_code, tr, &p));
+  const uint32_t steps = log_code - MLH_LOG_BLOWUP;
+  for (uint32_t k = 0; k < steps; ++k) {
+    uint8_t r[16];
+    mlh_transcript_next_challenge(tr, r);
+    mlh_status s = mlh_fri_prover_fold_step(ctx, p, k, r, tr);
+    if (s != MLH_OK) {
+      mlh_fri_prover_destroy(p);
+      return s;
+    }
+  }
+  if (!p->has_last) {
+    mlh_fri_prover_destroy(p);
+    return fail(ctx, MLH_ERR_INVALID, "fold produced no last element (log_code < 2)");
+  }
+  *out = p;
+  return MLH_OK;
+}
+
+uint32_t mlh_fri_prover_num_trees(const mlh_fri_prover* p) {
+  return p ? (uint32_t)p->layers.size() : 0;
+}
+
+mlh_status mlh_fri_prover_roots(const mlh_fri_prover* p, uint8_t* roots_out) {
+  if (!p || !roots_out) return MLH_ERR_INVALID;
+  for (size_t i = 0; i < p->layers.size(); ++i) memcpy(roots_out + 32 * i, p->layers[i].root, 32);
+  return MLH_OK;
+}
+
+mlh_status mlh_fri_prover_last_element(const mlh_fri_prover* p, uint8_t out[16]) {
+  if (!p || !out || !p->has_last) return MLH_ERR_INVALID;
+  memcpy(out, p->last, 16);
+  return MLH_OK;
+}
+
+void mlh_fri_prover_destroy(mlh_fri_prover* p) { delete p; }
+
+uint64_t mlh_fri_query_bytes(uint32_t log_code) {
+  if (log_code < 2) return 0;
+  uint64_t items = 0;
+  for (uint32_t t = 0; t + 1 < log_code; ++t) items += 1 + (log_code - 1 - t);
+  return items * 32;
+}
+
+}  // extern "C"
+
+// Gather opened query records from the device-resident layers/trees.
+struct QueryTree {
+  const fe* values;
+  const uint8_t* tree;
+  uint32_t log_n;  // layer values
+};
+
+__global__ void gather_queries_kernel(const QueryTree* __restrict__ trees, uint32_t ntrees,
+                                      const uint64_t* __restrict__ indices, uint32_t nq,
+                                      uint64_t qbytes, uint8_t* __restrict__ out) {
+  const uint32_t q = blockIdx.x;
+  if (q >= nq) return;
+  // record offsets per tree
+  uint64_t off = 0;
+  for (uint32_t t = 0; t < ntrees; ++t) {
+    const QueryTree T = trees[t];
+    const uint64_t half = 1ull << (T.log_n - 1);  // leaves
+    const uint64_t idx = indices[q] % half;        // fri/mod.rs:169-170
+    const uint32_t depth = T.log_n - 1;
+    uint8_t* rec = out + q * qbytes + off;
+    if (threadIdx.x == 0) {
+      fe_store(reinterpret_cast<fe*>(rec), fe_load(T.values + idx));
+      fe_store(reinterpret_cast<fe*>(rec + 16), fe_load(T.values + idx + half));
+    }
+    // siblings: level l node (idx >> l) ^ 1, level l starts at sum_{i<l} half>>i
+    for (uint32_t l = threadIdx.x; l < depth; l += blockDim.x) {
+      uint64_t lvl_off = 0;
+      for (uint32_t i = 0; i < l; ++i) lvl_off += half >> i;
+      const uint64_t sib = ((idx >> l) ^ 1ull);
+      const uint4* src = reinterpret_cast<const uint4*>(T.tree + (lvl_off + sib) * 32);
+      uint4* dst = reinterpret_cast<uint4*>(rec + 32 + (uint64_t)l * 32);
+      dst[0] = src[0];
+      dst[1] = src[1];
+    }
+    off += 32ull * (1 + depth);
+  }
+}
+
+static mlh_status gather_queries(mlh_ctx* ctx, const mlh_fri_prover* p, const uint64_t* idx,
+                                 uint32_t nq, uint8_t* host_out) {
+  const uint32_t nt = (uint32_t)p->layers.size();
+  const uint64_t qbytes = mlh_fri_query_bytes(p->log_code);
+  std::vector<QueryTree> qt(nt);
+  for (uint32_t t = 0; t < nt; ++t) qt[t] = QueryTree{p->layers[t].values, p->layers[t].tree, p->layers[t].log_n};
+  PoolBuf dtrees(ctx), didx(ctx), dout(ctx);
+  MLH_TRY(dtrees.alloc(nt * sizeof(QueryTree)));
+  MLH_TRY(didx.alloc(nq * sizeof(uint64_t)));
+  MLH_TRY(dout.alloc(nq * qbytes));
+  HIP_TRY(ctx, hipMemcpyAsync(dtrees.p, qt.data(), nt * sizeof(QueryTree), hipMemcpyHostToDevice,
+                              ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(didx.p, idx, nq * sizeof(uint64_t), hipMemcpyHostToDevice,
+                              ctx->stream));
+  hipLaunchKernelGGL(gather_queries_kernel, dim3(nq), dim3(64), 0, ctx->stream,
+                     dtrees.as<QueryTree>(), nt, didx.as<uint64_t>(), nq, qbytes,
+                     dout.as<uint8_t>());
+  HIP_TRY(ctx, hipGetLastError());
+  HIP_TRY(ctx, hipMemcpyAsync(host_out, dout.p, nq * qbytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+
+// FriProof::prove tail (fri/mod.rs:266-284): query indices from the
+// transcript, openings, last_random.
+static mlh_status fri_queries(mlh_ctx* ctx, mlh_fri_prover* p, mlh_transcript* tr,
+                              mlh_fri_proof* proof) {
+  const uint64_t domain = 1ull << p->log_code;
+  proof->log_code = p->log_code;
+  proof->num_trees = (uint32_t)p->layers.size();
+  proof->num_queries = MLH_NUM_QUERIES;
+  std::vector<uint64_t> idx(MLH_NUM_QUERIES);
+  for (int q = 0; q < MLH_NUM_QUERIES; ++q) {
+    uint8_t rnd[32];
+    mlh_transcript_random(tr, rnd);
+    uint64_t u;
+    memcpy(&u, rnd, 8);
+    idx[q] = u % (domain / 2);
+    uint8_t le[8];
+    memcpy(le, &idx[q], 8);
+    mlh_transcript_absorb(tr, le, 8);
+  }
+  if (proof->query_indices) memcpy(proof->query_indices, idx.data(), idx.size() * 8);
+  if (proof->commitments) mlh_fri_prover_roots(p, proof->commitments);
+  memcpy(proof->last_elem, p->last, 16);
+  mlh_transcript_random(tr, proof->last_random);
+  if (proof->queries) MLH_TRY(gather_queries(ctx, p, idx.data(), MLH_NUM_QUERIES, proof->queries));
+  return MLH_OK;
+}
+
+extern "C" {
+
+mlh_status mlh_fri_prover_open_query(mlh_ctx* ctx, const mlh_fri_prover* p, uint64_t index,
+                                     uint8_t* out) {
+  if (!ctx || !p || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (index >= (1ull << (p->log_code - 1))) return fail(ctx, MLH_ERR_INVALID, "index out of bounds");
+  return gather_queries(ctx, p, &index, 1, out);
+}
+
+mlh_status mlh_fri_prove(mlh_ctx* ctx, const void* dev_code, uint32_t log_code, mlh_transcript* tr,
+                         mlh_fri_proof* proof) {
+  if (!ctx || !dev_code || !tr || !proof) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  mlh_fri_prover* p = nullptr;
+  MLH_TRY(mlh_fri_prover_fold(ctx, dev_code, log_code, tr, &p));
+  mlh_status s = fri_queries(ctx, p, tr, proof);
+  mlh_fri_prover_destroy(p);
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// transcript
+// ---------------------------------------------------------------------------
+mlh_status mlh_transcript_create(mlh_transcript** out) {
+  if (!out) return MLH_ERR_INVALID;
+  *out = new mlh_transcript();
+  return MLH_OK;
+}
+mlh_status mlh_transcript_clone(const mlh_transcript* t, mlh_transcript** out) {
+  if (!t || !out) return MLH_ERR_INVALID;
+  *out = new mlh_transcript(*t);
+  return MLH_OK;
+}
+void mlh_transcript_destroy(mlh_transcript* t) { delete t; }
+mlh_status mlh_transcript_absorb(mlh_transcript* t, const uint8_t* bytes, uint64_t len) {
+  if (!t || (!bytes && len)) return MLH_ERR_INVALID;
+  t->sha.update(bytes, (size_t)len);
+  return MLH_OK;
+}
+mlh_status mlh_transcript_random(const mlh_transcript* t, uint8_t out[32]) {
+  if (!t || !out) return MLH_ERR_INVALID;
+  t->sha.digest(out);
+  return MLH_OK;
+}
+mlh_status mlh_transcript_next_challenge(mlh_transcript* t, uint8_t out[16]) {
+  if (!t || !out) return MLH_ERR_INVALID;
+  uint8_t d[32];
+  t->sha.digest(d);
+  h_store(out, h_reduce_once(h_load(d)));  // Field128::from(u128), field.rs:138-142
+  return MLH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// multilinear / sumcheck
+// ---------------------------------------------------------------------------
+mlh_status mlh_mle_to_coefficient(mlh_ctx* ctx, void* dev_evals, uint32_t log_n) {
+  if (!ctx || !dev_evals || log_n > 40) return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  HIP_TRY(ctx, launch_mobius(reinterpret_cast<fe*>(dev_evals), log_n, false, ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_mle_to_evaluation(mlh_ctx* ctx, void* dev_coeffs, uint32_t log_n) {
+  if (!ctx || !dev_coeffs || log_n > 40) return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  HIP_TRY(ctx, launch_mobius(reinterpret_cast<fe*>(dev_coeffs), log_n, true, ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_eq_table(mlh_ctx* ctx, const uint8_t* host_points, uint32_t n, void* dev_out) {
+  if (!ctx || !dev_out || (n && !host_points) || n > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  PoolBuf pts(ctx), scratch(ctx);
+  MLH_TRY(pts.alloc((n ? n : 1) * sizeof(fe)));
+  const uint32_t a = n / 2, b = n - a;
+  MLH_TRY(scratch.alloc(((1ull << a) + (1ull << b)) * sizeof(fe)));
+  if (n) HIP_TRY(ctx, hipMemcpyAsync(pts.p, host_points, n * 16ull, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, launch_eq_table(pts.as<fe>(), n, scratch.as<fe>(), reinterpret_cast<fe*>(dev_out),
+                               ctx->stream));
+  // pts/scratch return to the pool: keep them alive until the kernels ran
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+
+static mlh_status read_pair(mlh_ctx* ctx, const fe* dev2, uint8_t out[32]) {
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, dev2, 32, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(out, ctx->pinned, 32);
+  return MLH_OK;
+}
+
+mlh_status mlh_mle_evaluate(mlh_ctx* ctx, const void* dev_evals, uint32_t n,
+                            const uint8_t* host_args, uint8_t out[16]) {
+  if (!ctx || !dev_evals || !out || n > 40) return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  PoolBuf eq(ctx);
+  MLH_TRY(eq.alloc((16ull << n)));
+  MLH_TRY(mlh_eq_table(ctx, host_args, n, eq.p));
+  HIP_TRY(ctx, launch_dot(reinterpret_cast<const fe*>(dev_evals), eq.as<fe>(), 1ull << n,
+                          ctx->partials, ctx->small, ctx->stream));
+  uint8_t pair[32];
+  MLH_TRY(read_pair(ctx, ctx->small, pair));
+  memcpy(out, pair, 16);
+  return MLH_OK;
+}
+
+mlh_status mlh_sumcheck_partial_sums(mlh_ctx* ctx, const void* dev_matrix, const void* dev_delta,
+                                     uint32_t log_height, uint8_t out[32]) {
+  if (!ctx || !dev_matrix || !dev_delta || !out || log_height < 1 || log_height > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  HIP_TRY(ctx, launch_sums(reinterpret_cast<const fe*>(dev_matrix),
+                           reinterpret_cast<const fe*>(dev_delta), 1ull << (log_height - 1),
+                           ctx->partials, ctx->small, ctx->stream));
+  return read_pair(ctx, ctx->small, out);
+}
+
+mlh_status mlh_sumcheck_fold(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, uint32_t log_height,
+                             const uint8_t r[16]) {
+  if (!ctx || !dev_matrix || !dev_delta || !r || log_height < 1 || log_height > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  HIP_TRY(ctx, launch_fold(reinterpret_cast<fe*>(dev_matrix), reinterpret_cast<fe*>(dev_delta),
+                           1ull << log_height, to_fe(h_load(r)), ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_sumcheck_fold_and_sums(mlh_ctx* ctx, void* dev_matrix, void* dev_delta,
+                                      uint32_t log_height, const uint8_t r[16], uint8_t out[32]) {
+  if (!ctx || !dev_matrix || !dev_delta || !r || !out || log_height < 2 || log_height > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  HIP_TRY(ctx, launch_fold_sums(reinterpret_cast<fe*>(dev_matrix), reinterpret_cast<fe*>(dev_delta),
+                                1ull << log_height, to_fe(h_load(r)), ctx->partials, ctx->small,
+                                ctx->stream));
+  return read_pair(ctx, ctx->small, out);
+}
+
+}  // extern "C"
+
+// One sumcheck round on the host given the device sums: interpolation on
+// x = 0,1,2 (polynomials.rs:51-87, closed form), absorb c1, c2, challenge,
+// previous_sum = p(r)  (sumcheck.rs:188-199).
+static void sumcheck_round_host(const uint8_t sums[32], u128* prev, mlh_transcript* tr,
+                                uint8_t poly_out[32], u128* r_out) {
+  const u128 s1 = h_load(sums), s2 = h_load(sums + 16);
+  const u128 e0 = h_sub(*prev, s1);
+  const u128 inv2 = h_inv(2);
+  const u128 c2 = h_mul(h_add(h_sub(s2, h_add(s1, s1)), e0), inv2);
+  const u128 c1 = h_sub(h_sub(s1, e0), c2);
+  h_store(poly_out, c1);
+  h_store(poly_out + 16, c2);
+  mlh_transcript_absorb(tr, poly_out, 16);
+  mlh_transcript_absorb(tr, poly_out + 16, 16);
+  uint8_t rb[16];
+  mlh_transcript_next_challenge(tr, rb);
+  const u128 r = h_load(rb);
+  *prev = h_add(e0, h_mul(r, h_add(c1, h_mul(c2, r))));
+  *r_out = r;
+}
+
+extern "C" {
+
+mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, uint32_t log_height,
+                              const uint8_t sum[16], mlh_transcript* tr, uint8_t* polys_out,
+                              uint8_t* rs_out) {
+  if (!ctx || !dev_matrix || !dev_delta || !sum || !tr || log_height < 1 || log_height > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  u128 prev = h_load(sum);
+  uint8_t sums[32];
+  MLH_TRY(mlh_sumcheck_partial_sums(ctx, dev_matrix, dev_delta, log_height, sums));
+  for (uint32_t k = 0; k < log_height; ++k) {
+    uint8_t poly[32];
+    u128 r;
+    sumcheck_round_host(sums, &prev, tr, poly, &r);
+    if (polys_out) memcpy(polys_out + 32 * k, poly, 32);
+    uint8_t rb[16];
+    h_store(rb, r);
+    if (rs_out) memcpy(rs_out + 16 * k, rb, 16);
+    const uint32_t lh = log_height - k;
+    if (lh >= 2) {
+      MLH_TRY(mlh_sumcheck_fold_and_sums(ctx, dev_matrix, dev_delta, lh, rb, sums));
+    } else {
+      MLH_TRY(mlh_sumcheck_fold(ctx, dev_matrix, dev_delta, lh, rb));
+    }
+  }
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// multilinear PCS
+// ---------------------------------------------------------------------------
+mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
+                         const uint8_t* host_inputs, const uint8_t output[16], mlh_transcript* tr,
+                         mlh_pcs_proof* proof) {
+  if (!ctx || !dev_evals || !output || !tr || !proof || (n_vars && !host_inputs))
+    return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (n_vars < 1 || n_vars > 36) return fail(ctx, MLH_ERR_INVALID, "n_vars out of range");
+  const uint32_t log_domain = n_vars + MLH_LOG_BLOWUP;
+  const uint64_t n = 1ull << n_vars;
+  const u128 gen = h_pow2_generator(log_domain);  // gen_pows[1] (multilinear_pcs.rs:103-104)
+  uint8_t genb[16];
+  h_store(genb, gen);
+  PoolBuf coeffs(ctx), brev(ctx), code(ctx), matrix(ctx), delta(ctx);
+  MLH_TRY(coeffs.alloc(n * 16));
+  MLH_TRY(brev.alloc(n * 16));
+  MLH_TRY(code.alloc(2 * n * 16));
+  MLH_TRY(matrix.alloc(n * 16));
+  MLH_TRY(delta.alloc(n * 16));
+  // to_coefficient (:107), bit reverse (:109), reed_solomon (:112)
+  HIP_TRY(ctx, hipMemcpyAsync(coeffs.p, dev_evals, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
+  MLH_TRY(mlh_mle_to_coefficient(ctx, coeffs.p, n_vars));
+  MLH_TRY(mlh_bit_reverse_permutation(ctx, coeffs.p, brev.p, n_vars));
+  MLH_TRY(mlh_reed_solomon(ctx, brev.p, n_vars, genb, code.p));
+  // PCSProverData::init (:28-42): FRI init + sumcheck tables
+  mlh_fri_prover* fp = nullptr;
+  MLH_TRY(mlh_fri_prover_init(ctx, code.p, log_domain, tr, &fp));
+  std::unique_ptr<mlh_fri_prover, void (*)(mlh_fri_prover*)> guard(fp, mlh_fri_prover_destroy);
+  HIP_TRY(ctx, hipMemcpyAsync(matrix.p, dev_evals, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
+  MLH_TRY(mlh_eq_table(ctx, host_inputs, n_vars, delta.p));
+  // PCSProverData::fold loop (:57-75)
+  u128 prev = h_load(output);
+  uint8_t sums[32];
+  MLH_TRY(mlh_sumcheck_partial_sums(ctx, matrix.p, delta.p, n_vars, sums));
+  for (uint32_t k = 0; k < n_vars; ++k) {
+    uint8_t poly[32];
+    u128 r;
+    sumcheck_round_host(sums, &prev, tr, poly, &r);
+    if (proof->sumcheck_polys) memcpy(proof->sumcheck_polys + 32 * k, poly, 32);
+    uint8_t rb[16];
+    h_store(rb, r);
+    const uint32_t lh = n_vars - k;
+    if (lh >= 2) {
+      MLH_TRY(mlh_sumcheck_fold_and_sums(ctx, matrix.p, delta.p, lh, rb, sums));
+    } else {
+      MLH_TRY(mlh_sumcheck_fold(ctx, matrix.p, delta.p, lh, rb));
+    }
+    MLH_TRY(mlh_fri_prover_fold_step(ctx, fp, k, rb, tr));
+  }
+  if (!fp->has_last) return fail(ctx, MLH_ERR_INVALID, "no last element");
+  MLH_TRY(fri_queries(ctx, fp, tr, &proof->fri));
+  return MLH_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// host verifiers (fri/mod.rs:184-340, multilinear_pcs.rs:138-190)
+// ---------------------------------------------------------------------------
+static void sha_pair(const uint8_t* a, const uint8_t* b, uint8_t out[32]) {
+  HostSha256 s;
+  s.update(a, 32);
+  s.update(b, 32);
+  s.digest(out);
+}
+
+// MerkleInclusionPath::verify (merkle_tree/mod.rs:216-253); directions from index bits.
+static bool verify_path(const uint8_t* value32, const uint8_t* sibs, uint32_t depth,
+                        const uint8_t root[32], uint64_t index) {
+  uint8_t h[32];
+  HostSha256 s;
+  s.update(value32, 32);
+  s.digest(h);
+  for (uint32_t l = 0; l < depth; ++l) {
+    uint8_t nh[32];
+    if ((index >> l) & 1)
+      sha_pair(sibs + 32 * l, h, nh);  // Direction::Left
+    else
+      sha_pair(h, sibs + 32 * l, nh);  // Direction::Right
+    memcpy(h, nh, 32);
+  }
+  return memcmp(h, root, 32) == 0;
+}
+
+static mlh_status fri_verify_queries(const mlh_fri_proof* pf, mlh_transcript* tr,
+                                     const std::vector<u128>& rs) {
+  const uint32_t L = pf->log_code;
+  const uint64_t domain = 1ull << L;
+  const u128 gen = h_pow2_generator(L);
+  const uint64_t qbytes = mlh_fri_query_bytes(L);
+  const u128 inv2 = h_inv(2);
+  const u128 last = h_load(pf->last_elem);
+  for (uint32_t q = 0; q < pf->num_queries; ++q) {
+    uint8_t rnd[32];
+    mlh_transcript_random(tr, rnd);
+    uint64_t u;
+    memcpy(&u, rnd, 8);
+    const uint64_t index = u % (domain / 2);
+    uint8_t le[8];
+    memcpy(le, &index, 8);
+    mlh_transcript_absorb(tr, le, 8);
+    if (pf->query_indices && pf->query_indices[q] != index) return MLH_ERR_VERIFY;
+    const uint8_t* rec = pf->queries + q * qbytes;
+    uint64_t cur_n = domain / 2, cur_idx = index;
+    u128 cur_gen = gen;
+    uint64_t off = 0;
+    for (uint32_t t = 0; t < pf->num_trees; ++t) {
+      const uint32_t depth = L - 1 - t;
+      const uint8_t* val = rec + off;
+      if (!verify_path(val, val + 32, depth, pf->commitments + 32 * t, cur_idx)) return MLH_ERR_VERIFY;
+      const u128 v = h_load(val), mv = h_load(val + 16);
+      const u128 gp = h_pow(cur_gen, cur_idx);
+      const u128 even = h_mul(h_add(v, mv), inv2);
+      const u128 odd = h_mul(h_sub(v, mv), h_inv(h_mul(2, gp)));
+      const u128 folded = h_add(even, h_mul(rs[t], odd));
+      if (t + 1 == pf->num_trees) {
+        if (folded != last) return MLH_ERR_VERIFY;
+        break;
+      }
+      const uint64_t nidx = cur_idx % (cur_n / 2);
+      const uint8_t* nval = rec + off + 32ull * (1 + depth);
+      const u128 nv = nidx == cur_idx ? h_load(nval) : h_load(nval + 16);
+      if (nv != folded) return MLH_ERR_VERIFY;
+      cur_gen = h_mul(cur_gen, cur_gen);
+      cur_n /= 2;
+      cur_idx = nidx;
+      off += 32ull * (1 + depth);
+    }
+  }
+  uint8_t lr[32];
+  mlh_transcript_random(tr, lr);
+  return memcmp(lr, pf->last_random, 32) == 0 ? MLH_OK : MLH_ERR_VERIFY;
+}
+
+extern "C" {
+
+mlh_status mlh_fri_verify(const mlh_fri_proof* pf) {
+  if (!pf || !pf->commitments || !pf->queries) return MLH_ERR_INVALID;
+  if (pf->num_queries != MLH_NUM_QUERIES) return MLH_ERR_VERIFY;
+  if (pf->num_trees + MLH_LOG_BLOWUP != pf->log_code) return MLH_ERR_VERIFY;
+  mlh_transcript tr;
+  std::vector<u128> rs;
+  for (uint32_t t = 0; t < pf->num_trees; ++t) {
+    mlh_transcript_absorb(&tr, pf->commitments + 32 * t, 32);
+    uint8_t r[16];
+    mlh_transcript_next_challenge(&tr, r);
+    rs.push_back(h_load(r));
+  }
+  mlh_transcript_absorb(&tr, pf->last_elem, 16);
+  return fri_verify_queries(pf, &tr, rs);
+}
+
+mlh_status mlh_pcs_verify(const mlh_pcs_proof* pf, uint32_t n_vars, const uint8_t* inputs,
+                          const uint8_t output[16], mlh_transcript* tr) {
+  if (!pf || !tr || !output || !pf->sumcheck_polys || (n_vars && !inputs)) return MLH_ERR_INVALID;
+  const mlh_fri_proof* fp = &pf->fri;
+  if (fp->num_queries != MLH_NUM_QUERIES) return MLH_ERR_VERIFY;
+  if (fp->num_trees != n_vars) return MLH_ERR_VERIFY;
+  std::vector<u128> rs;
+  for (uint32_t k = 0; k < n_vars; ++k) {
+    mlh_transcript_absorb(tr, fp->commitments + 32 * k, 32);
+    mlh_transcript_absorb(tr, pf->sumcheck_polys + 32 * k, 32);
+    uint8_t r[16];
+    mlh_transcript_next_challenge(tr, r);
+    rs.push_back(h_load(r));
+  }
+  mlh_transcript_absorb(tr, fp->last_elem, 16);
+  // SumcheckPolynomial::to_polynomial chain (sumcheck.rs:269-276)
+  const u128 inv2 = h_inv(2);
+  auto to_poly = [&](uint32_t k, u128 s, u128 c[3]) {
+    c[1] = h_load(pf->sumcheck_polys + 32 * k);
+    c[2] = h_load(pf->sumcheck_polys + 32 * k + 16);
+    c[0] = h_mul(h_sub(s, h_add(c[1], c[2])), inv2);
+  };
+  auto eval = [&](const u128 c[3], u128 x) { return h_add(c[0], h_mul(x, h_add(c[1], h_mul(c[2], x)))); };
+  u128 c[3];
+  to_poly(0, h_load(output), c);
+  for (uint32_t k = 1; k < n_vars; ++k) {
+    const u128 v = eval(c, rs[k - 1]);
+    to_poly(k, v, c);
+  }
+  const u128 r = rs[n_vars - 1];
+  // Delta::evaluate (evaluation.rs:75-91)
+  u128 delta = 1;
+  for (uint32_t i = 0; i < n_vars; ++i) {
+    const u128 a = h_load(inputs + 16 * i), b = rs[i];
+    delta = h_mul(delta, h_add(h_mul(a, b), h_mul(h_sub(1, a), h_sub(1, b))));
+  }
+  if (h_mul(delta, h_load(fp->last_elem)) != eval(c, r)) return MLH_ERR_VERIFY;
+  return fri_verify_queries(fp, tr, rs);
+}
+
+// ---------------------------------------------------------------------------
+// bench helper
+// ---------------------------------------------------------------------------
+mlh_status mlh_bench_ntt(mlh_ctx* ctx, void* dev_buf, uint32_t log_n, uint32_t iters,
+                         float* ms_out) {
+  if (!ctx || !dev_buf || !ms_out || iters == 0) return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  uint8_t gen[16];
+  h_store(gen, h_pow2_generator(log_n));
+  MLH_TRY(mlh_ntt(ctx, dev_buf, dev_buf, log_n, gen));  // warm the table cache
+  hipEvent_t a, b;
+  HIP_TRY(ctx, hipEventCreate(&a));
+  HIP_TRY(ctx, hipEventCreate(&b));
+  HIP_TRY(ctx, hipEventRecord(a, ctx->stream));
+  for (uint32_t i = 0; i < iters; ++i) MLH_TRY(mlh_ntt(ctx, dev_buf, dev_buf, log_n, gen));
+  HIP_TRY(ctx, hipEventRecord(b, ctx->stream));
+  HIP_TRY(ctx, hipEventSynchronize(b));
+  float ms = 0;
+  HIP_TRY(ctx, hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  *ms_out = ms / iters;
+  return MLH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,221 @@
+// Device arithmetic over F_M, M = 2^128 - 45*2^40 + 1 (the `field.rs` modulus).
+//
+// Reference: src/field.rs:31 (Field128 wraps winter-math f128 BaseElement),
+// src/ntt/mod.rs:34-36 (modulus).  winter-math keeps elements canonical
+// (value < M) and Field128::as_ref exposes the raw little-endian u128, so the
+// device keeps exactly that representation in HBM: 16 bytes per element, four
+// little-endian u32 limbs, always canonical.  Any mathematically correct
+// arithmetic is then bit-identical to the reference's.
+//
+// gfx950 notes: there is no 64x64 multiplier; the 128x128 product is 16
+// v_mad_u64_u32 (32x32+64 -> 64) and the reduction uses the special form
+//   2^128 = C (mod M),  C = 45*2^40 - 1 = 0x2CFF_FFFFFFFF
+// so H*C = H*0x2D00*2^32 - H  (four small-constant mads, no second wide product).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mlh {
+
+struct __attribute__((aligned(16))) fe {
+  uint32_t w[4];
+};
+
+// 0x2D00 * 2^32 - 1 = C
+constexpr uint32_t kC0 = 0xFFFFFFFFu;
+constexpr uint32_t kC1 = 0x00002CFFu;
+constexpr uint32_t kCmul = 0x2D00u;  // C = kCmul*2^32 - 1
+// M = 0xFFFFFFFF_FFFFFFFF_FFFFD300_00000001
+constexpr uint32_t kM0 = 0x00000001u;
+constexpr uint32_t kM1 = 0xFFFFD300u;
+constexpr uint32_t kM2 = 0xFFFFFFFFu;
+constexpr uint32_t kM3 = 0xFFFFFFFFu;
+
+__device__ __forceinline__ fe fe_zero() { return fe{{0u, 0u, 0u, 0u}}; }
+__device__ __forceinline__ fe fe_one() { return fe{{1u, 0u, 0u, 0u}}; }
+
+__device__ __forceinline__ bool fe_eq(const fe& a, const fe& b) {
+  return ((a.w[0] ^ b.w[0]) | (a.w[1] ^ b.w[1]) | (a.w[2] ^ b.w[2]) | (a.w[3] ^ b.w[3])) == 0u;
+}
+
+__device__ __forceinline__ uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  return __builtin_addc(a, b, cin, cout);
+}
+__device__ __forceinline__ uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  return __builtin_subc(a, b, bin, bout);
+}
+
+// x + C, returning the carry out of bit 128.
+__device__ __forceinline__ fe add_c(const fe& x, uint32_t* carry) {
+  fe t;
+  uint32_t k;
+  t.w[0] = addc(x.w[0], kC0, 0u, &k);
+  t.w[1] = addc(x.w[1], kC1, k, &k);
+  t.w[2] = addc(x.w[2], 0u, k, &k);
+  t.w[3] = addc(x.w[3], 0u, k, &k);
+  *carry = k;
+  return t;
+}
+
+// s in [0, 2^128) plus an extra carry bit k (value s + k*2^128 < 2M):
+// canonical representative.  s + k*2^128 >= M  <=>  k | carry(s + C).
+__device__ __forceinline__ fe canon_with_carry(const fe& s, uint32_t k) {
+  uint32_t k2;
+  fe t = add_c(s, &k2);
+  const bool take = (k | k2) != 0u;
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.w[i] = take ? t.w[i] : s.w[i];
+  return r;
+}
+
+__device__ __forceinline__ fe fe_add(const fe& a, const fe& b) {
+  fe s;
+  uint32_t k;
+  s.w[0] = addc(a.w[0], b.w[0], 0u, &k);
+  s.w[1] = addc(a.w[1], b.w[1], k, &k);
+  s.w[2] = addc(a.w[2], b.w[2], k, &k);
+  s.w[3] = addc(a.w[3], b.w[3], k, &k);
+  return canon_with_carry(s, k);
+}
+
+__device__ __forceinline__ fe fe_sub(const fe& a, const fe& b) {
+  fe d;
+  uint32_t br;
+  d.w[0] = subb(a.w[0], b.w[0], 0u, &br);
+  d.w[1] = subb(a.w[1], b.w[1], br, &br);
+  d.w[2] = subb(a.w[2], b.w[2], br, &br);
+  d.w[3] = subb(a.w[3], b.w[3], br, &br);
+  // borrow: d + M = d - C (mod 2^128); d >= C+1 here so no further borrow.
+  const uint32_t m0 = br ? kC0 : 0u;
+  const uint32_t m1 = br ? kC1 : 0u;
+  uint32_t b2;
+  fe r;
+  r.w[0] = subb(d.w[0], m0, 0u, &b2);
+  r.w[1] = subb(d.w[1], m1, b2, &b2);
+  r.w[2] = subb(d.w[2], 0u, b2, &b2);
+  r.w[3] = subb(d.w[3], 0u, b2, &b2);
+  return r;
+}
+
+__device__ __forceinline__ fe fe_neg(const fe& a) { return fe_sub(fe_zero(), a); }
+
+__device__ __forceinline__ fe fe_dbl(const fe& a) { return fe_add(a, a); }
+
+// x / 2 mod M: even -> x >> 1, odd -> (x + M) >> 1 (x + M < 2^129).
+__device__ __forceinline__ fe fe_half(const fe& x) {
+  const uint32_t odd = x.w[0] & 1u;
+  fe s;
+  uint32_t k;
+  s.w[0] = addc(x.w[0], odd ? kM0 : 0u, 0u, &k);
+  s.w[1] = addc(x.w[1], odd ? kM1 : 0u, k, &k);
+  s.w[2] = addc(x.w[2], odd ? kM2 : 0u, k, &k);
+  s.w[3] = addc(x.w[3], odd ? kM3 : 0u, k, &k);
+  fe r;
+  r.w[0] = __builtin_amdgcn_alignbit(s.w[1], s.w[0], 1);
+  r.w[1] = __builtin_amdgcn_alignbit(s.w[2], s.w[1], 1);
+  r.w[2] = __builtin_amdgcn_alignbit(s.w[3], s.w[2], 1);
+  r.w[3] = __builtin_amdgcn_alignbit(k, s.w[3], 1);
+  return r;
+}
+
+// Full 256-bit product, operand scanning on v_mad_u64_u32.
+__device__ __forceinline__ void mul_wide(const fe& a, const fe& b, uint32_t r[8]) {
+  uint64_t t;
+  t = (uint64_t)a.w[0] * b.w[0];
+  r[0] = (uint32_t)t;
+  t = (uint64_t)a.w[0] * b.w[1] + (t >> 32);
+  r[1] = (uint32_t)t;
+  t = (uint64_t)a.w[0] * b.w[2] + (t >> 32);
+  r[2] = (uint32_t)t;
+  t = (uint64_t)a.w[0] * b.w[3] + (t >> 32);
+  r[3] = (uint32_t)t;
+  r[4] = (uint32_t)(t >> 32);
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t = (uint64_t)a.w[i] * b.w[j] + r[i + j] + c;
+      r[i + j] = (uint32_t)t;
+      c = t >> 32;
+    }
+    r[i + 4] = (uint32_t)c;
+  }
+}
+
+// Reduce a 256-bit value r (little-endian limbs) to canonical form.
+__device__ __forceinline__ fe reduce_wide(const uint32_t r[8]) {
+  // U = H * 0x2D00 (5 limbs), T = L + U*2^32 - H  (6 limbs, T >= 0)
+  uint32_t u[5];
+  uint64_t t;
+  t = (uint64_t)r[4] * kCmul;
+  u[0] = (uint32_t)t;
+  t = (uint64_t)r[5] * kCmul + (t >> 32);
+  u[1] = (uint32_t)t;
+  t = (uint64_t)r[6] * kCmul + (t >> 32);
+  u[2] = (uint32_t)t;
+  t = (uint64_t)r[7] * kCmul + (t >> 32);
+  u[3] = (uint32_t)t;
+  u[4] = (uint32_t)(t >> 32);
+  // A = L + (U << 32)
+  uint32_t a[6], k;
+  a[0] = r[0];
+  a[1] = addc(r[1], u[0], 0u, &k);
+  a[2] = addc(r[2], u[1], k, &k);
+  a[3] = addc(r[3], u[2], k, &k);
+  a[4] = addc(u[3], 0u, k, &k);
+  a[5] = u[4] + k;
+  // A -= H
+  uint32_t b;
+  a[0] = subb(a[0], r[4], 0u, &b);
+  a[1] = subb(a[1], r[5], b, &b);
+  a[2] = subb(a[2], r[6], b, &b);
+  a[3] = subb(a[3], r[7], b, &b);
+  a[4] = subb(a[4], 0u, b, &b);
+  a[5] = a[5] - b;
+  // Second fold: Th = a[4] + a[5]*2^32 (< 2^47).  Th*C = Th*0x2D00*2^32 - Th.
+  const uint64_t th = (uint64_t)a[4] | ((uint64_t)a[5] << 32);
+  const uint64_t v = th * (uint64_t)kCmul;  // < 2^61
+  fe s;
+  s.w[0] = a[0];
+  s.w[1] = addc(a[1], (uint32_t)v, 0u, &k);
+  s.w[2] = addc(a[2], (uint32_t)(v >> 32), k, &k);
+  s.w[3] = addc(a[3], 0u, k, &k);
+  uint32_t hi = k;
+  s.w[0] = subb(s.w[0], (uint32_t)th, 0u, &b);
+  s.w[1] = subb(s.w[1], (uint32_t)(th >> 32), b, &b);
+  s.w[2] = subb(s.w[2], 0u, b, &b);
+  s.w[3] = subb(s.w[3], 0u, b, &b);
+  hi -= b;  // value = s + hi*2^128, hi in {0,1}
+  return canon_with_carry(s, hi);
+}
+
+__device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
+  uint32_t r[8];
+  mul_wide(a, b, r);
+  return reduce_wide(r);
+}
+
+__device__ __forceinline__ fe fe_sqr(const fe& a) { return fe_mul(a, a); }
+
+__device__ __forceinline__ fe fe_pow(fe base, uint64_t e) {
+  fe acc = fe_one();
+  while (e) {
+    if (e & 1) acc = fe_mul(acc, base);
+    base = fe_mul(base, base);
+    e >>= 1;
+  }
+  return acc;
+}
+
+// 16-byte vector load/store of one element (global_load_dwordx4).
+__device__ __forceinline__ fe fe_load(const fe* p) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  return fe{{v.x, v.y, v.z, v.w}};
+}
+__device__ __forceinline__ void fe_store(fe* p, const fe& x) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(x.w[0], x.w[1], x.w[2], x.w[3]);
+}
+
+}  // namespace mlh

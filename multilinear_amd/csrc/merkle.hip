@@ -1,0 +1,213 @@
+// SHA-256 Merkle tree build on gfx950.
+//
+// Reference: src/merkle_tree/mod.rs:65-85 (Merkle::commit: leaf digests, then
+// `chunks(2)` levels until one digest is left, every layer kept), :92-131
+// (batch_commit), :178-189 (hash_leaf / hash_node), and src/fri/mod.rs:45-55
+// (commit_rs_code: leaf i = LE16(code[i]) ‖ LE16(code[i + n/2])).
+//
+// HBM layout of a tree with L = 2^l leaves: one buffer of 2L-1 digests in
+// level order (leaves at [0, L), level 1 at [L, L + L/2), ..., root last),
+// each digest the standard 32 SHA-256 output bytes.
+//
+// Kernels (one lane = one message; SHA-256 is VALU-bound, ~2k ops per
+// compression, so the design goal is full lanes, not bandwidth):
+//   * leaf_pairs   : leaf i from the RS pair (code[i], code[i + half]);
+//   * leaf_bytes   : generic fixed-length items (Merkle::commit over any T);
+//   * level2       : one lane builds a 2-level subtree (4 children -> 2 -> 1),
+//                    halving the launch count;
+//   * top          : one workgroup finishes the last <= 1024 nodes in LDS.
+#include "field.hpp"
+#include "merkle.hpp"
+#include "sha256.hpp"
+
+namespace mlh {
+
+__global__ void __launch_bounds__(256)
+leaf_pairs_kernel(const fe* __restrict__ code, uint64_t half, uint8_t* __restrict__ leaves) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= half) return;
+  const fe a = fe_load(code + i), b = fe_load(code + i + half);
+  uint32_t m[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    m[k] = bswap32(a.w[k]);
+    m[4 + k] = bswap32(b.w[k]);
+  }
+  digest_store(leaves + i * 32, sha256_msg32(m));
+}
+
+// Generic leaf: SHA256 of `item_len` bytes at items + i*item_len (any length).
+__global__ void leaf_bytes_kernel(const uint8_t* __restrict__ items, uint64_t item_len,
+                                  uint64_t count, uint8_t* __restrict__ leaves) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint8_t* p = items + i * item_len;
+  Sha256State st = sha256_iv();
+  uint32_t w[16];
+  const uint64_t total = item_len + 9;  // + 0x80 + 8-byte length
+  const uint64_t nblocks = (total + 63) / 64;
+  for (uint64_t blk = 0; blk < nblocks; ++blk) {
+    for (int wi = 0; wi < 16; ++wi) {
+      uint32_t word = 0;
+      for (int bi = 0; bi < 4; ++bi) {
+        const uint64_t pos = blk * 64 + wi * 4 + bi;
+        uint32_t byte;
+        if (pos < item_len) {
+          byte = p[pos];
+        } else if (pos == item_len) {
+          byte = 0x80u;
+        } else if (pos >= nblocks * 64 - 8) {
+          const uint64_t bits = item_len * 8;
+          const int sh = (int)(nblocks * 64 - 1 - pos) * 8;
+          byte = (uint32_t)((bits >> sh) & 0xFF);
+        } else {
+          byte = 0;
+        }
+        word = (word << 8) | byte;
+      }
+      w[wi] = word;
+    }
+    sha256_compress(st, w);
+  }
+  digest_store(leaves + i * 32, st);
+}
+
+// Batch leaf (merkle_tree/mod.rs:109-116): SHA256 of the m items data[j][i]
+// (j < m) concatenated; items are item_len bytes, batch j at items + j*stride.
+__global__ void leaf_batch_kernel(const uint8_t* __restrict__ items, uint64_t item_len,
+                                  uint64_t batch_stride, uint32_t m, uint64_t count,
+                                  uint8_t* __restrict__ leaves) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint64_t msg_len = item_len * m;
+  Sha256State st = sha256_iv();
+  uint32_t w[16];
+  const uint64_t total = msg_len + 9;
+  const uint64_t nblocks = (total + 63) / 64;
+  for (uint64_t blk = 0; blk < nblocks; ++blk) {
+    for (int wi = 0; wi < 16; ++wi) {
+      uint32_t word = 0;
+      for (int bi = 0; bi < 4; ++bi) {
+        const uint64_t pos = blk * 64 + wi * 4 + bi;
+        uint32_t byte;
+        if (pos < msg_len) {
+          const uint64_t j = pos / item_len, o = pos % item_len;
+          byte = items[j * batch_stride + i * item_len + o];
+        } else if (pos == msg_len) {
+          byte = 0x80u;
+        } else if (pos >= nblocks * 64 - 8) {
+          const uint64_t bits = msg_len * 8;
+          const int sh = (int)(nblocks * 64 - 1 - pos) * 8;
+          byte = (uint32_t)((bits >> sh) & 0xFF);
+        } else {
+          byte = 0;
+        }
+        word = (word << 8) | byte;
+      }
+      w[wi] = word;
+    }
+    sha256_compress(st, w);
+  }
+  digest_store(leaves + i * 32, st);
+}
+
+// One lane: children 4j..4j+3 -> parents 2j, 2j+1 -> grandparent j.
+__global__ void __launch_bounds__(256)
+level2_kernel(const uint8_t* __restrict__ child, uint8_t* __restrict__ parent,
+              uint8_t* __restrict__ grand, uint64_t ngrand) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ngrand) return;
+  const uint8_t* c = child + j * 128;
+  const Sha256State c0 = digest_load(c), c1 = digest_load(c + 32);
+  const Sha256State p0 = sha256_node(c0, c1);
+  digest_store(parent + (2 * j) * 32, p0);
+  const Sha256State c2 = digest_load(c + 64), c3 = digest_load(c + 96);
+  const Sha256State p1 = sha256_node(c2, c3);
+  digest_store(parent + (2 * j + 1) * 32, p1);
+  digest_store(grand + j * 32, sha256_node(p0, p1));
+}
+
+__global__ void __launch_bounds__(256)
+level1_kernel(const uint8_t* __restrict__ child, uint8_t* __restrict__ parent, uint64_t nparent) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nparent) return;
+  const Sha256State a = digest_load(child + j * 64), b = digest_load(child + j * 64 + 32);
+  digest_store(parent + j * 32, sha256_node(a, b));
+}
+
+// Finish a level of n <= 1024 digests (n a power of two >= 2) to the root in
+// one workgroup; writes every level into `out` consecutively.
+__global__ void __launch_bounds__(512)
+top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ out) {
+  __shared__ Sha256State s[1024];
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) s[i] = digest_load(level + i * 32);
+  __syncthreads();
+  uint64_t off = 0;
+  while (n > 1) {
+    const uint64_t np = n / 2;
+    Sha256State r;
+    const bool active = threadIdx.x < np;
+    if (active) r = sha256_node(s[2 * threadIdx.x], s[2 * threadIdx.x + 1]);
+    __syncthreads();
+    if (active) {
+      s[threadIdx.x] = r;
+      digest_store(out + (off + threadIdx.x) * 32, r);
+    }
+    __syncthreads();
+    off += np;
+    n = np;
+  }
+}
+
+static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+hipError_t launch_leaf_pairs(const fe* code, uint64_t half, uint8_t* leaves, hipStream_t st) {
+  hipLaunchKernelGGL(leaf_pairs_kernel, dim3(blocks_for(half, 256)), dim3(256), 0, st, code, half,
+                     leaves);
+  return hipGetLastError();
+}
+
+hipError_t launch_leaf_bytes(const uint8_t* items, uint64_t item_len, uint64_t count,
+                             uint8_t* leaves, hipStream_t st) {
+  hipLaunchKernelGGL(leaf_bytes_kernel, dim3(blocks_for(count, 128)), dim3(128), 0, st, items,
+                     item_len, count, leaves);
+  return hipGetLastError();
+}
+
+hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t batch_stride,
+                             uint32_t m, uint64_t count, uint8_t* leaves, hipStream_t st) {
+  hipLaunchKernelGGL(leaf_batch_kernel, dim3(blocks_for(count, 128)), dim3(128), 0, st, items,
+                     item_len, batch_stride, m, count, leaves);
+  return hipGetLastError();
+}
+
+// layers: 2L-1 digests, leaves already at [0, L).
+hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st) {
+  uint64_t n = L, off = 0;
+  while (n > 1024) {
+    uint8_t* child = layers + off * 32;
+    uint8_t* parent = child + n * 32;
+    if (n >= 4 * 1024) {
+      uint8_t* grand = parent + (n / 2) * 32;
+      hipLaunchKernelGGL(level2_kernel, dim3(blocks_for(n / 4, 256)), dim3(256), 0, st, child,
+                         parent, grand, n / 4);
+      off += n + n / 2;
+      n /= 4;
+    } else {
+      hipLaunchKernelGGL(level1_kernel, dim3(blocks_for(n / 2, 256)), dim3(256), 0, st, child,
+                         parent, n / 2);
+      off += n;
+      n /= 2;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (n > 1) {
+    const unsigned threads = n / 2 < 64 ? 64 : (unsigned)(n / 2);
+    hipLaunchKernelGGL(top_kernel, dim3(1), dim3(threads), 0, st, layers + off * 32, n,
+                       layers + (off + n) * 32);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mlh

@@ -1,0 +1,384 @@
+// Radix-2 NTT over F_M for gfx950.
+//
+// Reference semantics: src/ntt/mod.rs:69-110 (Polynomial::ntt) and :132-173
+// (LagrangePolynomial::intt): natural-order coefficients in, natural-order
+// evaluations out, evals[i] = sum_j c_j * gen^(i*j); the inverse uses gen^-1
+// and scales by n^-1.  The reference's bit-reverse + serial-twiddle DIT is an
+// implementation detail; any exact algorithm gives identical field values.
+//
+// MI355X design (DESIGN.md "NTT"): N = R_1 * ... * R_P with R_p = 2^6..2^9.
+// Pass p transforms digit p of the index in place (a generalised four-step):
+//   * a workgroup owns C = 8 adjacent "columns" x R rows, so every global
+//     access is 8 elements x 16 B = 128 contiguous bytes (dwordx4 per lane);
+//   * each thread holds 8 elements in VGPRs and runs radix-2 DIT stages in
+//     register phases of <= 3 stages; phases exchange through LDS
+//     (C*R*16 B, 32 KiB at R = 256);
+//   * the sub-transform input is read in bit-reversed row order straight from
+//     HBM (the permutation is on the per-lane global address, free), so the
+//     DIT output is in natural order;
+//   * passes p < P multiply by the inter-pass twiddle w^(j_rest*k*S_p), read
+//     from a two-level table (T_lo[e & 4095] * T_hi[e >> 12]); for the
+//     inverse, T_lo carries the n^-1 scale so no extra pass is needed;
+//   * the last pass tiles 8 consecutive k_1 values so its scattered natural-
+//     order stores are still 128-byte runs.
+// Sizes N <= 2^10 use one LDS-resident workgroup (ntt_small).
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "field.hpp"
+#include "ntt.hpp"
+
+namespace mlh {
+
+constexpr int kCols = 8;  // columns per tile (8 x 16 B = 128 B runs)
+constexpr int kEPT = 8;   // elements per thread
+
+__device__ __forceinline__ uint32_t bitrev(uint32_t x, int bits) {
+  return __builtin_bitreverse32(x) >> (32 - bits);
+}
+
+struct PassGeom {
+  uint32_t log_n;
+  uint32_t nradix;      // P
+  uint32_t p;           // 0-based pass index
+  uint32_t logr[kMaxPasses];
+  uint64_t stride;      // W_p (elements between consecutive rows of this digit)
+  uint64_t S;           // R_1*...*R_{p-1}
+};
+
+// Last pass: natural output index is K = k_1 + R_1*rev(mid) + (N/R_P)*k_P,
+// where mid holds digits 2..P-1 in storage order (digit 2 most significant)
+// and rev() re-weights them in natural order (digit 2 least significant).
+__device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64_t mid) {
+  uint64_t rev = 0;
+  // storage: lowest digit of mid is digit P-1 (0-based index nradix-2)
+  for (int q = (int)g.nradix - 2; q >= 1; --q) {
+    uint32_t shift = 0;  // natural weight of digit q: R_2*...*R_{q}
+    for (int i = 1; i < q; ++i) shift += g.logr[i];
+    rev += (mid & ((1ull << g.logr[q]) - 1)) << shift;
+    mid >>= g.logr[q];
+  }
+  return rev;
+}
+
+template <int LOGR, bool LAST, bool ZERO_TOP>
+__global__ void __launch_bounds__(kCols * (1 << LOGR) / kEPT)
+ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
+                const fe* __restrict__ tlo, const fe* __restrict__ thi, PassGeom g) {
+  constexpr int R = 1 << LOGR;
+  constexpr int TPC = R / kEPT;  // threads per column
+  __shared__ fe lds[R * kCols];
+
+  const int tid = threadIdx.x;
+  const int c = tid % kCols;
+  const int t = tid / kCols;
+  const uint64_t N = 1ull << g.log_n;
+  const uint64_t tile = blockIdx.x;
+
+  // ---- tile geometry -----------------------------------------------------
+  uint64_t base, jrest = 0, k1 = 0, mid = 0;
+  uint64_t rstride;  // element stride between rows of this digit
+  uint64_t cstride;  // element stride between the 8 columns
+  if (!LAST) {
+    const uint64_t W = g.stride;
+    const uint64_t lowcount = W / kCols;
+    const uint64_t hi = tile / lowcount, lo = tile % lowcount;
+    base = hi * (uint64_t)R * W + lo * kCols;
+    jrest = lo * kCols + c;
+    rstride = W;
+    cstride = 1;
+  } else {
+    const uint64_t RP = (uint64_t)R;
+    const uint64_t R1 = 1ull << g.logr[0];
+    const uint64_t W1 = N >> g.logr[0];
+    const uint64_t MID = N / (R1 * RP);
+    const uint64_t d1hi = tile / MID;
+    mid = tile % MID;
+    base = d1hi * kCols * W1 + mid * RP;
+    k1 = d1hi * kCols + c;
+    rstride = 1;
+    cstride = W1;
+  }
+  const fe* src = in + base + (uint64_t)c * cstride;
+  fe* dst = out + base + (uint64_t)c * cstride;
+
+  // ---- phase 1: load bit-reversed rows, stages 0..2 in registers ---------
+  fe x[kEPT];
+#pragma unroll
+  for (int e = 0; e < kEPT; ++e) {
+    const uint32_t row = bitrev((uint32_t)(t * kEPT + e), LOGR);
+    if (ZERO_TOP && row >= (uint32_t)(R / 2)) {
+      x[e] = fe_zero();
+    } else {
+      x[e] = fe_load(src + (uint64_t)row * rstride);
+    }
+  }
+
+  // Generic register phase: stages [s0, s0+q) on groups of 2^q elements.
+  auto run_phase = [&](auto S0_, auto Q_) {
+    constexpr int s0 = decltype(S0_)::value;
+    constexpr int q = decltype(Q_)::value;
+    constexpr int G = kEPT >> q;
+#pragma unroll
+    for (int s = s0; s < s0 + q; ++s) {
+      const int d = 1 << (s - s0);  // element distance inside a group
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) {
+        const uint32_t gamma = (uint32_t)(t * G + gi);
+        const uint32_t bpos = (gamma & ((1u << s0) - 1u)) | ((gamma >> s0) << (s0 + q));
+#pragma unroll
+        for (int i = 0; i < (1 << q); ++i) {
+          if (i & d) continue;
+          const int e0 = gi * (1 << q) + i;
+          const int e1 = e0 + d;
+          const uint32_t pos = bpos + ((uint32_t)i << s0);
+          const uint32_t j = pos & ((1u << s) - 1u);
+          fe v = x[e1];
+          if (s > 0) {
+            // phase 1 (s0 == 0): j is a compile-time function of i -> uniform load
+            const fe w = tw[j << (LOGR - 1 - s)];
+            if (s0 == 0) {
+              if ((i & ((1 << s) - 1)) != 0) v = fe_mul(v, w);
+            } else {
+              v = fe_mul(v, w);
+            }
+          }
+          const fe u = x[e0];
+          x[e0] = fe_add(u, v);
+          x[e1] = fe_sub(u, v);
+        }
+      }
+    }
+  };
+  auto positions = [&](auto S0_, auto Q_, uint32_t (&pos)[kEPT]) {
+    constexpr int s0 = decltype(S0_)::value;
+    constexpr int q = decltype(Q_)::value;
+    constexpr int G = kEPT >> q;
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      const uint32_t gamma = (uint32_t)(t * G + gi);
+      const uint32_t bpos = (gamma & ((1u << s0) - 1u)) | ((gamma >> s0) << (s0 + q));
+#pragma unroll
+      for (int i = 0; i < (1 << q); ++i) pos[gi * (1 << q) + i] = bpos + ((uint32_t)i << s0);
+    }
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I3 = std::integral_constant<int, 3>;
+  constexpr int Q1 = LOGR < 3 ? LOGR : 3;
+  run_phase(I0{}, std::integral_constant<int, Q1>{});
+  uint32_t pos[kEPT];
+  positions(I0{}, std::integral_constant<int, Q1>{}, pos);
+
+  // ---- remaining phases through LDS -------------------------------------
+  auto exchange_and_run = [&](auto S0_, auto Q_) {
+    __syncthreads();  // previous phase's reads of lds are done
+#pragma unroll
+    for (int e = 0; e < kEPT; ++e) fe_store(&lds[pos[e] * kCols + c], x[e]);
+    __syncthreads();
+    positions(S0_, Q_, pos);
+#pragma unroll
+    for (int e = 0; e < kEPT; ++e) x[e] = fe_load(&lds[pos[e] * kCols + c]);
+    run_phase(S0_, Q_);
+  };
+  if constexpr (LOGR > 3) {
+    constexpr int Q2 = (LOGR - 3) < 3 ? (LOGR - 3) : 3;
+    exchange_and_run(I3{}, std::integral_constant<int, Q2>{});
+    if constexpr (LOGR > 6) {
+      constexpr int Q3 = LOGR - 6;
+      static_assert(Q3 <= 3, "LOGR <= 9");
+      exchange_and_run(std::integral_constant<int, 6>{}, std::integral_constant<int, Q3>{});
+    }
+  }
+
+  // ---- epilogue: inter-pass twiddle, store --------------------------------
+  uint64_t kbase = 0;
+  uint32_t kshift = 0;
+  if (LAST) {
+    kbase = k1 + (reverse_mid_digits(g, mid) << g.logr[0]);
+    kshift = g.log_n - LOGR;
+  }
+#pragma unroll
+  for (int e = 0; e < kEPT; ++e) {
+    const uint64_t k = pos[e];
+    fe v = x[e];
+    if (!LAST) {
+      const uint64_t ex = (jrest * k * g.S) & (N - 1);
+      const fe w = fe_mul(tlo[ex & 4095], thi[ex >> 12]);
+      v = fe_mul(v, w);
+      fe_store(dst + k * rstride, v);
+    } else {
+      fe_store(out + kbase + (k << kshift), v);
+    }
+  }
+  (void)TPC;
+}
+
+// Single-workgroup NTT for N <= 2^10: LDS-resident radix-2 DIT.
+__global__ void __launch_bounds__(512)
+ntt_small_kernel(const fe* __restrict__ in, fe* __restrict__ out, const fe* __restrict__ tw,
+                 uint32_t log_n, uint32_t in_len, fe scale, int apply_scale) {
+  __shared__ fe lds[1024];
+  const uint32_t N = 1u << log_n;
+  for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+    const uint32_t src = bitrev(i, (int)log_n);
+    lds[i] = src < in_len ? fe_load(in + src) : fe_zero();
+  }
+  __syncthreads();
+  for (uint32_t s = 0; s < log_n; ++s) {
+    const uint32_t h = 1u << s;
+    for (uint32_t b = threadIdx.x; b < N / 2; b += blockDim.x) {
+      const uint32_t j = b & (h - 1);
+      const uint32_t p0 = j + ((b >> s) << (s + 1));
+      const fe u = lds[p0];
+      fe v = lds[p0 + h];
+      if (j) v = fe_mul(v, tw[j << (log_n - 1 - s)]);
+      lds[p0] = fe_add(u, v);
+      lds[p0 + h] = fe_sub(u, v);
+    }
+    __syncthreads();
+  }
+  for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+    fe v = lds[i];
+    if (apply_scale) v = fe_mul(v, scale);
+    fe_store(out + i, v);
+  }
+}
+
+// table[t] = base^t, t < count (twiddle tables; one-time per context).
+__global__ void pow_table_kernel(fe* __restrict__ out, fe base, fe scale, uint64_t count) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= count) return;
+  fe v = fe_pow(base, t);
+  v = fe_mul(v, scale);
+  fe_store(out + t, v);
+}
+
+// gen_pows[i] = g^i for i < count (NttField::pow_2_generator_powers,
+// src/ntt/mod.rs:18-28): block-base x in-block power, no serial chain.
+__global__ void pow_series_kernel(fe* __restrict__ out, const fe* __restrict__ tlo,
+                                  const fe* __restrict__ thi, uint64_t count) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= count) return;
+  fe_store(out + t, fe_mul(tlo[t & 4095], thi[t >> 12]));
+}
+
+// ---- host-side launchers ---------------------------------------------------
+
+template <int LOGR>
+static hipError_t launch_pass(bool last, bool zero_top, const fe* in, fe* out, const fe* tw,
+                              const fe* tlo, const fe* thi, const PassGeom& g, uint64_t tiles,
+                              hipStream_t st) {
+  constexpr int threads = kCols * (1 << LOGR) / kEPT;
+  if (last) {
+    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, true, false>), dim3((unsigned)tiles), dim3(threads), 0,
+                       st, in, out, tw, tlo, thi, g);
+  } else if (zero_top) {
+    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, false, true>), dim3((unsigned)tiles), dim3(threads), 0,
+                       st, in, out, tw, tlo, thi, g);
+  } else {
+    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, false, false>), dim3((unsigned)tiles), dim3(threads),
+                       0, st, in, out, tw, tlo, thi, g);
+  }
+  return hipGetLastError();
+}
+
+void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr) {
+  // Test hook: MLH_NTT_PLAN="4,8,4" forces a radix plan (digits 4..9 summing
+  // to log_n) so every pass shape can be checked at oracle-sized N.
+  if (const char* env = getenv("MLH_NTT_PLAN")) {
+    uint32_t tmp[kMaxPasses], cnt = 0, sum = 0;
+    const char* q = env;
+    while (*q && cnt < (uint32_t)kMaxPasses) {
+      const uint32_t v = (uint32_t)strtoul(q, (char**)&q, 10);
+      if (v < 4 || v > 9) { cnt = 0; break; }
+      tmp[cnt++] = v;
+      sum += v;
+      if (*q == ',') ++q; else break;
+    }
+    if (cnt >= 2 && sum == log_n) {
+      *nradix = cnt;
+      for (uint32_t i = 0; i < cnt; ++i) logr[i] = tmp[i];
+      return;
+    }
+  }
+  const uint32_t P = (log_n + 8) / 9;  // ceil(log_n / 9)
+  *nradix = P;
+  uint32_t rem = log_n;
+  for (uint32_t p = 0; p < P; ++p) {
+    const uint32_t left = P - p;
+    const uint32_t r = (rem + left - 1) / left;  // larger digits first
+    logr[p] = r;
+    rem -= r;
+  }
+}
+
+hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n, uint64_t in_len,
+                            fe scale, bool apply_scale, hipStream_t st) {
+  const uint32_t N = 1u << log_n;
+  const uint32_t threads = N / 2 < 64 ? 64 : (N / 2 > 512 ? 512 : N / 2);
+  hipLaunchKernelGGL(ntt_small_kernel, dim3(1), dim3(threads), 0, st, in, out, tw, log_n,
+                     (uint32_t)in_len, scale, apply_scale ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables& tb,
+                             uint32_t log_n, bool zero_top, hipStream_t st) {
+  PassGeom g;
+  g.log_n = log_n;
+  g.nradix = tb.nradix;
+  for (uint32_t p = 0; p < tb.nradix; ++p) g.logr[p] = tb.logr[p];
+  const uint64_t N = 1ull << log_n;
+  uint64_t S = 1;
+  uint64_t W = N;
+  for (uint32_t p = 0; p < tb.nradix; ++p) {
+    const uint32_t lr = tb.logr[p];
+    W >>= lr;
+    g.p = p;
+    g.stride = W;
+    g.S = S;
+    const bool last = (p + 1 == tb.nradix);
+    const uint64_t tiles = N / ((uint64_t)kCols << lr);
+    // pass 0: in -> scratch; middle passes in place on scratch; the last pass
+    // (a digit-reversal permutation of its tiles) scratch -> out.  The last
+    // pass can never run in place: a block would overwrite tiles that other,
+    // not yet resident, blocks still have to read.
+    const fe* src = (p == 0) ? in : scratch;
+    fe* dst = last ? out : scratch;
+    const bool zt = zero_top && p == 0;
+    const fe* tl = (p == 0) ? tb.tlo0 : tb.tlo;  // n^-1 scale applied once
+    hipError_t e;
+    switch (lr) {
+      case 4: e = launch_pass<4>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
+      case 5: e = launch_pass<5>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
+      case 6: e = launch_pass<6>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
+      case 7: e = launch_pass<7>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
+      case 8: e = launch_pass<8>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
+      case 9: e = launch_pass<9>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
+      default: return hipErrorInvalidValue;
+    }
+    if (e != hipSuccess) return e;
+    if (getenv("MLH_DEBUG_SYNC")) {
+      e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return e;
+    }
+    S <<= lr;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st) {
+  const unsigned blocks = (unsigned)((count + 255) / 256);
+  hipLaunchKernelGGL(pow_table_kernel, dim3(blocks), dim3(256), 0, st, out, base, scale, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_pow_series(fe* out, const fe* tlo, const fe* thi, uint64_t count,
+                             hipStream_t st) {
+  const unsigned blocks = (unsigned)((count + 255) / 256);
+  hipLaunchKernelGGL(pow_series_kernel, dim3(blocks), dim3(256), 0, st, out, tlo, thi, count);
+  return hipGetLastError();
+}
+
+}  // namespace mlh

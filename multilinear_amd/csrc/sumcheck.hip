@@ -1,0 +1,304 @@
+// MLE / sumcheck kernels on gfx950.
+//
+// Reference:
+//   * eq ("delta") table: src/constraint_system/sumcheck.rs:128-145 with
+//     Mask::evaluate (evaluation.rs:51-73): delta[idx] = prod_i (bit_i(idx) ?
+//     p[n-1-i] : 1 - p[n-1-i]) (big-endian point order);
+//   * round sums: SumcheckTables::partial_sum (sumcheck.rs:204-232), PCS
+//     composition x[0] (multilinear_pcs.rs:56), evaluated at X = 1 and X = 2:
+//       s1 = sum_{i<h} m[i+h] d[i+h],
+//       s2 = sum_{i<h} (2 m[i+h] - m[i]) (2 d[i+h] - d[i]);
+//   * fold: SumcheckTables::fold (sumcheck.rs:234-247): t[i] = (1-r) t[i] + r t[i+h],
+//     computed as t[i] + r (t[i+h] - t[i]) (same field value, one modmul);
+//   * Moebius transform: MultilinearPolynomialEvals::to_coefficient
+//     (polynomials.rs:150-163), and its zeta inverse (:111-124);
+//   * MLE evaluate (polynomials.rs:165-187) = dot(evals, eq(args)).
+//
+// The round kernels are HBM-streaming: 16 B per lane dwordx4 loads, sums
+// reduced with 64-lane shuffles, then LDS, then one partial per workgroup
+// (reduced by a second single-workgroup launch; no float-style atomics exist
+// for F_M).  fold_sums fuses round k's fold with round k+1's sums: lane i reads
+// t[i], t[i+h/2], t[i+h], t[i+3h/2] and writes the two folded values, so each
+// round moves 2*S*16 B in and S*16 B out (the survey's 48 S bytes).
+#include "field.hpp"
+#include "sumcheck.hpp"
+
+namespace mlh {
+
+constexpr int kRedThreads = 256;
+
+__device__ __forceinline__ fe shfl_xor_fe(const fe& x, int mask) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.w[i] = (uint32_t)__shfl_xor((int)x.w[i], mask, 64);
+  return r;
+}
+
+// Block reduction of two field sums; thread 0 ends with the totals.
+__device__ __forceinline__ void block_reduce2(fe& a, fe& b) {
+  __shared__ fe sa[kRedThreads / 64], sb[kRedThreads / 64];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    a = fe_add(a, shfl_xor_fe(a, m));
+    b = fe_add(b, shfl_xor_fe(b, m));
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sa[wid] = a;
+    sb[wid] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      a = fe_add(a, sa[w]);
+      b = fe_add(b, sb[w]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kRedThreads)
+sums_kernel(const fe* __restrict__ m, const fe* __restrict__ d, uint64_t h,
+            fe* __restrict__ partials) {
+  fe s1 = fe_zero(), s2 = fe_zero();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < h; i += stride) {
+    const fe m0 = fe_load(m + i), m1 = fe_load(m + i + h);
+    const fe d0 = fe_load(d + i), d1 = fe_load(d + i + h);
+    s1 = fe_add(s1, fe_mul(m1, d1));
+    const fe mm = fe_sub(fe_dbl(m1), m0), dd = fe_sub(fe_dbl(d1), d0);
+    s2 = fe_add(s2, fe_mul(mm, dd));
+  }
+  block_reduce2(s1, s2);
+  if (threadIdx.x == 0) {
+    fe_store(partials + 2 * blockIdx.x, s1);
+    fe_store(partials + 2 * blockIdx.x + 1, s2);
+  }
+}
+
+__device__ __forceinline__ fe lerp(const fe& lo, const fe& hi, const fe& r) {
+  return fe_add(lo, fe_mul(r, fe_sub(hi, lo)));
+}
+
+// Fold tables of size S with r (in place, first half) and emit the next
+// round's sums over the folded tables (h' = S/4).
+__global__ void __launch_bounds__(kRedThreads)
+fold_sums_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r,
+                 fe* __restrict__ partials) {
+  const uint64_t h = S / 2, q = S / 4;
+  fe s1 = fe_zero(), s2 = fe_zero();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < q; i += stride) {
+    const fe ma = fe_load(m + i), mb = fe_load(m + i + q);
+    const fe mc = fe_load(m + i + h), md = fe_load(m + i + h + q);
+    const fe da = fe_load(d + i), db = fe_load(d + i + q);
+    const fe dc = fe_load(d + i + h), dd = fe_load(d + i + h + q);
+    const fe m0 = lerp(ma, mc, r), m1 = lerp(mb, md, r);
+    const fe d0 = lerp(da, dc, r), d1 = lerp(db, dd, r);
+    fe_store(m + i, m0);
+    fe_store(m + i + q, m1);
+    fe_store(d + i, d0);
+    fe_store(d + i + q, d1);
+    s1 = fe_add(s1, fe_mul(m1, d1));
+    s2 = fe_add(s2, fe_mul(fe_sub(fe_dbl(m1), m0), fe_sub(fe_dbl(d1), d0)));
+  }
+  block_reduce2(s1, s2);
+  if (threadIdx.x == 0) {
+    fe_store(partials + 2 * blockIdx.x, s1);
+    fe_store(partials + 2 * blockIdx.x + 1, s2);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+fold_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r) {
+  const uint64_t h = S / 2;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= h) return;
+  fe_store(m + i, lerp(fe_load(m + i), fe_load(m + i + h), r));
+  fe_store(d + i, lerp(fe_load(d + i), fe_load(d + i + h), r));
+}
+
+__global__ void __launch_bounds__(kRedThreads)
+reduce_partials_kernel(const fe* __restrict__ partials, uint32_t nblocks, fe* __restrict__ out) {
+  fe a = fe_zero(), b = fe_zero();
+  for (uint32_t i = threadIdx.x; i < nblocks; i += blockDim.x) {
+    a = fe_add(a, fe_load(partials + 2 * i));
+    b = fe_add(b, fe_load(partials + 2 * i + 1));
+  }
+  block_reduce2(a, b);
+  if (threadIdx.x == 0) {
+    fe_store(out, a);
+    fe_store(out + 1, b);
+  }
+}
+
+// dot(a, b) partials (second slot unused = 0).
+__global__ void __launch_bounds__(kRedThreads)
+dot_kernel(const fe* __restrict__ a, const fe* __restrict__ b, uint64_t n,
+           fe* __restrict__ partials) {
+  fe s = fe_zero(), z = fe_zero();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    s = fe_add(s, fe_mul(fe_load(a + i), fe_load(b + i)));
+  block_reduce2(s, z);
+  if (threadIdx.x == 0) {
+    fe_store(partials + 2 * blockIdx.x, s);
+    fe_store(partials + 2 * blockIdx.x + 1, z);
+  }
+}
+
+// eq table of `cnt` points (big-endian): out[x] = prod_{i<cnt} (bit_i(x) ?
+// p[cnt-1-i] : 1 - p[cnt-1-i]).
+__global__ void eq_small_kernel(const fe* __restrict__ pts, uint32_t cnt, fe* __restrict__ out) {
+  const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= (1u << cnt)) return;
+  fe acc = fe_one();
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const fe p = pts[cnt - 1 - i];
+    acc = fe_mul(acc, ((x >> i) & 1u) ? p : fe_sub(fe_one(), p));
+  }
+  fe_store(out + x, acc);
+}
+
+// delta[idx] = lo[idx & (2^a - 1)] * hi[idx >> a]
+__global__ void __launch_bounds__(256)
+eq_expand_kernel(const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t a, uint64_t n,
+                 fe* __restrict__ out) {
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  fe_store(out + idx, fe_mul(lo[idx & ((1ull << a) - 1)], hi[idx >> a]));
+}
+
+// Moebius (sign = -1) / zeta (sign = +1) transform over `nbits` consecutive
+// index bits [b0, b0 + nbits) of a 2^log_n table, in place.  A workgroup owns
+// a tile of 8 adjacent low-index columns (or 8 consecutive elements of each
+// row when b0 == 0) x 2^nbits rows staged in LDS.
+template <int SIGN>
+__global__ void __launch_bounds__(256)
+mobius_pass_kernel(fe* __restrict__ c, uint32_t log_n, uint32_t b0, uint32_t nbits) {
+  __shared__ fe lds[2048];
+  const uint64_t R = 1ull << nbits;
+  const uint64_t W = 1ull << b0;  // row stride
+  uint64_t cols, base;
+  // columns = index bits below b0 (contiguous); tile = up to 8 of them
+  cols = W < 8 ? W : 8;
+  const uint64_t lowcount = W / cols;
+  const uint64_t tile = blockIdx.x;
+  const uint64_t hi = tile / lowcount, lo = tile % lowcount;
+  base = hi * R * W + lo * cols;
+  const uint64_t E = R * cols;
+  for (uint64_t e = threadIdx.x; e < E; e += blockDim.x) {
+    const uint64_t row = e / cols, col = e % cols;
+    lds[e] = fe_load(c + base + row * W + col);
+  }
+  __syncthreads();
+  for (uint32_t b = 0; b < nbits; ++b) {
+    const uint64_t bit = 1ull << b;
+    for (uint64_t e = threadIdx.x; e < E / 2; e += blockDim.x) {
+      const uint64_t pr = e / cols, col = e % cols;  // pair index over rows
+      const uint64_t r0 = (pr & (bit - 1)) | ((pr >> b) << (b + 1));
+      const uint64_t i0 = r0 * cols + col, i1 = (r0 | bit) * cols + col;
+      lds[i1] = SIGN < 0 ? fe_sub(lds[i1], lds[i0]) : fe_add(lds[i1], lds[i0]);
+    }
+    __syncthreads();
+  }
+  for (uint64_t e = threadIdx.x; e < E; e += blockDim.x) {
+    const uint64_t row = e / cols, col = e % cols;
+    fe_store(c + base + row * W + col, lds[e]);
+  }
+  (void)log_n;
+}
+
+// out[i] = in[bitrev(i)] (bit_reverse_permutation, src/ntt/mod.rs:113-123).
+__global__ void __launch_bounds__(256)
+bitrev_kernel(const fe* __restrict__ in, fe* __restrict__ out, uint32_t log_n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (1ull << log_n)) return;
+  const uint64_t j = log_n ? (__builtin_bitreverse64(i) >> (64 - log_n)) : 0;
+  fe_store(out + i, fe_load(in + j));
+}
+
+// ---- launchers -------------------------------------------------------------
+
+static inline unsigned red_blocks(uint64_t work) {
+  uint64_t b = (work + kRedThreads - 1) / kRedThreads;
+  if (b > kMaxRedBlocks) b = kMaxRedBlocks;
+  if (b == 0) b = 1;
+  return (unsigned)b;
+}
+
+hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* out,
+                       hipStream_t st) {
+  const unsigned nb = red_blocks(h);
+  hipLaunchKernelGGL(sums_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, d, h, partials);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* out,
+                            hipStream_t st) {
+  const unsigned nb = red_blocks(S / 4);
+  hipLaunchKernelGGL(fold_sums_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, d, S, r, partials);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st) {
+  const uint64_t h = S / 2;
+  hipLaunchKernelGGL(fold_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, st, m, d, S, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
+                      hipStream_t st) {
+  const unsigned nb = red_blocks(n);
+  hipLaunchKernelGGL(dot_kernel, dim3(nb), dim3(kRedThreads), 0, st, a, b, n, partials);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, out);
+  return hipGetLastError();
+}
+
+// pts: n device points; scratch: 2^(n-a) + 2^a elements.
+hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st) {
+  const uint32_t a = n / 2, b = n - a;
+  fe* lo = scratch;
+  fe* hi = scratch + (1u << a);
+  // lo: last a points (bits 0..a-1), hi: first b points (bits a..n-1)
+  hipLaunchKernelGGL(eq_small_kernel, dim3(((1u << a) + 255) / 256), dim3(256), 0, st, pts + b, a,
+                     lo);
+  hipLaunchKernelGGL(eq_small_kernel, dim3(((1u << b) + 255) / 256), dim3(256), 0, st, pts, b, hi);
+  const uint64_t N = 1ull << n;
+  hipLaunchKernelGGL(eq_expand_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, lo, hi,
+                     a, N, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_mobius(fe* c, uint32_t log_n, bool inverse_zeta, hipStream_t st) {
+  uint32_t b0 = 0;
+  while (b0 < log_n) {
+    const uint32_t nb = (log_n - b0) < 8 ? (log_n - b0) : 8;
+    const uint64_t W = 1ull << b0;
+    const uint64_t cols = W < 8 ? W : 8;
+    // tile: 2^nb rows x cols elements must fit 2048 LDS slots
+    uint32_t bits = nb;
+    while ((1ull << bits) * cols > 2048) --bits;
+    const uint64_t tiles = (1ull << log_n) / ((1ull << bits) * cols);
+    if (inverse_zeta)
+      hipLaunchKernelGGL(mobius_pass_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, st, c, log_n,
+                         b0, bits);
+    else
+      hipLaunchKernelGGL(mobius_pass_kernel<-1>, dim3((unsigned)tiles), dim3(256), 0, st, c, log_n,
+                         b0, bits);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    b0 += bits;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_bitrev(const fe* in, fe* out, uint32_t log_n, hipStream_t st) {
+  const uint64_t N = 1ull << log_n;
+  hipLaunchKernelGGL(bitrev_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, in, out,
+                     log_n);
+  return hipGetLastError();
+}
+
+}  // namespace mlh

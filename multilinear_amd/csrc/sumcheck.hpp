@@ -1,0 +1,25 @@
+// Sumcheck / MLE launch interface (internal to libmlhip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "field.hpp"
+
+namespace mlh {
+
+constexpr uint32_t kMaxRedBlocks = 2048;  // partials buffer: 2 * kMaxRedBlocks elements
+
+// out[0] = s1, out[1] = s2 over tables of size 2h (device).
+hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* out,
+                       hipStream_t st);
+// fold size-S tables with r, then sums of the folded (size S/2) tables.
+hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* out,
+                            hipStream_t st);
+hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st);
+hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
+                      hipStream_t st);
+hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st);
+hipError_t launch_mobius(fe* c, uint32_t log_n, bool inverse_zeta, hipStream_t st);
+hipError_t launch_bitrev(const fe* in, fe* out, uint32_t log_n, hipStream_t st);
+
+}  // namespace mlh

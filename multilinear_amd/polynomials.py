@@ -1,0 +1,52 @@
+"""src/polynomials.rs multilinear parts on the MI355X."""
+import ctypes
+
+from .device import check, context, fe_from_bytes, lib, ptr
+
+
+def _log2(n):
+    if n < 1 or n & (n - 1):
+        raise ValueError("length must be a power of two")
+    return n.bit_length() - 1
+
+
+def to_coefficient(evals, device=0):
+    """MultilinearPolynomialEvals::to_coefficient (polynomials.rs:150-163); new tensor."""
+    ctx = context(device)
+    out = evals.clone()
+    check(lib().mlh_mle_to_coefficient(ctx, ptr(out), _log2(evals.shape[0])), ctx)
+    return out
+
+
+def to_evaluation(coeffs, device=0):
+    """MultilinearPolynomial::to_evaluation (polynomials.rs:111-124); new tensor."""
+    ctx = context(device)
+    out = coeffs.clone()
+    check(lib().mlh_mle_to_evaluation(ctx, ptr(out), _log2(coeffs.shape[0])), ctx)
+    return out
+
+
+def _points(args):
+    raw = b"".join(int(a).to_bytes(16, "little") for a in args)
+    return (ctypes.c_uint8 * max(1, len(raw))).from_buffer_copy(raw or b"\0")
+
+
+def evaluate(evals, args, device=0):
+    """MultilinearPolynomialEvals::evaluate (polynomials.rs:165-187)."""
+    n = len(args)
+    if 1 << n != evals.shape[0]:
+        raise ValueError("Wrong number of arguments")
+    ctx = context(device)
+    out = (ctypes.c_uint8 * 16)()
+    check(lib().mlh_mle_evaluate(ctx, ptr(evals), n, _points(args), out), ctx)
+    return fe_from_bytes(out)
+
+
+def eq_table(points, device=0):
+    """delta table of build_tables_for_pcs (sumcheck.rs:133-138)."""
+    from .device import empty
+
+    ctx = context(device)
+    out = empty(1 << len(points), device)
+    check(lib().mlh_eq_table(ctx, _points(points), len(points), ptr(out)), ctx)
+    return out

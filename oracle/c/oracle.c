@@ -1,0 +1,395 @@
+/*
+ * oracle.c -- single-threaded C restatement of the reference CPU path.
+ * TEST INFRASTRUCTURE ONLY (see oracle/__init__.py): the checker for the
+ * full-size on-box parity tests and the bench's cpu_baseline ("port").
+ *
+ * It follows the reference loops, not the GPU design:
+ *   - Polynomial::ntt / LagrangePolynomial::intt (src/ntt/mod.rs:69-173):
+ *     clone, bit_reverse_permutation, unrolled len=2 stage, iterative DIT with
+ *     a serial per-stage twiddle vector gen^(n/len) powers, n^-1 scaling;
+ *   - NttField::pow_2_generator_powers (src/ntt/mod.rs:18-28), serial;
+ *   - reed_solomon (src/fri/mod.rs:19-28): resize to 2N, ntt;
+ *   - commit_rs_code + Merkle::commit (src/fri/mod.rs:45-55,
+ *     src/merkle_tree/mod.rs:65-85, :178-189): SHA-256 leaves of the 32-byte
+ *     pairs, chunks(2) levels, all layers kept;
+ *   - FriProverData::fold_step / fold (src/fri/mod.rs:79-145): clone of the
+ *     layer, twiddle gen_pows[len - i*2^k], multiply by half;
+ *   - Transcript (src/transcript.rs): running SHA-256;
+ *   - to_coefficient (src/polynomials.rs:150-163), Mask-based delta table
+ *     (sumcheck.rs:128-145, evaluation.rs:51-73), partial_sum / fold
+ *     (sumcheck.rs:204-247).
+ * Field: M = 2^128 - 45*2^40 + 1, canonical u128 little endian.
+ * SHA-256: FIPS 180-4, written here (the reference uses the sha2 crate).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+
+static const u128 MOD = (((u128)0xFFFFFFFFFFFFFFFFull) << 64) | (u128)0xFFFFD30000000001ull;
+static const uint64_t CF = 0x2CFFFFFFFFFFull; /* 2^128 mod M */
+
+static inline u128 fadd(u128 a, u128 b) {
+  u128 s = a + b;
+  if (s < a) return s + CF; /* wrapped past 2^128 */
+  return s >= MOD ? s - MOD : s;
+}
+static inline u128 fsub(u128 a, u128 b) { return a >= b ? a - b : a - b + MOD; }
+
+/* 128x128 -> 256, then fold hi*2^128 = hi*CF until hi = 0 */
+static inline u128 fmul(u128 a, u128 b) {
+  uint64_t a0 = (uint64_t)a, a1 = (uint64_t)(a >> 64), b0 = (uint64_t)b, b1 = (uint64_t)(b >> 64);
+  u128 p00 = (u128)a0 * b0, p01 = (u128)a0 * b1, p10 = (u128)a1 * b0, p11 = (u128)a1 * b1;
+  /* column accumulate into 4 x 64-bit words */
+  uint64_t w0 = (uint64_t)p00;
+  u128 t = (p00 >> 64) + (uint64_t)p01 + (uint64_t)p10;
+  uint64_t w1 = (uint64_t)t;
+  t = (t >> 64) + (p01 >> 64) + (p10 >> 64) + (uint64_t)p11;
+  uint64_t w2 = (uint64_t)t;
+  uint64_t w3 = (uint64_t)((t >> 64) + (p11 >> 64));
+  u128 lo = ((u128)w1 << 64) | w0;
+  u128 hi = ((u128)w3 << 64) | w2;
+  while (hi) {
+    /* hi * CF: hi < 2^128, CF < 2^46 */
+    uint64_t h0 = (uint64_t)hi, h1 = (uint64_t)(hi >> 64);
+    u128 q0 = (u128)h0 * CF; /* < 2^110 */
+    u128 q1 = (u128)h1 * CF; /* < 2^110, weight 2^64 */
+    u128 nhi = q1 >> 64;
+    u128 add1 = q1 << 64;
+    u128 s = lo + q0;
+    if (s < lo) nhi++;
+    u128 s2 = s + add1;
+    if (s2 < s) nhi++;
+    lo = s2;
+    hi = nhi;
+  }
+  return lo >= MOD ? lo - MOD : lo;
+}
+static u128 fpow(u128 b, u128 e) {
+  u128 r = 1;
+  while (e) {
+    if (e & 1) r = fmul(r, b);
+    b = fmul(b, b);
+    e >>= 1;
+  }
+  return r;
+}
+static u128 finv(u128 a) { return fpow(a, MOD - 2); }
+
+static inline u128 ld(const uint8_t* p) {
+  u128 v;
+  memcpy(&v, p, 16);
+  return v;
+}
+static inline void st(uint8_t* p, u128 v) { memcpy(p, &v, 16); }
+
+/* ------------------------------------------------------------------ SHA-256 */
+typedef struct {
+  uint32_t h[8];
+  uint8_t buf[64];
+  uint64_t len;
+} sha_t;
+
+static const uint32_t SK[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+    0xc67178f2u};
+
+#define ROR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
+
+static void sha_block(uint32_t h[8], const uint8_t* b) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; i++)
+    w[i] = ((uint32_t)b[4 * i] << 24) | ((uint32_t)b[4 * i + 1] << 16) |
+           ((uint32_t)b[4 * i + 2] << 8) | b[4 * i + 3];
+  for (int i = 16; i < 64; i++) {
+    uint32_t s0 = ROR(w[i - 15], 7) ^ ROR(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = ROR(w[i - 2], 17) ^ ROR(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = h[0], bb = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int i = 0; i < 64; i++) {
+    uint32_t t1 = hh + (ROR(e, 6) ^ ROR(e, 11) ^ ROR(e, 25)) + ((e & f) ^ (~e & g)) + SK[i] + w[i];
+    uint32_t t2 = (ROR(a, 2) ^ ROR(a, 13) ^ ROR(a, 22)) + ((a & bb) ^ (a & c) ^ (bb & c));
+    hh = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = bb;
+    bb = a;
+    a = t1 + t2;
+  }
+  h[0] += a;
+  h[1] += bb;
+  h[2] += c;
+  h[3] += d;
+  h[4] += e;
+  h[5] += f;
+  h[6] += g;
+  h[7] += hh;
+}
+
+static void sha_init(sha_t* s) {
+  static const uint32_t iv[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  memcpy(s->h, iv, 32);
+  s->len = 0;
+}
+static void sha_update(sha_t* s, const uint8_t* p, size_t n) {
+  while (n) {
+    size_t fill = s->len % 64, take = 64 - fill < n ? 64 - fill : n;
+    memcpy(s->buf + fill, p, take);
+    s->len += take;
+    p += take;
+    n -= take;
+    if (s->len % 64 == 0) sha_block(s->h, s->buf);
+  }
+}
+static void sha_final(const sha_t* s0, uint8_t out[32]) {
+  sha_t s = *s0;
+  uint64_t bits = s.len * 8;
+  uint8_t one = 0x80, zero = 0;
+  sha_update(&s, &one, 1);
+  while (s.len % 64 != 56) sha_update(&s, &zero, 1);
+  uint8_t lb[8];
+  for (int i = 0; i < 8; i++) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
+  sha_update(&s, lb, 8);
+  for (int i = 0; i < 8; i++) {
+    out[4 * i] = s.h[i] >> 24;
+    out[4 * i + 1] = s.h[i] >> 16;
+    out[4 * i + 2] = s.h[i] >> 8;
+    out[4 * i + 3] = s.h[i];
+  }
+}
+void orc_sha256(const uint8_t* msg, uint64_t len, uint8_t out[32]) {
+  sha_t s;
+  sha_init(&s);
+  sha_update(&s, msg, len);
+  sha_final(&s, out);
+}
+
+/* ---------------------------------------------------------------------- NTT */
+static uint64_t rev_bits(uint64_t x, int bits) {
+  uint64_t r = 0;
+  for (int b = 0; b < bits; b++) r |= ((x >> b) & 1ull) << (bits - 1 - b);
+  return r;
+}
+
+static void bit_reverse_permutation(u128* v, uint64_t n) {
+  int bits = 0;
+  while ((1ull << bits) < n) bits++;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t j = rev_bits(i, bits);
+    if (i < j) {
+      u128 t = v[i];
+      v[i] = v[j];
+      v[j] = t;
+    }
+  }
+}
+
+static void dit(u128* v, uint64_t n, u128 gen) {
+  for (uint64_t i = 0; i < n; i += 2) {
+    u128 u = v[i], w = v[i + 1];
+    v[i] = fadd(u, w);
+    v[i + 1] = fsub(u, w);
+  }
+  u128* pows = (u128*)malloc(sizeof(u128) * (n / 2 > 0 ? n / 2 : 1));
+  for (uint64_t len = 4; len <= n; len *= 2) {
+    u128 cur = fpow(gen, n / len), acc = 1;
+    for (uint64_t j = 0; j < len / 2; j++) {
+      pows[j] = acc;
+      acc = fmul(acc, cur);
+    }
+    for (uint64_t i = 0; i < n; i += len)
+      for (uint64_t j = 0; j < len / 2; j++) {
+        u128 w = fmul(v[i + j + len / 2], pows[j]), u = v[i + j];
+        v[i + j] = fadd(u, w);
+        v[i + j + len / 2] = fsub(u, w);
+      }
+  }
+  free(pows);
+}
+
+/* in/out: 2^log_n elements (16 B each); may alias. */
+int orc_ntt(const uint8_t* in, uint8_t* out, uint32_t log_n, const uint8_t gen[16], int inverse) {
+  uint64_t n = 1ull << log_n;
+  if (log_n < 1) return 2;
+  u128* v = (u128*)malloc(n * sizeof(u128));
+  if (!v) return 5;
+  memcpy(v, in, n * 16); /* clone (ntt/mod.rs:76) */
+  bit_reverse_permutation(v, n);
+  u128 g = ld(gen);
+  if (inverse) g = finv(g);
+  dit(v, n, g);
+  if (inverse) {
+    u128 ninv = finv((u128)n);
+    for (uint64_t i = 0; i < n; i++) v[i] = fmul(v[i], ninv);
+  }
+  memcpy(out, v, n * 16);
+  free(v);
+  return 0;
+}
+
+void orc_pow_2_generator(uint32_t log_size, uint8_t out[16]) {
+  st(out, fpow(3, (MOD - 1) >> log_size));
+}
+
+void orc_pow_2_generator_powers(uint32_t log_size, uint8_t* out) {
+  u128 g = fpow(3, (MOD - 1) >> log_size), cur = 1;
+  for (uint64_t i = 0; i < (1ull << log_size); i++) {
+    st(out + 16 * i, cur);
+    cur = fmul(cur, g);
+  }
+}
+
+int orc_reed_solomon(const uint8_t* coeffs, uint32_t log_n, const uint8_t gen[16], uint8_t* code) {
+  uint64_t n = 1ull << log_n;
+  uint8_t* tmp = (uint8_t*)calloc(2 * n, 16);
+  memcpy(tmp, coeffs, n * 16);
+  int r = orc_ntt(tmp, code, log_n + 1, gen, 0);
+  free(tmp);
+  return r;
+}
+
+/* ------------------------------------------------------------------- Merkle */
+/* layers: (2L-1)*32 bytes, leaves first; pairs (code[i], code[i + n/2]). */
+void orc_merkle_commit_pairs(const uint8_t* code, uint32_t log_code, uint8_t* layers) {
+  uint64_t n = 1ull << log_code, L = n / 2;
+  for (uint64_t i = 0; i < L; i++) {
+    uint8_t leaf[32];
+    memcpy(leaf, code + 16 * i, 16);
+    memcpy(leaf + 16, code + 16 * (i + L), 16);
+    orc_sha256(leaf, 32, layers + 32 * i);
+  }
+  uint64_t off = 0, cnt = L;
+  while (cnt > 1) {
+    for (uint64_t j = 0; j < cnt / 2; j++)
+      orc_sha256(layers + 32 * (off + 2 * j), 64, layers + 32 * (off + cnt + j));
+    off += cnt;
+    cnt /= 2;
+  }
+}
+
+/* ------------------------------------------------------------------ FRI fold */
+/* FriProverData::fold with a fresh transcript (fri/mod.rs:136-145): writes the
+ * T = log_code - 1 roots and the last element; returns 6 if not an RS code. */
+int orc_fri_commit(const uint8_t* code, uint32_t log_code, uint8_t* roots, uint8_t last[16],
+                   uint8_t last_random[32]) {
+  uint64_t n0 = 1ull << log_code;
+  sha_t tr;
+  sha_init(&tr);
+  u128 g = fpow(3, (MOD - 1) >> log_code);
+  u128 ginv = finv(g), inv2 = finv(2);
+  /* gen_pows (ntt/mod.rs:18-28), used as gen_pows[len - i*2^k] */
+  u128* gp = (u128*)malloc(n0 * sizeof(u128));
+  u128 cur = 1;
+  for (uint64_t i = 0; i < n0; i++) {
+    gp[i] = cur;
+    cur = fmul(cur, g);
+  }
+  (void)ginv;
+  u128* layer = (u128*)malloc(n0 * sizeof(u128));
+  memcpy(layer, code, n0 * 16);
+  uint8_t* tree = (uint8_t*)malloc((n0 - 1) * 32);
+  uint64_t n = n0;
+  uint32_t t = 0;
+  orc_merkle_commit_pairs((const uint8_t*)layer, log_code, tree);
+  memcpy(roots + 32 * t, tree + 32 * (n - 2), 32);
+  sha_update(&tr, roots + 32 * t, 32);
+  t++;
+  int rc = 0;
+  for (uint32_t k = 0; k + 1 < log_code; k++) {
+    uint8_t rnd[32];
+    sha_final(&tr, rnd);
+    u128 r = ld(rnd);
+    if (r >= MOD) r -= MOD;
+    uint64_t half = n / 2;
+    u128* next = (u128*)malloc(half * sizeof(u128)); /* clone + fold */
+    for (uint64_t i = 0; i < half; i++) {
+      u128 a = layer[i], b = layer[i + half];
+      u128 tw = i == 0 ? 1 : gp[n0 - i * (1ull << k)];
+      u128 odd = fmul(fsub(a, b), tw);
+      next[i] = fmul(fadd(fadd(a, b), fmul(r, odd)), inv2);
+    }
+    free(layer);
+    layer = next;
+    n = half;
+    if (half == 2) {
+      if (layer[0] != layer[1]) rc = 6;
+      st(last, layer[0]);
+      sha_update(&tr, last, 16);
+      break;
+    }
+    orc_merkle_commit_pairs((const uint8_t*)layer, (uint32_t)__builtin_ctzll(n), tree);
+    memcpy(roots + 32 * t, tree + 32 * (n - 2), 32);
+    sha_update(&tr, roots + 32 * t, 32);
+    t++;
+  }
+  if (last_random) sha_final(&tr, last_random);
+  free(layer);
+  free(tree);
+  free(gp);
+  return rc;
+}
+
+/* ------------------------------------------------------- multilinear / sumcheck */
+void orc_to_coefficient(uint8_t* v, uint32_t log_n) {
+  uint64_t n = 1ull << log_n;
+  for (uint32_t i = 0; i < log_n; i++) {
+    uint64_t m = 1ull << i;
+    for (uint64_t j = 0; j < n; j++)
+      if (j & m) st(v + 16 * j, fsub(ld(v + 16 * j), ld(v + 16 * (j ^ m))));
+  }
+}
+
+/* delta[idx] = prod_i (bit_i(idx) ? p[n-1-i] : 1 - p[n-1-i]) -- n mults per entry */
+void orc_eq_table(const uint8_t* pts, uint32_t n, uint8_t* out) {
+  for (uint64_t idx = 0; idx < (1ull << n); idx++) {
+    u128 acc = 1;
+    for (uint32_t i = 0; i < n; i++) {
+      u128 p = ld(pts + 16 * (n - 1 - i));
+      acc = fmul(acc, ((idx >> i) & 1) ? p : fsub(1, p));
+    }
+    st(out + 16 * idx, acc);
+  }
+}
+
+/* partial_sum at X=1 and X=2 (sumcheck.rs:204-232), composition x[0]. */
+void orc_partial_sums(const uint8_t* m, const uint8_t* d, uint32_t log_h, uint8_t out[32]) {
+  uint64_t off = (1ull << log_h) / 2;
+  u128 s1 = 0, s2 = 0;
+  for (uint64_t i = 0; i < off; i++) s1 = fadd(s1, fmul(ld(m + 16 * (i + off)), ld(d + 16 * (i + off))));
+  u128 r = 2, s = fsub(1, r);
+  for (uint64_t i = 0; i < off; i++) {
+    u128 dd = fadd(fmul(s, ld(d + 16 * i)), fmul(r, ld(d + 16 * (i + off))));
+    u128 mm = fadd(fmul(s, ld(m + 16 * i)), fmul(r, ld(m + 16 * (i + off))));
+    s2 = fadd(s2, fmul(mm, dd));
+  }
+  st(out, s1);
+  st(out + 16, s2);
+}
+
+/* fold (sumcheck.rs:234-247), in place */
+void orc_fold(uint8_t* m, uint8_t* d, uint32_t log_h, const uint8_t rb[16]) {
+  uint64_t off = (1ull << log_h) / 2;
+  u128 r = ld(rb), s = fsub(1, r);
+  for (uint64_t i = 0; i < off; i++) {
+    st(d + 16 * i, fadd(fmul(s, ld(d + 16 * i)), fmul(r, ld(d + 16 * (i + off)))));
+    st(m + 16 * i, fadd(fmul(s, ld(m + 16 * i)), fmul(r, ld(m + 16 * (i + off)))));
+  }
+}
+
+/* field op KATs for the tests */
+void orc_mul(const uint8_t a[16], const uint8_t b[16], uint8_t out[16]) {
+  st(out, fmul(ld(a), ld(b)));
+}

@@ -1,0 +1,111 @@
+"""ctypes binding of the C oracle (oracle/liboracle.so).  Test infrastructure only."""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise ImportError("oracle/liboracle.so not built (make -C oracle)")
+        L = ctypes.CDLL(path)
+        P = ctypes.c_void_p
+        U = ctypes.c_uint32
+        L.orc_ntt.argtypes = [P, P, U, P, ctypes.c_int]
+        L.orc_reed_solomon.argtypes = [P, U, P, P]
+        L.orc_merkle_commit_pairs.argtypes = [P, U, P]
+        L.orc_fri_commit.argtypes = [P, U, P, P, P]
+        L.orc_to_coefficient.argtypes = [P, U]
+        L.orc_eq_table.argtypes = [P, U, P]
+        L.orc_partial_sums.argtypes = [P, P, U, P]
+        L.orc_fold.argtypes = [P, P, U, P]
+        L.orc_sha256.argtypes = [P, ctypes.c_uint64, P]
+        L.orc_mul.argtypes = [P, P, P]
+        L.orc_pow_2_generator.argtypes = [U, P]
+        L.orc_pow_2_generator_powers.argtypes = [U, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _fe(v):
+    return np.frombuffer(int(v).to_bytes(16, "little"), dtype=np.uint8).copy()
+
+
+def ntt(limbs, log_n, gen, inverse=False):
+    """limbs: (n,4) uint32 array -> new array."""
+    a = np.ascontiguousarray(limbs, dtype=np.uint32)
+    out = np.empty_like(a)
+    g = _fe(gen)
+    rc = lib().orc_ntt(_p(a), _p(out), log_n, _p(g), 1 if inverse else 0)
+    assert rc == 0
+    return out
+
+
+def reed_solomon(limbs, log_n, gen):
+    a = np.ascontiguousarray(limbs, dtype=np.uint32)
+    out = np.empty((2 * a.shape[0], 4), dtype=np.uint32)
+    rc = lib().orc_reed_solomon(_p(a), log_n, _p(_fe(gen)), _p(out))
+    assert rc == 0
+    return out
+
+
+def merkle_commit_pairs(limbs, log_code):
+    a = np.ascontiguousarray(limbs, dtype=np.uint32)
+    L = 1 << (log_code - 1)
+    layers = np.empty((2 * L - 1, 32), dtype=np.uint8)
+    lib().orc_merkle_commit_pairs(_p(a), log_code, _p(layers))
+    return layers
+
+
+def fri_commit(limbs, log_code):
+    """-> (roots list, last_elem int, last_random bytes, rc)."""
+    a = np.ascontiguousarray(limbs, dtype=np.uint32)
+    roots = np.zeros((log_code - 1, 32), dtype=np.uint8)
+    last = np.zeros(16, dtype=np.uint8)
+    lr = np.zeros(32, dtype=np.uint8)
+    rc = lib().orc_fri_commit(_p(a), log_code, _p(roots), _p(last), _p(lr))
+    return [bytes(r) for r in roots], int.from_bytes(bytes(last), "little"), bytes(lr), rc
+
+
+def to_coefficient(limbs, log_n):
+    a = np.ascontiguousarray(limbs, dtype=np.uint32).copy()
+    lib().orc_to_coefficient(_p(a), log_n)
+    return a
+
+
+def eq_table(points):
+    pts = np.frombuffer(b"".join(int(p).to_bytes(16, "little") for p in points) or b"\0" * 16,
+                        dtype=np.uint8).copy()
+    out = np.empty((1 << len(points), 4), dtype=np.uint32)
+    lib().orc_eq_table(_p(pts), len(points), _p(out))
+    return out
+
+
+def partial_sums(m, d, log_h):
+    out = np.zeros(32, dtype=np.uint8)
+    lib().orc_partial_sums(_p(np.ascontiguousarray(m)), _p(np.ascontiguousarray(d)), log_h, _p(out))
+    b = bytes(out)
+    return int.from_bytes(b[:16], "little"), int.from_bytes(b[16:], "little")
+
+
+def sha256(msg: bytes) -> bytes:
+    buf = np.frombuffer(msg, dtype=np.uint8).copy() if msg else np.zeros(1, dtype=np.uint8)
+    out = np.zeros(32, dtype=np.uint8)
+    lib().orc_sha256(_p(buf), len(msg), _p(out))
+    return bytes(out)
+
+
+def mul(a, b):
+    out = np.zeros(16, dtype=np.uint8)
+    lib().orc_mul(_p(_fe(a)), _p(_fe(b)), _p(out))
+    return int.from_bytes(bytes(out), "little")

@@ -1,0 +1,432 @@
+"""GPU parity: libmlhip (HIP kernels through the C ABI) vs the CPU oracle.
+
+Bit-exact comparisons (integer field work) on seeded inputs at sizes the
+Python oracle finishes in seconds, plus the reference's own test patterns
+(coeffs 0..N, ntt/mod.rs:185; values 7i+3, fri/mod.rs:352 and
+multilinear_pcs.rs:218) and edge cases (n = 2, non-generators, bad sizes).
+"""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from oracle import field as F  # noqa: E402  (checker only)
+from oracle import fri as OF  # noqa: E402
+from oracle import merkle as OM  # noqa: E402
+from oracle import ntt as ON  # noqa: E402
+from oracle import pcs as OP  # noqa: E402
+from oracle import polynomials as OPL  # noqa: E402
+from oracle import sumcheck as OS  # noqa: E402
+from oracle import transcript as OT  # noqa: E402
+
+from multilinear_amd import _lib  # noqa: E402
+from multilinear_amd import device as D  # noqa: E402
+from multilinear_amd import fri as MF  # noqa: E402
+from multilinear_amd import merkle_tree as MM  # noqa: E402
+from multilinear_amd import multilinear_pcs as MP  # noqa: E402
+from multilinear_amd import ntt as MN  # noqa: E402
+from multilinear_amd import polynomials as MPL  # noqa: E402
+from multilinear_amd import sumcheck as MS  # noqa: E402
+from multilinear_amd.transcript import Transcript  # noqa: E402
+
+
+def dev(values):
+    return D.to_device(D.ints_to_limbs(values))
+
+
+def host(t):
+    return D.limbs_to_ints(D.from_device(t))
+
+
+def rand_vals(n, seed):
+    r = random.Random(seed)
+    return [r.randrange(F.M) for _ in range(n)]
+
+
+# ---- NTT -------------------------------------------------------------------
+
+@pytest.mark.parametrize("log_n", list(range(1, 15)) + [16])
+def test_ntt_matches_oracle(log_n):
+    n = 1 << log_n
+    g = F.pow_2_generator(log_n)
+    for coeffs in ([F.from_i64(i) for i in range(n)], rand_vals(n, log_n)):
+        want = ON.ntt(coeffs, g)
+        got = host(MN.Polynomial(dev(coeffs)).ntt(g).evals)
+        assert got == want
+
+
+@pytest.mark.parametrize("log_n", [1, 2, 5, 10, 11, 12, 13, 17, 18, 19, 20])
+def test_intt_roundtrip(log_n):
+    """intt_test (ntt/mod.rs:191-201): INTT(NTT(x)) == x."""
+    n = 1 << log_n
+    g = F.pow_2_generator(log_n)
+    x = D.random_device(n, 1234 + log_n)
+    lag = MN.Polynomial(x).ntt(g)
+    back = lag.intt().coeffs
+    assert bool((back == x).all())
+
+
+@pytest.mark.parametrize("log_n", [3, 11, 14])
+def test_intt_matches_oracle(log_n):
+    n = 1 << log_n
+    g = F.pow_2_generator(log_n)
+    ev = rand_vals(n, 99 + log_n)
+    got = host(MN.LagrangePolynomial(g, dev(ev)).intt().coeffs)
+    assert got == ON.intt(ev, g)
+
+
+def test_ntt_in_place_and_host_path():
+    import ctypes
+
+    log_n = 12
+    n = 1 << log_n
+    g = F.pow_2_generator(log_n)
+    vals = rand_vals(n, 5)
+    x = dev(vals)
+    ctx = D.context()
+    D.check(D.lib().mlh_ntt(ctx, D.ptr(x), D.ptr(x), log_n, D.fe_bytes(g)), ctx)
+    want = ON.ntt(vals, g)
+    assert host(x) == want
+    src = D.ints_to_limbs(vals).tobytes()
+    inb = (ctypes.c_uint8 * len(src)).from_buffer_copy(src)
+    outb = (ctypes.c_uint8 * len(src))()
+    D.check(D.lib().mlh_ntt_host(ctx, inb, outb, log_n, D.fe_bytes(g), 0), ctx)
+    assert D.limbs_to_ints(np.frombuffer(bytes(outb), dtype=np.uint32)) == want
+
+
+def test_ntt_rejects_bad_inputs():
+    ctx = D.context()
+    x = dev(list(range(16)))
+    # not a generator of order 16
+    st = D.lib().mlh_ntt(ctx, D.ptr(x), D.ptr(x), 4, D.fe_bytes(F.pow_2_generator(5)))
+    assert st == 3
+    st = D.lib().mlh_ntt(ctx, D.ptr(x), D.ptr(x), 0, D.fe_bytes(1))
+    assert st == 2
+
+
+def test_bit_reverse_and_generator_powers():
+    vals = rand_vals(1 << 10, 7)
+    got = host(MN.bit_reverse_permutation(dev(vals)))
+    want = list(vals)
+    ON.bit_reverse_permutation(want)
+    assert got == want
+    for ls in (3, 12, 13):
+        assert host(MN.pow_2_generator_powers(ls)) == F.pow_2_generator_powers(ls)
+    assert MN.pow_2_generator(40) == F.WINTER_TWO_ADIC_ROOT
+    assert MN.pow_2_generator(41) is None
+
+
+# ---- Reed-Solomon / Merkle ---------------------------------------------------
+
+@pytest.mark.parametrize("log_n", [1, 4, 10, 12])
+def test_reed_solomon_matches_oracle(log_n):
+    n = 1 << log_n
+    vals = [F.from_i64(7 * i + 3) for i in range(n)]
+    g = F.pow_2_generator(log_n + 1)
+    assert host(MF.reed_solomon(dev(vals), g)) == OF.reed_solomon(vals, g)
+
+
+@pytest.mark.parametrize("log_code", [1, 2, 3, 11, 13])
+def test_merkle_commit_pairs_matches_oracle(log_code):
+    code = rand_vals(1 << log_code, 31 + log_code)
+    want = OF.commit_rs_code(code)
+    got = MM.Merkle.commit_pairs(dev(code))
+    assert got.root() == want.root()
+    gl = got.layers()
+    assert len(gl) == len(want.layers)
+    for a, b in zip(gl, want.layers):
+        assert [bytes(x) for x in a] == b
+
+
+def test_merkle_commit_generic_items():
+    """merkle_test (merkle_tree/mod.rs:300-309) data, 1-byte items."""
+    data = [bytes([v]) for v in [0, 8, 4, 1, 5, 7, 6, 1]]
+    got = MM.Merkle.commit(data)
+    want = OM.Merkle.commit(data)
+    assert got.root() == want.root()
+    value, path = want.open(5)
+    assert OM.verify(value, path, got.root(), 5)
+    # longer items cross SHA-256 block boundaries
+    items = [bytes(random.Random(i).randrange(256) for _ in range(100)) for i in range(16)]
+    assert MM.Merkle.commit(items).root() == OM.Merkle.commit(items).root()
+
+
+def test_merkle_batch_commit():
+    """batched_merkle_test (merkle_tree/mod.rs:311-351)."""
+    data = [[bytes([v]) for v in [0, 8, 4, 1, 5, 7, 6, 1]],
+            [bytes([v]) for v in [1, 3, 2, 3, 2, 1, 2, 3]]]
+    assert MM.Merkle.batch_commit(data).root() == OM.Merkle.batch_commit(data).root()
+
+
+# ---- FRI ---------------------------------------------------------------------
+
+@pytest.mark.parametrize("log_domain,k", [(11, 0), (11, 3), (13, 0), (13, 11), (14, 5)])
+def test_fri_fold_matches_oracle(log_domain, k):
+    n = 1 << (log_domain - k)
+    layer = rand_vals(n, 1000 + k)
+    r = rand_vals(1, 77)[0]
+    gp = F.pow_2_generator_powers(log_domain)
+    pairs = [(layer[i], layer[i + n // 2]) for i in range(n // 2)]
+    want = OF.fold_layer(pairs, gp, k, r)
+    assert host(MF.fold_layer(dev(layer), k, log_domain, r)) == want
+
+
+def _fri_oracle(log_n, vals):
+    gp = F.pow_2_generator_powers(log_n + 1)
+    code = OF.reed_solomon(vals, gp[1])
+    return code, OF.FriProof.prove(code, gp, OT.Transcript())
+
+
+@pytest.mark.parametrize("log_n", [1, 2, 5, 10])
+def test_fri_prove_matches_oracle(log_n):
+    """prove_and_verify_test (fri/mod.rs:349-363): values 7i+3."""
+    vals = [F.from_i64(7 * i + 3) for i in range(1 << log_n)]
+    code, want = _fri_oracle(log_n, vals)
+    dcode = dev(code)
+    got = MF.FriProof.prove(dcode, Transcript())
+    assert got.commitments == want.commitments
+    assert got.last_elem == want.last_elem
+    assert got.last_random == want.last_random
+    for q in range(_lib.NUM_QUERIES):
+        gq = got.query(q)
+        wq = want.queries[q]
+        assert len(gq) == len(wq)
+        for (gv, gs), (wv, wpath) in zip(gq, wq):
+            assert gv == wv
+            assert gs == [s for s, _ in wpath]
+    assert got.verify()
+    assert want.verify()
+
+
+def test_fri_verify_rejects_tampering():
+    vals = [F.from_i64(7 * i + 3) for i in range(1 << 6)]
+    code, _ = _fri_oracle(6, vals)
+    p = MF.FriProof.prove(dev(code), Transcript())
+    assert p.verify()
+    p._q[40] ^= 1
+    assert not p.verify()
+
+
+def test_fri_prover_step_api():
+    """FriProverData::init / fold_step / open_query_at used step by step."""
+    log_n = 8
+    vals = rand_vals(1 << log_n, 3)
+    gp = F.pow_2_generator_powers(log_n + 1)
+    code = OF.reed_solomon(vals, gp[1])
+    otr = OT.Transcript()
+    opd = OF.FriProverData.fold(gp, code, otr)
+    tr = Transcript()
+    dcode = dev(code)
+    pd = MF.FriProverData.init(dcode, tr)
+    for k in range(log_n):
+        r = tr.next_challenge()
+        pd.fold_step(k, r, tr)
+    assert pd.fold_roots() == opd.fold_roots()
+    assert pd.last_element == opd.last_element
+    assert tr.random() == otr.random()
+    q = pd.open_query_at(37, log_n + 1)
+    wq = opd.open_query_at(37)
+    assert [v for v, _ in q] == [v for v, _ in wq]
+
+
+def test_fri_not_rs_code():
+    """fold of a non-codeword hits the reference's "not an RS code" assert."""
+    log_code = 6
+    code = rand_vals(1 << log_code, 11)
+    with pytest.raises(_lib.MlhError) as e:
+        MF.FriProof.prove(dev(code), Transcript())
+    assert e.value.status == 6
+
+
+# ---- multilinear / sumcheck / PCS -------------------------------------------
+
+@pytest.mark.parametrize("log_n", [1, 3, 8, 11, 17])
+def test_mobius_and_zeta(log_n):
+    ev = rand_vals(1 << log_n, 50 + log_n)
+    dv = dev(ev)
+    c = MPL.to_coefficient(dv)
+    if log_n <= 11:
+        assert host(c) == OPL.to_coefficient(ev)
+    assert bool((MPL.to_evaluation(c) == dv).all())
+
+
+def test_eq_table_and_evaluate():
+    for n in (1, 2, 5, 9, 12):
+        pts = rand_vals(n, 600 + n)
+        assert host(MPL.eq_table(pts)) == OS.eq_table(pts)
+        assert OS.eq_table(pts)[: 1 << min(n, 4)] == [OS.mask_evaluate(i, n, pts) for i in range(1 << min(n, 4))]
+    n = 10
+    ev = rand_vals(1 << n, 4)
+    args = rand_vals(n, 5)
+    assert MPL.evaluate(dev(ev), args) == OPL.mle_evaluate(ev, args)
+
+
+def test_sumcheck_rounds_match_oracle():
+    n = 10
+    ev = rand_vals(1 << n, 8)
+    pts = rand_vals(n, 9)
+    ot = OS.SumcheckTables.build_tables_for_pcs(pts, ev)
+    mt = MS.SumcheckTables.build_tables_for_pcs(pts, dev(ev))
+    assert mt.partial_sums() == (ot.partial_sum(1), ot.partial_sum(2))
+    r = rand_vals(1, 10)[0]
+    ot.fold(r)
+    mt.fold(r)
+    assert host(mt.matrix)[: 1 << (n - 1)] == ot.matrix
+    assert host(mt.delta)[: 1 << (n - 1)] == ot.delta
+    assert mt.partial_sums() == (ot.partial_sum(1), ot.partial_sum(2))
+    # full prove against the oracle's round loop
+    total = OPL.mle_evaluate(ev, pts)
+    ot2 = OS.SumcheckTables.build_tables_for_pcs(pts, ev)
+    otr = OT.Transcript()
+    prev = total
+    want_polys, want_rs = [], []
+    for _ in range(n):
+        nz, r2, prev = ot2.compute_sumcheck_polynomial(prev, otr)
+        want_polys.append(tuple(nz))
+        want_rs.append(r2)
+    mt2 = MS.SumcheckTables.build_tables_for_pcs(pts, dev(ev))
+    tr = Transcript()
+    polys, rs = mt2.compute_sumcheck_polynomials(total, tr)
+    assert polys == want_polys
+    assert rs == want_rs
+    assert tr.random() == otr.random()
+
+
+@pytest.mark.parametrize("n", [1, 2, 8, 10])
+def test_pcs_prove_matches_oracle(n):
+    """multilinear_pcs_bench_test pattern: evals 7i+3, point (0..n)."""
+    ev = [F.from_i64(7 * i + 3) for i in range(1 << n)]
+    inputs = [F.from_i64(i) for i in range(n)]
+    out = OPL.mle_evaluate(ev, inputs)
+    want = OP.PCSProof.prove(inputs, out, ev, OT.Transcript())
+    got = MP.PCSProof.prove(inputs, out, dev(ev), Transcript())
+    assert got.sumcheck_polynomials == [tuple(p) for p in want.sumcheck_polynomials]
+    assert got.fri_proof.commitments == want.fri_proof.commitments
+    assert got.fri_proof.last_elem == want.fri_proof.last_elem
+    assert got.fri_proof.last_random == want.fri_proof.last_random
+    assert got.verify(Transcript())
+    assert want.verify(OT.Transcript())
+
+
+def test_pcs_random_point():
+    n = 9
+    ev = rand_vals(1 << n, 21)
+    inputs = rand_vals(n, 22)
+    out = OPL.mle_evaluate(ev, inputs)
+    got = MP.PCSProof.prove(inputs, out, dev(ev), Transcript())
+    want = OP.PCSProof.prove(inputs, out, ev, OT.Transcript())
+    assert got.fri_proof.last_random == want.fri_proof.last_random
+    assert got.verify(Transcript())
+    # wrong claimed output -> verifier rejects
+    bad = MP.PCSProof.prove(inputs, (out + 1) % F.M, dev(ev), Transcript())
+    assert not bad.verify(Transcript())
+
+
+# ---- full-size properties (BASELINE configs) ----------------------------------
+
+def _sum_mod(t):
+    a = D.from_device(t).astype(np.uint64)
+    s = [int(a[:, i].sum()) for i in range(4)]
+    return (s[0] + (s[1] << 32) + (s[2] << 64) + (s[3] << 96)) % F.M
+
+
+def _alt_sum_mod(t):
+    a = D.from_device(t).astype(np.uint64)
+    ev, od = a[0::2], a[1::2]
+    s = [int(ev[:, i].sum()) - int(od[:, i].sum()) for i in range(4)]
+    return (s[0] + (s[1] << 32) + (s[2] << 64) + (s[3] << 96)) % F.M
+
+
+@pytest.mark.slow
+def test_ntt_2_24_properties():
+    """Config 2: 2^24 forward + inverse, bit-exact round trip; evals[0] =
+    sum(c), evals[N/2] = alternating sum (size-independent identities)."""
+    log_n = 24
+    g = F.pow_2_generator(log_n)
+    x = D.random_device(1 << log_n, 2024)
+    ev = MN.Polynomial(x).ntt(g).evals
+    e = D.from_device(ev[[0, 1 << (log_n - 1)]])
+    vals = D.limbs_to_ints(e)
+    assert vals[0] == _sum_mod(x)
+    assert vals[1] == _alt_sum_mod(x)
+    back = MN.LagrangePolynomial(g, ev).intt().coeffs
+    assert bool((back == x).all())
+
+
+@pytest.mark.slow
+def test_fri_commit_2_24_verifies():
+    """Config 3 shape: 2^24 coefficients -> RS code 2^25 -> full FRI prove,
+    accepted by the verifier; code[0] == sum(coeffs)."""
+    log_n = 24
+    x = D.random_device(1 << log_n, 77)
+    g = F.pow_2_generator(log_n + 1)
+    code = MF.reed_solomon(x, g)
+    assert D.limbs_to_ints(D.from_device(code[:1]))[0] == _sum_mod(x)
+    p = MF.FriProof.prove(code, Transcript())
+    assert p.verify()
+
+
+@pytest.mark.parametrize("plan", ["4,4,4", "4,8,4", "8,4,4", "4,4,8", "5,5,5", "4,9,4",
+                                  "4,4,4,4", "6,5,4"])
+def test_ntt_forced_radix_plans(plan, monkeypatch):
+    """Every pass shape (first / middle / last, radix 2^4..2^9, 3-4 passes) at
+    oracle-sized N via the MLH_NTT_PLAN test hook."""
+    monkeypatch.setenv("MLH_NTT_PLAN", plan)
+    log_n = sum(int(v) for v in plan.split(","))
+    n = 1 << log_n
+    g = F.pow_2_generator(log_n)
+    vals = rand_vals(n, 4242 + log_n)
+    got = MN.Polynomial(dev(vals)).ntt(g)
+    assert host(got.evals) == ON.ntt(vals, g)
+    assert host(got.intt().coeffs) == vals
+    # RS LDE (zero-padded first pass) with the same plan on 2^log_n outputs
+    half = vals[: n // 2]
+    assert host(MF.reed_solomon(dev(half), g)) == OF.reed_solomon(half, g)
+
+
+# ---- full-size parity against the C restatement of the reference loops ---------
+
+def _c_oracle():
+    from oracle import coracle
+
+    coracle.lib()
+    return coracle
+
+
+@pytest.mark.parametrize("log_n", [15, 17, 19, 20, 21, 22, 23,
+                                   pytest.param(24, marks=pytest.mark.slow)])
+def test_ntt_vs_c_oracle(log_n):
+    C = _c_oracle()
+    g = F.pow_2_generator(log_n)
+    x = D.random_limbs(1 << log_n, 900 + log_n)
+    want = C.ntt(x, log_n, g)
+    got = D.from_device(MN.Polynomial(D.to_device(x)).ntt(g).evals)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, "first mismatches at %s of %d" % (bad[:8].tolist(), bad.size)
+
+
+@pytest.mark.parametrize("log_n", [18, 21])
+def test_intt_vs_c_oracle(log_n):
+    C = _c_oracle()
+    g = F.pow_2_generator(log_n)
+    x = D.random_limbs(1 << log_n, 300 + log_n)
+    want = C.ntt(x, log_n, g, inverse=True)
+    got = D.from_device(MN.LagrangePolynomial(g, D.to_device(x)).intt().coeffs)
+    assert (got == want).all()
+
+
+@pytest.mark.parametrize("log_n", [17, 20])
+def test_reed_solomon_and_fri_commit_vs_c_oracle(log_n):
+    C = _c_oracle()
+    g = F.pow_2_generator(log_n + 1)
+    x = D.random_limbs(1 << log_n, 500 + log_n)
+    want = C.reed_solomon(x, log_n, g)
+    dcode = MF.reed_solomon(D.to_device(x), g)
+    assert (D.from_device(dcode) == want).all()
+    roots, last, lr, rc = C.fri_commit(want, log_n + 1)
+    assert rc == 0
+    pd = MF.FriProverData.fold(dcode, Transcript())
+    assert pd.fold_roots() == roots
+    assert pd.last_element == last
