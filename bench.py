@@ -1,0 +1,274 @@
+"""bench.py -- headline benchmark (BASELINE.json metric) on 1..8 MI355X.
+
+Metric: "NTT 2^24 field-elems/sec + FRI commit ms; % HBM roofline".
+  * step  = one forward 2^24-point NTT (config 2, src/ntt/mod.rs:69-110) over
+            a device-resident synthetic vector (seeded uniform field elements);
+  * value = 2^24 * steps * world_size / max-over-ranks(time of the K steps)
+            (weak scaling: each rank transforms its own polynomial; the path
+            has no exchange step at this size, DESIGN.md "Multi-GPU");
+  * extra lines in the same JSON: inverse NTT, FRI commit (config 3:
+    2^24 coeffs -> RS LDE 2^25 -> Merkle root on host), full FRI prove and
+    the 24-round sumcheck (config 4), each timed after the headline loop;
+  * roofline: the dominant kernel (ntt_pass<8,0,0>) timed live with HIP
+    events on its launch stream over the headline loop; algorithmic bytes per
+    launch = 32 B x 2^24 (each element read once and written once);
+  * cpu_baseline: the oracle's C restatement of the reference NTT
+    (oracle/liboracle.so, 1 thread) on one 2^24 NTT, rank 0 at N = 1 only.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      torchrun --nproc-per-node N bench.py --gpus N ...  (one rank per GPU)
+"""
+import argparse
+import ctypes
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK = 7.864e13   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz full-rate lane-ops/s
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def cpu_baseline(log_n):
+    """Oracle C restatement of the reference CPU NTT, 1 thread (bench leg only)."""
+    from multilinear_amd import device as D
+    from oracle import coracle
+    from oracle import field as F
+
+    x = D.random_limbs(1 << log_n, 1)
+    g = F.pow_2_generator(log_n)
+    t0 = time.perf_counter()
+    coracle.ntt(x, log_n, g)
+    dt = time.perf_counter() - t0
+    return {
+        "value": (1 << log_n) / dt,
+        "unit": "field-elems/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": "one 2^%d-point forward NTT, C restatement of src/ntt/mod.rs:69-110 "
+                  "(bit-reverse + serial-twiddle DIT), %.2f s; host %s, nproc %d"
+                  % (log_n, dt, cpu_model(), os.cpu_count() or 0),
+    }
+
+
+def load_pmc(kernel, log_n):
+    """HBM traffic per launch from the committed rocprofv3 PMC summary, if it
+    matches this kernel/size (tools/pmc_summary.py writes it)."""
+    path = os.path.join(ROOT, "profiles", "pmc_ntt.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("kernel") == kernel and d.get("log_n") == log_n:
+        return d.get("traffic_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=24)
+    ap.add_argument("--extra-reps", type=int, default=3, help="reps of the secondary timings")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from multilinear_amd import device as D
+    from multilinear_amd import fri as MF
+    from multilinear_amd.transcript import Transcript
+
+    log_n = args.log_n
+    N = 1 << log_n
+    lib = D.lib()
+    ctx = D.context(local)
+    gen = D.fe_bytes(int.from_bytes(bytes(_gen(lib, log_n)), "little"))
+    x = D.random_device(N, 1000 + rank, local)
+    out = D.empty(N, local)
+
+    def ntt_once():
+        D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(out), log_n, gen), ctx)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        ntt_once()
+    barrier()
+    lib.mlh_profile_reset(ctx)
+    lib.mlh_profile_enable(ctx, 1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ntt_once()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    lib.mlh_profile_enable(ctx, 0)
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    barrier()
+
+    # dominant kernel timing (HIP events on the launch stream, timed region)
+    kernels = {}
+    for lab in ("ntt_pass<8,0,0>", "ntt_pass<8,1,0>", "ntt_pass<9,0,0>", "ntt_pass<9,1,0>",
+                "ntt_pass<7,0,0>", "ntt_pass<7,1,0>"):
+        cnt = ctypes.c_uint64()
+        tot = ctypes.c_double()
+        lib.mlh_profile_get(ctx, lab.encode(), ctypes.byref(cnt), ctypes.byref(tot))
+        if cnt.value:
+            kernels[lab] = {"launches": cnt.value, "avg_ms": tot.value / cnt.value}
+    dom = max(kernels.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
+    dom_name, dom_stat = dom
+    alg_bytes = 32.0 * N  # one read + one write of every 16-B element per launch
+    achieved_gbs = alg_bytes / (dom_stat["avg_ms"] * 1e-3) / 1e9
+    traffic = load_pmc(dom_name, log_n)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = N * args.steps * world / elapsed
+    result = {
+        "metric": "NTT 2^24 field-elems/sec + FRI commit ms; % HBM roofline at 1/2/4/8 GPUs",
+        "value": value,
+        "unit": "field-elems/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u128 mod M (F_M, M = 2^128 - 45*2^40 + 1)",
+        "data": "synthetic: seeded uniform field elements generated on device",
+        "config": {
+            "workload": "config 2: forward 2^%d-point NTT per step, natural order in/out, "
+                        "device resident" % log_n,
+            "log_n": log_n,
+            "parallelism": "replicas x%d (independent polynomial per GPU)" % world,
+        },
+        "ntt_hbm_frac": (32.0 * N / (ms_per_step * 1e-3) / 1e9) / HBM_PEAK_GBS,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom_name,
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "launch_avg_ms": dom_stat["avg_ms"],
+            "alg_bytes_per_launch": alg_bytes,
+        },
+        "kernels": kernels,
+    }
+
+    if not args.no_extras:
+        reps = args.extra_reps
+        # inverse NTT
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            D.check(lib.mlh_intt(ctx, D.ptr(out), D.ptr(x), log_n, gen), ctx)
+        torch.cuda.synchronize()
+        result["intt_ms"] = (time.perf_counter() - t0) / reps * 1e3
+        # FRI commit (config 3): coeffs (2^log_n) -> RS code -> Merkle root
+        code = D.empty(2 * N, local)
+        layers = torch.empty((N * 2 - 1, 32), dtype=torch.uint8, device="cuda:%d" % local)
+        g2 = D.fe_bytes(int.from_bytes(bytes(_gen(lib, log_n + 1)), "little"))
+        root = (ctypes.c_uint8 * 32)()
+
+        def fri_commit():
+            D.check(lib.mlh_reed_solomon(ctx, D.ptr(x), log_n, g2, D.ptr(code)), ctx)
+            D.check(lib.mlh_merkle_commit_pairs(ctx, D.ptr(code), log_n + 1, D.ptr(layers), root), ctx)
+
+        fri_commit()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fri_commit()
+        torch.cuda.synchronize()
+        fc_ms = (time.perf_counter() - t0) / reps * 1e3
+        fc_bytes = 16 * N + 32 * N + 32 * N + 32 * (2 * N - 1)
+        result["fri_commit_ms"] = fc_ms
+        result["fri_commit_hbm_frac"] = fc_bytes / (fc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+        # full FRI prove (fold, 24 trees, 128 queries) on the same code
+        t0 = time.perf_counter()
+        p = MF.FriProof.prove(code, Transcript(), local)
+        torch.cuda.synchronize()
+        result["fri_prove_ms"] = (time.perf_counter() - t0) * 1e3
+        result["fri_prove_verified"] = bool(p.verify())
+        del layers
+        # sumcheck (config 4): 24 rounds over evals (2^log_n) with a random point
+        import random
+
+        from multilinear_amd import polynomials as MPL
+        from multilinear_amd import sumcheck as MS
+
+        rr = random.Random(5)
+        M = D.M
+        pts = [rr.randrange(M) for _ in range(log_n)]
+        t0 = time.perf_counter()
+        delta = MPL.eq_table(pts, local)
+        torch.cuda.synchronize()
+        result["eq_table_ms"] = (time.perf_counter() - t0) * 1e3
+        m = x.clone()
+        tabs = MS.SumcheckTables(m, delta)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tabs.compute_sumcheck_polynomials(0, Transcript(), local)
+        torch.cuda.synchronize()
+        sc_ms = (time.perf_counter() - t0) * 1e3
+        result["sumcheck_ms"] = sc_ms
+        sc_bytes = sum(48 * (N >> k) for k in range(log_n))
+        result["sumcheck_hbm_frac"] = sc_bytes / (sc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(log_n)
+        result["vs_cpu_1core"] = value / result["cpu_baseline"]["value"]
+
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def _gen(lib, log_n):
+    out = (ctypes.c_uint8 * 16)()
+    lib.mlh_pow_2_generator(log_n, out)
+    return out
+
+
+if __name__ == "__main__":
+    main()

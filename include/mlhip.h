@@ -205,6 +205,13 @@ mlh_status mlh_pcs_verify(const mlh_pcs_proof* proof, uint32_t n_vars, const uin
                           const uint8_t output[16], mlh_transcript* tr);
 
 /* ---- device timing helpers (bench / profiling) --------------------------- */
+/* Kernel timer: while enabled, every NTT pass launch is bracketed by HIP
+ * events on the context stream; mlh_profile_get (synchronising) returns the
+ * launch count and summed milliseconds for a kernel label such as
+ * "ntt_pass<8,0,0>" (radix log2, last pass, zero-padded input). */
+mlh_status mlh_profile_enable(mlh_ctx* ctx, int on);
+mlh_status mlh_profile_reset(mlh_ctx* ctx);
+mlh_status mlh_profile_get(mlh_ctx* ctx, const char* label, uint64_t* count, double* total_ms);
 /* Time `iters` forward NTTs of 2^log_n on the context stream with HIP events
  * (dev_buf is transformed in place); returns the mean ms per NTT. */
 mlh_status mlh_bench_ntt(mlh_ctx* ctx, void* dev_buf, uint32_t log_n, uint32_t iters,

@@ -108,6 +108,9 @@ SIGNATURES = {
     "mlh_pcs_prove": (_I, [_P, _P, _U32, _P, _P, _P, ctypes.POINTER(PcsProofC)]),
     "mlh_pcs_verify": (_I, [ctypes.POINTER(PcsProofC), _U32, _P, _P, _P]),
     "mlh_bench_ntt": (_I, [_P, _P, _U32, _U32, ctypes.POINTER(ctypes.c_float)]),
+    "mlh_profile_enable": (_I, [_P, _I]),
+    "mlh_profile_reset": (_I, [_P]),
+    "mlh_profile_get": (_I, [_P, ctypes.c_char_p, ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_double)]),
 }
 
 _lib = None

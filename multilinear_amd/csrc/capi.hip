@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <string>
@@ -55,7 +56,48 @@ struct mlh_ctx {
   uint8_t* pinned = nullptr;          // 4 KiB pinned host staging
   fe* ntt_scratch = nullptr;          // NTT ping-pong buffer (grow-only)
   size_t ntt_scratch_bytes = 0;
+  // kernel timer (mlh_profile_*): HIP events on the launch stream
+  bool prof_on = false;
+  std::vector<hipEvent_t> ev_free;
+  struct Pending {
+    std::string label;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::map<std::string, std::pair<uint64_t, double>> prof;  // label -> (count, total ms)
 };
+
+static hipEvent_t take_event(mlh_ctx* ctx) {
+  if (!ctx->ev_free.empty()) {
+    hipEvent_t e = ctx->ev_free.back();
+    ctx->ev_free.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+static void resolve_profile(mlh_ctx* ctx) {
+  for (auto& p : ctx->pending) {
+    (void)hipEventSynchronize(p.b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    auto& slot = ctx->prof[p.label];
+    slot.first += 1;
+    slot.second += ms;
+  }
+  // events are shared between consecutive pairs: collect unique ones
+  std::vector<hipEvent_t> evs;
+  for (auto& p : ctx->pending) {
+    evs.push_back(p.a);
+    evs.push_back(p.b);
+  }
+  std::sort(evs.begin(), evs.end());
+  evs.erase(std::unique(evs.begin(), evs.end()), evs.end());
+  for (auto e : evs) ctx->ev_free.push_back(e);
+  ctx->pending.clear();
+}
 
 struct mlh_transcript {
   HostSha256 sha;
@@ -211,6 +253,18 @@ static mlh_status ntt_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, 
     HIP_TRY(ctx, hipMalloc(&ctx->ntt_scratch, need));
     ctx->ntt_scratch_bytes = need;
   }
+  if (ctx->prof_on) {
+    std::vector<hipEvent_t> ev(tb.nradix + 1);
+    for (auto& e : ev) e = take_event(ctx);
+    HIP_TRY(ctx, launch_ntt_passes(in, out, ctx->ntt_scratch, tb, log_n, zero_top, ctx->stream,
+                                   ev.data()));
+    for (uint32_t p = 0; p < tb.nradix; ++p) {
+      char lab[64];
+      ntt_pass_label(tb, p, zero_top, lab, sizeof lab);
+      ctx->pending.push_back(mlh_ctx::Pending{lab, ev[p], ev[p + 1]});
+    }
+    return MLH_OK;
+  }
   HIP_TRY(ctx, launch_ntt_passes(in, out, ctx->ntt_scratch, tb, log_n, zero_top, ctx->stream));
   return MLH_OK;
 }
@@ -242,6 +296,8 @@ void mlh_context_destroy(mlh_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  resolve_profile(ctx);
+  for (auto e : ctx->ev_free) (void)hipEventDestroy(e);
   for (auto& kv : ctx->tables) (void)hipFree(kv.second);
   for (auto& kv : ctx->pool) (void)hipFree(kv.second);
   for (auto& kv : ctx->live) (void)hipFree(kv.first);
@@ -1050,6 +1106,31 @@ mlh_status mlh_pcs_verify(const mlh_pcs_proof* pf, uint32_t n_vars, const uint8_
   }
   if (h_mul(delta, h_load(fp->last_elem)) != eval(c, r)) return MLH_ERR_VERIFY;
   return fri_verify_queries(fp, tr, rs);
+}
+
+// ---------------------------------------------------------------------------
+// kernel timer
+// ---------------------------------------------------------------------------
+mlh_status mlh_profile_enable(mlh_ctx* ctx, int on) {
+  if (!ctx) return MLH_ERR_INVALID;
+  ctx->prof_on = on != 0;
+  return MLH_OK;
+}
+
+mlh_status mlh_profile_reset(mlh_ctx* ctx) {
+  if (!ctx) return MLH_ERR_INVALID;
+  resolve_profile(ctx);
+  ctx->prof.clear();
+  return MLH_OK;
+}
+
+mlh_status mlh_profile_get(mlh_ctx* ctx, const char* label, uint64_t* count, double* total_ms) {
+  if (!ctx || !label || !count || !total_ms) return MLH_ERR_INVALID;
+  resolve_profile(ctx);
+  auto it = ctx->prof.find(label);
+  *count = it == ctx->prof.end() ? 0 : it->second.first;
+  *total_ms = it == ctx->prof.end() ? 0.0 : it->second.second;
+  return MLH_OK;
 }
 
 // ---------------------------------------------------------------------------

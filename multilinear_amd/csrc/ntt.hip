@@ -22,6 +22,7 @@
 //   * the last pass tiles 8 consecutive k_1 values so its scattered natural-
 //     order stores are still 128-byte runs.
 // Sizes N <= 2^10 use one LDS-resident workgroup (ntt_small).
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <type_traits>
@@ -323,8 +324,13 @@ hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n,
   return hipGetLastError();
 }
 
+void ntt_pass_label(const NttTables& tb, uint32_t p, bool zero_top, char* buf, size_t n) {
+  const bool last = p + 1 == tb.nradix;
+  snprintf(buf, n, "ntt_pass<%u,%d,%d>", tb.logr[p], last ? 1 : 0, (zero_top && p == 0) ? 1 : 0);
+}
+
 hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables& tb,
-                             uint32_t log_n, bool zero_top, hipStream_t st) {
+                             uint32_t log_n, bool zero_top, hipStream_t st, hipEvent_t* ev) {
   PassGeom g;
   g.log_n = log_n;
   g.nradix = tb.nradix;
@@ -348,6 +354,7 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
     fe* dst = last ? out : scratch;
     const bool zt = zero_top && p == 0;
     const fe* tl = (p == 0) ? tb.tlo0 : tb.tlo;  // n^-1 scale applied once
+    if (ev) (void)hipEventRecord(ev[p], st);
     hipError_t e;
     switch (lr) {
       case 4: e = launch_pass<4>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
@@ -365,6 +372,7 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
     }
     S <<= lr;
   }
+  if (ev) (void)hipEventRecord(ev[tb.nradix], st);
   return hipSuccess;
 }
 

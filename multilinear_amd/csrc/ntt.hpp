@@ -29,8 +29,13 @@ hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n,
                             fe scale, bool apply_scale, hipStream_t st);
 // in: N elements (or N/2 when zero_top: the upper half is implicit zeros).
 // in may equal out; scratch: N elements, distinct from in and out.
+// ev (optional, nradix + 1 events): ev[p] is recorded before pass p, ev[P]
+// after the last pass (kernel timing on the launch stream).
 hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables& tb,
-                             uint32_t log_n, bool zero_top, hipStream_t st);
+                             uint32_t log_n, bool zero_top, hipStream_t st,
+                             hipEvent_t* ev = nullptr);
+// rocprof-style kernel label of pass p ("ntt_pass<8,0,0>")
+void ntt_pass_label(const NttTables& tb, uint32_t p, bool zero_top, char* buf, size_t n);
 hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st);
 hipError_t launch_pow_series(fe* out, const fe* tlo, const fe* thi, uint64_t count,
                              hipStream_t st);
