@@ -84,3 +84,25 @@ def verify(value: bytes, path, root: bytes, index: int) -> bool:
         else:
             h = hash_node(h, sib)
     return h == root and computed_index == index
+
+
+def batch_open(tree, index):
+    """Merkle::batch_open (merkle_tree/mod.rs:134-175): the column
+    data[j][index] for every batch j, and the sibling path."""
+    if index >= len(tree.data[0]):
+        return None
+    value = [b[index] for b in tree.data]
+    path = []
+    cur = index
+    for layer in tree.layers:
+        sib, d = (cur + 1, RIGHT) if cur % 2 == 0 else (cur - 1, LEFT)
+        if sib >= len(layer):
+            break
+        path.append((layer[sib], d))
+        cur //= 2
+    return value, path
+
+
+def batch_verify(value, path, root, index):
+    """MerkleInclusionPath::batch_verify (merkle_tree/mod.rs:255-293)."""
+    return verify(b"".join(value), path, root, index)

@@ -1,0 +1,138 @@
+"""CPU tests of the drop-in boundary: libmlhip.so loads, exports every symbol
+include/mlhip.h declares, the ctypes table covers them, and the host-only
+entry points (generators, transcript, proof sizes, the host-side FRI / PCS
+verifiers) behave like the reference -- no GPU compute is called here."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from multilinear_amd import _lib
+from oracle import field as F
+from oracle import fri as OF
+from oracle import pcs as OP
+from oracle import polynomials as OPL
+from oracle import transcript as OT
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "mlhip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mlh_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 50
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
+
+
+def test_no_gpu_means_loud_failure():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.mlh_context_create(0, None, ctypes.byref(h)) == 4  # MLH_ERR_HIP, no fallback
+
+
+def test_generators_match_oracle():
+    lib = _lib.load()
+    for k in (0, 1, 12, 24, 25, 40):
+        out = (ctypes.c_uint8 * 16)()
+        assert lib.mlh_pow_2_generator(k, out) == 0
+        assert int.from_bytes(bytes(out), "little") == F.pow_2_generator(k)
+    assert lib.mlh_pow_2_generator(41, (ctypes.c_uint8 * 16)()) == 1
+
+
+def test_transcript_matches_reference_semantics():
+    from multilinear_amd.transcript import Transcript
+
+    t, o = Transcript(), OT.Transcript()
+    for chunk in (b"", b"root" * 8, bytes(range(100)), b"x" * 64, b"y" * 63):
+        t.absorb(chunk)
+        o.absorb(chunk)
+        assert t.random() == o.random()
+        assert t.next_challenge() == o.next_challenge()
+        assert t.next_challenge() == t.next_challenge()  # no absorb between calls
+    c = t.clone()
+    c.absorb(b"z")
+    assert c.random() != t.random()
+
+
+def test_proof_sizes():
+    lib = _lib.load()
+    assert lib.mlh_merkle_layers_bytes(1 << 10) == (2 * 1024 - 1) * 32
+    L = 11
+    assert lib.mlh_fri_query_bytes(L) == 32 * sum(1 + (L - 1 - t) for t in range(L - 1))
+
+
+def _fill_fri_struct(proof, log_code):
+    """Pack an oracle FriProof into the C struct layout of mlhip.h."""
+    from multilinear_amd import _lib as L
+
+    T = log_code - 1
+    commit = (ctypes.c_uint8 * (32 * T)).from_buffer_copy(b"".join(proof.commitments))
+    qb = L.load().mlh_fri_query_bytes(log_code)
+    raw = b""
+    for q in proof.queries:
+        for value, path in q:
+            raw += value + b"".join(s for s, _ in path)
+    assert len(raw) == qb * 128
+    qbuf = (ctypes.c_uint8 * len(raw)).from_buffer_copy(raw)
+    c = L.FriProofC()
+    c.log_code = log_code
+    c.num_trees = T
+    c.num_queries = 128
+    c.commitments = ctypes.cast(commit, ctypes.c_void_p)
+    c.last_elem[:] = list(F.to_bytes(proof.last_elem))
+    c.last_random[:] = list(proof.last_random)
+    c.query_indices = None
+    c.queries = ctypes.cast(qbuf, ctypes.c_void_p)
+    return c, (commit, qbuf)
+
+
+def test_host_fri_verifier_accepts_oracle_proof():
+    """mlh_fri_verify (FriProof::verify, fri/mod.rs:287-340) on an oracle proof."""
+    lib = _lib.load()
+    ln = 8
+    vals = [F.from_i64(7 * i + 3) for i in range(1 << ln)]
+    gp = F.pow_2_generator_powers(ln + 1)
+    code = OF.reed_solomon(vals, gp[1])
+    proof = OF.FriProof.prove(code, gp, OT.Transcript())
+    c, keep = _fill_fri_struct(proof, ln + 1)
+    assert lib.mlh_fri_verify(ctypes.byref(c)) == 0
+    c.last_random[0] ^= 1
+    assert lib.mlh_fri_verify(ctypes.byref(c)) == 7
+    c.last_random[0] ^= 1
+    keep[1][100] ^= 1
+    assert lib.mlh_fri_verify(ctypes.byref(c)) == 7
+
+
+def test_host_pcs_verifier_accepts_oracle_proof():
+    """mlh_pcs_verify (PCSProof::verify, multilinear_pcs.rs:138-190)."""
+    from multilinear_amd.device import fe_bytes
+    from multilinear_amd.polynomials import _points
+    from multilinear_amd.transcript import Transcript
+
+    lib = _lib.load()
+    n = 7
+    ev = [F.from_i64(7 * i + 3) for i in range(1 << n)]
+    pts = [F.from_i64(i) for i in range(n)]
+    out = OPL.mle_evaluate(ev, pts)
+    p = OP.PCSProof.prove(pts, out, ev, OT.Transcript())
+    c, keep = _fill_fri_struct(p.fri_proof, n + 1)
+    polys = (ctypes.c_uint8 * (32 * n)).from_buffer_copy(
+        b"".join(F.to_bytes(a) + F.to_bytes(b) for a, b in p.sumcheck_polynomials))
+    pc = _lib.PcsProofC()
+    pc.fri = c
+    pc.sumcheck_polys = ctypes.cast(polys, ctypes.c_void_p)
+    assert lib.mlh_pcs_verify(ctypes.byref(pc), n, _points(pts), fe_bytes(out), Transcript().h) == 0
+    assert lib.mlh_pcs_verify(ctypes.byref(pc), n, _points(pts), fe_bytes(out + 1), Transcript().h) == 7

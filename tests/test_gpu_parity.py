@@ -430,3 +430,44 @@ def test_reed_solomon_and_fri_commit_vs_c_oracle(log_n):
     pd = MF.FriProverData.fold(dcode, Transcript())
     assert pd.fold_roots() == roots
     assert pd.last_element == last
+
+
+# ---- GPU against the committed golden fixtures ---------------------------------
+
+def _golden():
+    import json
+    import os
+
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+
+
+def _digest(values):
+    import hashlib
+
+    return hashlib.sha256(b"".join(F.to_bytes(v) for v in values)).hexdigest()
+
+
+def test_gpu_matches_golden_fixtures():
+    G = _golden()
+    for ln, rec in G["ntt_coeffs_0_to_n"].items():
+        ln = int(ln)
+        ev = host(MN.Polynomial(dev([F.from_i64(i) for i in range(1 << ln)])).ntt(F.pow_2_generator(ln)).evals)
+        assert _digest(ev) == rec["sha256"]
+    rec = G["fri_7i3_log10"]
+    vals = [F.from_i64(7 * i + 3) for i in range(1 << 10)]
+    code = MF.reed_solomon(dev(vals), F.pow_2_generator(11))
+    assert _digest(host(code)) == rec["code_sha256"]
+    p = MF.FriProof.prove(code, Transcript())
+    assert [c.hex() for c in p.commitments] == rec["commitments"]
+    assert "%032x" % p.last_elem == rec["last_elem"]
+    assert p.last_random.hex() == rec["last_random"]
+    n = 10
+    ev = [F.from_i64(7 * i + 3) for i in range(1 << n)]
+    pts = [F.from_i64(i) for i in range(n)]
+    out = MPL.evaluate(dev(ev), pts)
+    assert "%032x" % out == G["mle_eval_7i3_point_0_to_9"]
+    pc = MP.PCSProof.prove(pts, out, dev(ev), Transcript())
+    pr = G["pcs_7i3_n10"]
+    assert [["%032x" % c for c in q] for q in pc.sumcheck_polynomials] == pr["sumcheck_polys"]
+    assert [c.hex() for c in pc.fri_proof.commitments] == pr["commitments"]
+    assert pc.fri_proof.last_random.hex() == pr["last_random"]
