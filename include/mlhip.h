@@ -70,6 +70,13 @@ mlh_status mlh_pow_2_generator(uint32_t log_size, uint8_t gen_out[16]);
  * i < 2^log_size, written to dev (no serial chain on the device). */
 mlh_status mlh_pow_2_generator_powers(mlh_ctx* ctx, uint32_t log_size, void* dev_out);
 
+/* Elementwise Field128 ops on device vectors of n elements (src/field.rs:66-111:
+ * Add, Sub, Mul, Neg).  Inputs canonical; out may alias an input. */
+mlh_status mlh_field_add(mlh_ctx* ctx, const void* dev_a, const void* dev_b, void* dev_out, uint64_t n);
+mlh_status mlh_field_sub(mlh_ctx* ctx, const void* dev_a, const void* dev_b, void* dev_out, uint64_t n);
+mlh_status mlh_field_mul(mlh_ctx* ctx, const void* dev_a, const void* dev_b, void* dev_out, uint64_t n);
+mlh_status mlh_field_neg(mlh_ctx* ctx, const void* dev_a, void* dev_out, uint64_t n);
+
 /* ---- NTT (src/ntt/mod.rs) ------------------------------------------------ */
 /* Polynomial::ntt (ntt/mod.rs:69-110): evals[i] = sum_j coeffs[j] gen^(ij),
  * natural order in and out.  gen must have order exactly 2^log_n.  In-place

@@ -70,6 +70,10 @@ SIGNATURES = {
     "mlh_memcpy_d2d": (_I, [_P, _P, _P, _S]),
     "mlh_pow_2_generator": (_I, [_U32, _P]),
     "mlh_pow_2_generator_powers": (_I, [_P, _U32, _P]),
+    "mlh_field_add": (_I, [_P, _P, _P, _P, _U64]),
+    "mlh_field_sub": (_I, [_P, _P, _P, _P, _U64]),
+    "mlh_field_mul": (_I, [_P, _P, _P, _P, _U64]),
+    "mlh_field_neg": (_I, [_P, _P, _P, _U64]),
     "mlh_ntt": (_I, [_P, _P, _P, _U32, _P]),
     "mlh_intt": (_I, [_P, _P, _P, _U32, _P]),
     "mlh_bit_reverse_permutation": (_I, [_P, _P, _P, _U32]),

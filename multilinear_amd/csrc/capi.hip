@@ -23,6 +23,7 @@
 
 #include "../../include/mlhip.h"
 #include "field.hpp"
+#include "fieldops.hpp"
 #include "host_field.hpp"
 #include "host_sha256.hpp"
 #include "merkle.hpp"
@@ -388,6 +389,25 @@ mlh_status mlh_ntt(mlh_ctx* ctx, const void* dev_coeffs, void* dev_evals, uint32
 mlh_status mlh_intt(mlh_ctx* ctx, const void* dev_evals, void* dev_coeffs, uint32_t log_n,
                     const uint8_t gen[16]) {
   return ntt_entry(ctx, dev_evals, dev_coeffs, log_n, gen, true);
+}
+
+static mlh_status vec_op(mlh_ctx* ctx, int op, const void* a, const void* b, void* out, uint64_t n) {
+  if (!ctx || !a || !out || (op < 3 && !b)) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  HIP_TRY(ctx, launch_vec_op(op, reinterpret_cast<const fe*>(a), reinterpret_cast<const fe*>(b),
+                             reinterpret_cast<fe*>(out), n, ctx->stream));
+  return MLH_OK;
+}
+mlh_status mlh_field_add(mlh_ctx* ctx, const void* a, const void* b, void* out, uint64_t n) {
+  return vec_op(ctx, 0, a, b, out, n);
+}
+mlh_status mlh_field_sub(mlh_ctx* ctx, const void* a, const void* b, void* out, uint64_t n) {
+  return vec_op(ctx, 1, a, b, out, n);
+}
+mlh_status mlh_field_mul(mlh_ctx* ctx, const void* a, const void* b, void* out, uint64_t n) {
+  return vec_op(ctx, 2, a, b, out, n);
+}
+mlh_status mlh_field_neg(mlh_ctx* ctx, const void* a, void* out, uint64_t n) {
+  return vec_op(ctx, 3, a, nullptr, out, n);
 }
 
 mlh_status mlh_bit_reverse_permutation(mlh_ctx* ctx, const void* dev_in, void* dev_out,

@@ -119,29 +119,59 @@ __device__ __forceinline__ fe fe_half(const fe& x) {
   return r;
 }
 
-// Full 256-bit product, operand scanning on v_mad_u64_u32.
+// acc += a*b with the 64-bit carry-out of v_mad_u64_u32 (an SGPR lane mask)
+// counted into c2 by v_addc.  hipcc never uses that carry-out on its own and
+// instead shuffles {x, 0} register pairs (~37 v_mov per product).
+__device__ __forceinline__ void mac_carry(uint64_t& acc, uint32_t a, uint32_t b, uint32_t& c2) {
+  uint64_t out, cy, cy2;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(out), "=s"(cy) : "v"(a), "v"(b), "v"(acc));
+  asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(c2), "=s"(cy2) : "v"(c2), "s"(cy));
+  acc = out;
+}
+
+// Full 256-bit product, product scanning (Comba) over 64-bit column
+// accumulators {lo, hi}.  Column 1's first MAC adds to hi(a0*b0) < 2^32 and
+// column 6 holds the top 64 bits of a < 2^256 product, so neither can
+// overflow; every other MAC counts its carry (13 in total: a first MAC of
+// columns 2..5 adds to {hi(prev), carries} < 2^34 and CAN overflow).
 __device__ __forceinline__ void mul_wide(const fe& a, const fe& b, uint32_t r[8]) {
-  uint64_t t;
-  t = (uint64_t)a.w[0] * b.w[0];
-  r[0] = (uint32_t)t;
-  t = (uint64_t)a.w[0] * b.w[1] + (t >> 32);
-  r[1] = (uint32_t)t;
-  t = (uint64_t)a.w[0] * b.w[2] + (t >> 32);
-  r[2] = (uint32_t)t;
-  t = (uint64_t)a.w[0] * b.w[3] + (t >> 32);
-  r[3] = (uint32_t)t;
-  r[4] = (uint32_t)(t >> 32);
-#pragma unroll
-  for (int i = 1; i < 4; ++i) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      t = (uint64_t)a.w[i] * b.w[j] + r[i + j] + c;
-      r[i + j] = (uint32_t)t;
-      c = t >> 32;
-    }
-    r[i + 4] = (uint32_t)c;
-  }
+  uint64_t acc;
+  uint32_t c2;
+  acc = (uint64_t)a.w[0] * b.w[0];
+  r[0] = (uint32_t)acc;
+  acc >>= 32;
+  acc = (uint64_t)a.w[0] * b.w[1] + acc;
+  c2 = 0;
+  mac_carry(acc, a.w[1], b.w[0], c2);
+  r[1] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);
+  c2 = 0;
+  mac_carry(acc, a.w[0], b.w[2], c2);
+  mac_carry(acc, a.w[1], b.w[1], c2);
+  mac_carry(acc, a.w[2], b.w[0], c2);
+  r[2] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);
+  c2 = 0;
+  mac_carry(acc, a.w[0], b.w[3], c2);
+  mac_carry(acc, a.w[1], b.w[2], c2);
+  mac_carry(acc, a.w[2], b.w[1], c2);
+  mac_carry(acc, a.w[3], b.w[0], c2);
+  r[3] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);
+  c2 = 0;
+  mac_carry(acc, a.w[1], b.w[3], c2);
+  mac_carry(acc, a.w[2], b.w[2], c2);
+  mac_carry(acc, a.w[3], b.w[1], c2);
+  r[4] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);
+  c2 = 0;
+  mac_carry(acc, a.w[2], b.w[3], c2);
+  mac_carry(acc, a.w[3], b.w[2], c2);
+  r[5] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);
+  acc = (uint64_t)a.w[3] * b.w[3] + acc;
+  r[6] = (uint32_t)acc;
+  r[7] = (uint32_t)(acc >> 32);
 }
 
 // Reduce a 256-bit value r (little-endian limbs) to canonical form.

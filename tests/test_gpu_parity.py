@@ -471,3 +471,62 @@ def test_gpu_matches_golden_fixtures():
     assert [["%032x" % c for c in q] for q in pc.sumcheck_polynomials] == pr["sumcheck_polys"]
     assert [c.hex() for c in pc.fri_proof.commitments] == pr["commitments"]
     assert pc.fri_proof.last_random.hex() == pr["last_random"]
+
+
+# ---- field arithmetic on adversarial operands ------------------------------------
+
+def _edge_values():
+    """Limb patterns that stress every carry path of the 128x128 product and
+    the 2^128 = C folds: all-ones limbs, values just below M, powers of two."""
+    vals = [0, 1, 2, F.M - 1, F.M - 2, (F.M - 1) // 2, (F.M + 1) // 2, 2**127, 2**96, 2**64 - 1,
+            2**96 - 1, 2**128 - 2**96 - 1, F.M - 2**64, F.M - 2**32, 0x2CFFFFFFFFFF, 0x2D0000000000]
+    for top in (0xFFFFFFFE, 0xFFFFFFFF):
+        for mid in (0xFFFFFFFF, 0xFFFFD2FF, 0xFFFFD300, 0):
+            v = (top << 96) | (mid << 64) | (0xFFFFFFFF << 32) | 0xFFFFFFFF
+            if v < F.M:
+                vals.append(v)
+    r = random.Random(77)
+    for _ in range(64):  # near-M and dense-ones randoms
+        vals.append(F.M - 1 - r.randrange(2**48))
+        v = sum((0xFFFFFFFF if r.random() < 0.8 else r.randrange(2**32)) << (32 * i) for i in range(4))
+        vals.append(v % F.M)
+    return [v % F.M for v in vals]
+
+
+def test_field_ops_adversarial():
+    ev = _edge_values()
+    a = [x for x in ev for _ in ev]
+    b = [y for _ in ev for y in ev]
+    da, db = dev(a), dev(b)
+    out = D.empty(len(a))
+    ctx = D.context()
+    lib = D.lib()
+    for fn, py in ((lib.mlh_field_mul, lambda x, y: x * y % F.M),
+                   (lib.mlh_field_add, lambda x, y: (x + y) % F.M),
+                   (lib.mlh_field_sub, lambda x, y: (x - y) % F.M)):
+        D.check(fn(ctx, D.ptr(da), D.ptr(db), D.ptr(out), len(a)), ctx)
+        got = host(out)
+        want = [py(x, y) for x, y in zip(a, b)]
+        bad = [i for i in range(len(a)) if got[i] != want[i]]
+        assert not bad, (fn.__name__, len(bad), hex(a[bad[0]]), hex(b[bad[0]]))
+    D.check(lib.mlh_field_neg(ctx, D.ptr(da), D.ptr(out), len(a)), ctx)
+    assert host(out) == [(-x) % F.M for x in a]
+
+
+def test_field_mul_random_bulk():
+    n = 1 << 20
+    x = D.random_limbs(n, 5)
+    y = D.random_limbs(n, 6)
+    out = D.empty(n)
+    ctx = D.context()
+    dx, dy = D.to_device(x), D.to_device(y)  # keep the tensors alive across the call
+    D.check(D.lib().mlh_field_mul(ctx, D.ptr(dx), D.ptr(dy), D.ptr(out), n), ctx)
+    got = D.from_device(out)
+    xi, yi, gi = D.limbs_to_ints(x[:4096]), D.limbs_to_ints(y[:4096]), D.limbs_to_ints(got[:4096])
+    assert gi == [p * q % F.M for p, q in zip(xi, yi)]
+    from oracle import coracle
+
+    coracle.lib()
+    for i in range(0, n, 997):
+        assert D.limbs_to_ints(got[i:i + 1])[0] == coracle.mul(D.limbs_to_ints(x[i:i + 1])[0],
+                                                                 D.limbs_to_ints(y[i:i + 1])[0])
