@@ -215,6 +215,15 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
     const uint64_t R = 1ull << tb->logr[p];
     MLH_TRY(get_table(ctx, h_pow(w, N / R), R / 2, 1, &tb->tw[p]));
   }
+  {
+    uint64_t S = 1;
+    for (uint32_t p = 0; p + 1 < tb->nradix; ++p) {  // the last pass has no twiddle
+      const uint64_t span = N / S;
+      if (span <= kDirectMax)
+        MLH_TRY(get_table(ctx, h_pow(w, S), span, p == 0 ? scale : (u128)1, &tb->tdir[p]));
+      S <<= tb->logr[p];
+    }
+  }
   MLH_TRY(get_table(ctx, w, 4096, scale, &tb->tlo0));
   MLH_TRY(get_table(ctx, w, 4096, 1, &tb->tlo));
   MLH_TRY(get_table(ctx, h_pow(w, 4096), hi_count(log_n), 1, &tb->thi));

@@ -46,6 +46,7 @@ struct PassGeom {
   uint32_t logr[kMaxPasses];
   uint64_t stride;      // W_p (elements between consecutive rows of this digit)
   uint64_t S;           // R_1*...*R_{p-1}
+  uint32_t direct;      // 1: twiddle = tdir[jrest*k] (table of w^(S t), t < N/S)
 };
 
 // Last pass: natural output index is K = k_1 + R_1*rev(mid) + (N/R_P)*k_P,
@@ -63,12 +64,21 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
   return rev;
 }
 
-template <int LOGR, bool LAST, bool ZERO_TOP>
-__global__ void __launch_bounds__(kCols * (1 << LOGR) / kEPT)
+// TW: 0 = two-level twiddle (T_lo * T_hi), 1 = direct table, 2 = none (last pass)
+// waves per SIMD the LDS tile allows (160 KiB/CU): caps VGPRs to match
+constexpr int pass_waves_per_simd(int logr) {
+  return logr == 8 ? 5 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2));
+}
+
+template <int LOGR, int TW, bool ZERO_TOP>
+__global__ void __launch_bounds__(kCols * (1 << LOGR) / kEPT,
+                                  TW == 2 ? 1 : pass_waves_per_simd(LOGR))
 ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
-                const fe* __restrict__ tlo, const fe* __restrict__ thi, PassGeom g) {
+                const fe* __restrict__ tlo, const fe* __restrict__ thi,
+                const fe* __restrict__ tdir, PassGeom g) {
   constexpr int R = 1 << LOGR;
   constexpr int TPC = R / kEPT;  // threads per column
+  constexpr bool LAST = TW == 2;
   __shared__ fe lds[R * kCols];
 
   const int tid = threadIdx.x;
@@ -109,7 +119,8 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
 #pragma unroll
   for (int e = 0; e < kEPT; ++e) {
     const uint32_t row = bitrev((uint32_t)(t * kEPT + e), LOGR);
-    if (ZERO_TOP && row >= (uint32_t)(R / 2)) {
+    // rows >= R/2 are the implicit zero half; bitrev puts them exactly at odd e
+    if (ZERO_TOP && (e & 1)) {
       x[e] = fe_zero();
     } else {
       x[e] = fe_load(src + (uint64_t)row * rstride);
@@ -135,6 +146,10 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
           const int e1 = e0 + d;
           const uint32_t pos = bpos + ((uint32_t)i << s0);
           const uint32_t j = pos & ((1u << s) - 1u);
+          if (ZERO_TOP && s0 == 0 && s == 0) {  // (u, 0) -> (u, u)
+            x[e1] = x[e0];
+            continue;
+          }
           fe v = x[e1];
           if (s > 0) {
             // phase 1 (s0 == 0): j is a compile-time function of i -> uniform load
@@ -205,8 +220,13 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     const uint64_t k = pos[e];
     fe v = x[e];
     if (!LAST) {
-      const uint64_t ex = (jrest * k * g.S) & (N - 1);
-      const fe w = fe_mul(tlo[ex & 4095], thi[ex >> 12]);
+      fe w;
+      if (TW == 1) {
+        w = tdir[jrest * k];  // one lookup: w^(S * jrest * k)
+      } else {
+        const uint64_t ex = (jrest * k * g.S) & (N - 1);
+        w = fe_mul(tlo[ex & 4095], thi[ex >> 12]);
+      }
       v = fe_mul(v, w);
       fe_store(dst + k * rstride, v);
     } else {
@@ -269,18 +289,27 @@ __global__ void pow_series_kernel(fe* __restrict__ out, const fe* __restrict__ t
 
 template <int LOGR>
 static hipError_t launch_pass(bool last, bool zero_top, const fe* in, fe* out, const fe* tw,
-                              const fe* tlo, const fe* thi, const PassGeom& g, uint64_t tiles,
-                              hipStream_t st) {
+                              const fe* tlo, const fe* thi, const fe* tdir, const PassGeom& g,
+                              uint64_t tiles, hipStream_t st) {
   constexpr int threads = kCols * (1 << LOGR) / kEPT;
+  const dim3 grid((unsigned)tiles), blk(threads);
   if (last) {
-    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, true, false>), dim3((unsigned)tiles), dim3(threads), 0,
-                       st, in, out, tw, tlo, thi, g);
-  } else if (zero_top) {
-    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, false, true>), dim3((unsigned)tiles), dim3(threads), 0,
-                       st, in, out, tw, tlo, thi, g);
+    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 2, false>), grid, blk, 0, st, in, out, tw, tlo, thi,
+                       tdir, g);
+  } else if (tdir) {
+    if (zero_top)
+      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 1, true>), grid, blk, 0, st, in, out, tw, tlo, thi,
+                         tdir, g);
+    else
+      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 1, false>), grid, blk, 0, st, in, out, tw, tlo,
+                         thi, tdir, g);
   } else {
-    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, false, false>), dim3((unsigned)tiles), dim3(threads),
-                       0, st, in, out, tw, tlo, thi, g);
+    if (zero_top)
+      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 0, true>), grid, blk, 0, st, in, out, tw, tlo, thi,
+                         tdir, g);
+    else
+      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 0, false>), grid, blk, 0, st, in, out, tw, tlo,
+                         thi, tdir, g);
   }
   return hipGetLastError();
 }
@@ -326,7 +355,8 @@ hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n,
 
 void ntt_pass_label(const NttTables& tb, uint32_t p, bool zero_top, char* buf, size_t n) {
   const bool last = p + 1 == tb.nradix;
-  snprintf(buf, n, "ntt_pass<%u,%d,%d>", tb.logr[p], last ? 1 : 0, (zero_top && p == 0) ? 1 : 0);
+  const int tw = last ? 2 : (tb.tdir[p] ? 1 : 0);
+  snprintf(buf, n, "ntt_pass<%u,%d,%d>", tb.logr[p], tw, (zero_top && p == 0) ? 1 : 0);
 }
 
 hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables& tb,
@@ -344,6 +374,7 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
     g.p = p;
     g.stride = W;
     g.S = S;
+    g.direct = tb.tdir[p] != nullptr ? 1u : 0u;
     const bool last = (p + 1 == tb.nradix);
     const uint64_t tiles = N / ((uint64_t)kCols << lr);
     // pass 0: in -> scratch; middle passes in place on scratch; the last pass
@@ -357,12 +388,12 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
     if (ev) (void)hipEventRecord(ev[p], st);
     hipError_t e;
     switch (lr) {
-      case 4: e = launch_pass<4>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
-      case 5: e = launch_pass<5>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
-      case 6: e = launch_pass<6>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
-      case 7: e = launch_pass<7>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
-      case 8: e = launch_pass<8>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
-      case 9: e = launch_pass<9>(last, zt, src, dst, tb.tw[p], tl, tb.thi, g, tiles, st); break;
+      case 4: e = launch_pass<4>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
+      case 5: e = launch_pass<5>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
+      case 6: e = launch_pass<6>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
+      case 7: e = launch_pass<7>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
+      case 8: e = launch_pass<8>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
+      case 9: e = launch_pass<9>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
       default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;

@@ -8,6 +8,7 @@
 namespace mlh {
 
 constexpr int kMaxPasses = 6;
+constexpr uint64_t kDirectMax = 1ull << 16;  // 1 MiB direct twiddle tables
 
 // Device twiddle tables for one (log_n, generator, direction).
 struct NttTables {
@@ -19,6 +20,9 @@ struct NttTables {
   const fe* tlo = nullptr;               // passes > 0: w^t, t < 4096
   const fe* thi = nullptr;               // w^(4096 t), t < ceil(N/4096)
   const fe* tw_small = nullptr;          // N <= 2^10: w^t, t < N/2
+  // per pass with N/S <= kDirectMax: w^(S t) (x scale on pass 0), t < N/S --
+  // the inter-pass twiddle becomes one lookup instead of lookup*lookup
+  const fe* tdir[kMaxPasses] = {nullptr};
   fe scale;                              // n^-1 (inverse) or 1
   bool inverse = false;
 };
