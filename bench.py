@@ -1,17 +1,20 @@
 """bench.py -- headline benchmark (BASELINE.json metric) on 1..8 MI355X.
 
 Metric: "NTT 2^24 field-elems/sec + FRI commit ms; % HBM roofline".
-  * step  = one forward 2^24-point NTT (config 2, src/ntt/mod.rs:69-110) over
-            a device-resident synthetic vector (seeded uniform field elements);
-  * value = 2^24 * steps * world_size / max-over-ranks(time of the K steps)
-            (weak scaling: each rank transforms its own polynomial; the path
-            has no exchange step at this size, DESIGN.md "Multi-GPU");
-  * extra lines in the same JSON: inverse NTT, FRI commit (config 3:
-    2^24 coeffs -> RS LDE 2^25 -> Merkle root on host), full FRI prove and
-    the 24-round sumcheck (config 4), each timed after the headline loop;
-  * roofline: the dominant kernel (ntt_pass<8,0,0>) timed live with HIP
-    events on its launch stream over the headline loop; algorithmic bytes per
-    launch = 32 B x 2^24 (each element read once and written once);
+  * N = 1: step = one forward 2^24-point NTT (config 2, src/ntt/mod.rs:69-110)
+            over a device-resident synthetic vector (seeded uniform elements);
+  * N > 1: step = one SHARDED forward NTT of N * 2^24 points (weak scaling:
+            2^24 elements per GPU): local 2^24 NTT, one RCCL all-to-all over
+            xGMI, cross-shard DFT kernel (multilinear_amd/dist.py);
+  * value = 2^24 * N * steps / max-over-ranks(time of the K steps);
+  * extras in the same JSON line: inverse NTT, FRI commit (config 3: 2^24
+    coeffs -> RS LDE 2^25 -> Merkle root), full FRI prove, the 24-round
+    sumcheck (config 4) [N = 1], and config 5: RS encode + FRI prove of a
+    2^28-element codeword, single GPU at N = 1, sharded over the N ranks at
+    N > 1 (strong scaling), each timed after the headline loop;
+  * roofline: the dominant kernel (an ntt_pass) timed live with HIP events on
+    its launch stream over the headline loop; algorithmic bytes per launch =
+    32 B x 2^24 (each element read once and written once);
   * cpu_baseline: the oracle's C restatement of the reference NTT
     (oracle/liboracle.so, 1 thread) on one 2^24 NTT, rank 0 at N = 1 only.
 
@@ -89,6 +92,7 @@ def main():
     ap.add_argument("--extra-reps", type=int, default=3, help="reps of the secondary timings")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--fri-log", type=int, default=28, help="config 5 codeword size (log2)")
     args = ap.parse_args()
 
     import torch
@@ -115,8 +119,20 @@ def main():
     x = D.random_device(N, 1000 + rank, local)
     out = D.empty(N, local)
 
-    def ntt_once():
-        D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(out), log_n, gen), ctx)
+    if world & (world - 1):
+        raise SystemExit("world size must be a power of two")
+    log_p = world.bit_length() - 1
+    if world == 1:
+        def ntt_once():
+            D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(out), log_n, gen), ctx)
+    else:
+        from multilinear_amd import dist as DS
+
+        tp, ops = DS.Transport(), DS.HipOps(local)
+        g_total = int.from_bytes(bytes(_gen(lib, log_n + log_p)), "little")
+
+        def ntt_once():  # x: this rank's cyclic shard of the N * 2^24 vector
+            DS.ntt(x, log_n + log_p, g_total, tp, ops)
 
     def barrier():
         torch.cuda.synchronize()
@@ -144,14 +160,16 @@ def main():
 
     # dominant kernel timing (HIP events on the launch stream, timed region)
     kernels = {}
-    for lab in ("ntt_pass<8,0,0>", "ntt_pass<8,1,0>", "ntt_pass<9,0,0>", "ntt_pass<9,1,0>",
-                "ntt_pass<7,0,0>", "ntt_pass<7,1,0>"):
+    labels = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(3)
+              for z in range(2)] + ["shard_dft<%d,0>" % p for p in range(1, 5)]
+    for lab in labels:
         cnt = ctypes.c_uint64()
         tot = ctypes.c_double()
         lib.mlh_profile_get(ctx, lab.encode(), ctypes.byref(cnt), ctypes.byref(tot))
         if cnt.value:
             kernels[lab] = {"launches": cnt.value, "avg_ms": tot.value / cnt.value}
-    dom = max(kernels.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
+    dom = max(((k, v) for k, v in kernels.items() if k.startswith("ntt_pass")),
+              key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
     dom_name, dom_stat = dom
     alg_bytes = 32.0 * N  # one read + one write of every 16-B element per launch
     achieved_gbs = alg_bytes / (dom_stat["avg_ms"] * 1e-3) / 1e9
@@ -173,10 +191,13 @@ def main():
         "dtype": "u128 mod M (F_M, M = 2^128 - 45*2^40 + 1)",
         "data": "synthetic: seeded uniform field elements generated on device",
         "config": {
-            "workload": "config 2: forward 2^%d-point NTT per step, natural order in/out, "
-                        "device resident" % log_n,
-            "log_n": log_n,
-            "parallelism": "replicas x%d (independent polynomial per GPU)" % world,
+            "workload": ("config 2: forward 2^%d-point NTT per step, natural order in/out, "
+                         "device resident" % log_n) if world == 1 else
+                        ("sharded forward 2^%d-point NTT per step (2^%d per GPU): cyclic shards "
+                         "in, block-cyclic out, one RCCL all-to-all" % (log_n + log_p, log_n)),
+            "log_n": log_n + log_p,
+            "parallelism": "single GPU" if world == 1 else
+                           "sharded x%d (four-step NTT, all-to-all over xGMI)" % world,
         },
         "ntt_hbm_frac": (32.0 * N / (ms_per_step * 1e-3) / 1e9) / HBM_PEAK_GBS,
         "roofline": {
@@ -193,7 +214,7 @@ def main():
         "kernels": kernels,
     }
 
-    if not args.no_extras:
+    if not args.no_extras and world == 1:
         reps = args.extra_reps
         # inverse NTT
         torch.cuda.synchronize()
@@ -253,6 +274,9 @@ def main():
         sc_bytes = sum(48 * (N >> k) for k in range(log_n))
         result["sumcheck_hbm_frac"] = sc_bytes / (sc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
 
+    if not args.no_extras and args.fri_log:
+        result.update(config5(args, lib, ctx, local, world, rank, barrier))
+
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(log_n)
         result["vs_cpu_1core"] = value / result["cpu_baseline"]["value"]
@@ -262,6 +286,52 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def config5(args, lib, ctx, local, world, rank, barrier):
+    """Config 5: RS encode (2^(L-1) coeffs) + FRI prove of the 2^L codeword;
+    single GPU at N = 1, sharded over the ranks at N > 1 (strong scaling)."""
+    import torch
+
+    from multilinear_amd import device as D
+    from multilinear_amd import fri as MF
+    from multilinear_amd.transcript import Transcript
+
+    L = args.fri_log
+    g = int.from_bytes(bytes(_gen(lib, L)), "little")
+    reps = max(1, min(args.extra_reps, 3))
+    if world == 1:
+        coeffs = D.random_device(1 << (L - 1), 77, local)
+
+        def run():
+            code = MF.reed_solomon(coeffs, g, local)
+            return MF.FriProof.prove(code, Transcript(), local)
+    else:
+        from multilinear_amd import dist as DS
+
+        tp, ops = DS.Transport(), DS.HipOps(local)
+        coeffs = D.random_device(1 << (L - 1 - tp.world.bit_length() + 1), 77 + rank, local)
+
+        def run():
+            code = DS.reed_solomon(coeffs, L - 1, g, tp, ops)
+            return DS.fri_prove(code, L, Transcript(), tp, ops)
+
+    p = run()  # warm-up (tables, allocator)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        p = run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    import torch.distributed as tdist
+
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    return {"config5_log_code": L, "config5_rs_fri_prove_ms": dt * 1e3,
+            "config5_verified": bool(p.verify()),
+            "config5_layout": "single GPU" if world == 1 else "sharded x%d" % world}
 
 
 def _gen(lib, log_n):

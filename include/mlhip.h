@@ -157,6 +157,46 @@ mlh_status mlh_fri_prove(mlh_ctx* ctx, const void* dev_code, uint32_t log_code, 
 /* FriProof::verify (fri/mod.rs:287-340), host side; MLH_ERR_VERIFY if rejected. */
 mlh_status mlh_fri_verify(const mlh_fri_proof* proof);
 
+/* Batched open_query_at: nq records (layout above) for host indices idx[nq]. */
+mlh_status mlh_fri_prover_open_queries(mlh_ctx* ctx, const mlh_fri_prover* p,
+                                       const uint64_t* idx, uint32_t nq, uint8_t* out);
+
+/* ---- sharded building blocks (one process per GPU) ------------------------
+ * The reference is single-node CPU code with no distributed API; these are
+ * the rank-local steps multilinear_amd/dist.py drives between torch.distributed
+ * (RCCL) collectives.  A sharded vector of 2^log_n elements over P = 2^log_p
+ * ranks uses a block-cyclic layout with block 2^log_s: local index l of rank
+ * r holds global ((l >> log_s) << (log_s + log_p)) | (r << log_s) | (l mod 2^log_s).
+ * The distributed NTT (Polynomial::ntt / reed_solomon, ntt/mod.rs:69-108)
+ * takes the cyclic layout (log_s = 0) and produces log_s = log_n - 2 log_p. */
+/* Cross-shard stage: dev_in/dev_out are [P][S], S = 2^(log_n - 2 log_p).
+ * Forward: row g of dev_in is the chunk received from rank g (its local
+ * length-N/P NTT with generator gen^P, chunk `rank`); dev_out row t holds
+ * X[t N/P + rank S + jl].  inverse != 0: the reverse (row t in, row g out,
+ * scaled by 1/P; the local inverse NTT supplies 1/(N/P)).  gen has order 2^log_n. */
+mlh_status mlh_shard_ntt_cross(mlh_ctx* ctx, const void* dev_in, void* dev_out, uint32_t log_n,
+                               uint32_t log_p, uint32_t rank, const uint8_t gen[16], int inverse);
+/* fold_step's fold (fri/mod.rs:89-114) on a sharded layer of 2^log_local local
+ * values (pairs l, l + n_local/2 are global pairs i, i + n/2 while the layer
+ * spans >= 2 blocks per rank); k and log_domain are global. */
+mlh_status mlh_shard_fri_fold(mlh_ctx* ctx, const void* dev_layer, uint32_t log_local, uint32_t k,
+                              uint32_t log_domain, const uint8_t r[16], void* dev_next,
+                              uint32_t log_s, uint32_t log_p, uint32_t rank);
+/* Fold, then hash the folded layer's local leaves and build its local tree
+ * (dev_tree: mlh_merkle_layers_bytes(2^(log_local-2)) bytes).  Levels below
+ * log_s are the global tree's; the caller combines the level-log_s nodes of
+ * all ranks. */
+mlh_status mlh_shard_fri_fold_commit(mlh_ctx* ctx, const void* dev_layer, uint32_t log_local,
+                                     uint32_t k, uint32_t log_domain, const uint8_t r[16],
+                                     void* dev_next, void* dev_tree, uint32_t log_s,
+                                     uint32_t log_p, uint32_t rank);
+/* Merkle::open (merkle_tree/mod.rs:31-58) on a local pair tree: for each
+ * local leaf idx[q]: values[idx], values[idx + n/2], then the sibling digests
+ * of levels 0..levels-1.  out: nq * 32 * (1 + levels) bytes (host). */
+mlh_status mlh_merkle_open_pairs(mlh_ctx* ctx, const void* dev_values, uint32_t log_n,
+                                 const void* dev_tree, uint32_t levels, const uint64_t* idx,
+                                 uint32_t nq, uint8_t* out);
+
 /* ---- transcript (src/transcript.rs), host side --------------------------- */
 mlh_status mlh_transcript_create(mlh_transcript** out);
 mlh_status mlh_transcript_clone(const mlh_transcript* t, mlh_transcript** out);

@@ -91,10 +91,15 @@ SIGNATURES = {
     "mlh_fri_prover_roots": (_I, [_P, _P]),
     "mlh_fri_prover_last_element": (_I, [_P, _P]),
     "mlh_fri_prover_open_query": (_I, [_P, _P, _U64, _P]),
+    "mlh_fri_prover_open_queries": (_I, [_P, _P, _P, _U32, _P]),
     "mlh_fri_prover_destroy": (None, [_P]),
     "mlh_fri_query_bytes": (_U64, [_U32]),
     "mlh_fri_prove": (_I, [_P, _P, _U32, _P, ctypes.POINTER(FriProofC)]),
     "mlh_fri_verify": (_I, [ctypes.POINTER(FriProofC)]),
+    "mlh_shard_ntt_cross": (_I, [_P, _P, _P, _U32, _U32, _U32, _P, _I]),
+    "mlh_shard_fri_fold": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _U32, _U32, _U32]),
+    "mlh_shard_fri_fold_commit": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _P, _U32, _U32, _U32]),
+    "mlh_merkle_open_pairs": (_I, [_P, _P, _U32, _P, _U32, _P, _U32, _P]),
     "mlh_transcript_create": (_I, [ctypes.POINTER(_P)]),
     "mlh_transcript_clone": (_I, [_P, ctypes.POINTER(_P)]),
     "mlh_transcript_destroy": (None, [_P]),

@@ -23,6 +23,7 @@
 
 #include "../../include/mlhip.h"
 #include "field.hpp"
+#include "dist.hpp"
 #include "fieldops.hpp"
 #include "host_field.hpp"
 #include "host_sha256.hpp"
@@ -99,6 +100,26 @@ static void resolve_profile(mlh_ctx* ctx) {
   for (auto e : evs) ctx->ev_free.push_back(e);
   ctx->pending.clear();
 }
+
+// Kernel-timer bracket around one launch (no-op unless mlh_profile_enable).
+struct ProfScope {
+  mlh_ctx* ctx;
+  const char* label;
+  hipEvent_t a = nullptr;
+  ProfScope(mlh_ctx* c, const char* lab) : ctx(c), label(lab) {
+    if (ctx->prof_on) {
+      a = take_event(ctx);
+      (void)hipEventRecord(a, ctx->stream);
+    }
+  }
+  void end() {
+    if (!a) return;
+    hipEvent_t b = take_event(ctx);
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->pending.push_back(mlh_ctx::Pending{label, a, b});
+    a = nullptr;
+  }
+};
 
 struct mlh_transcript {
   HostSha256 sha;
@@ -768,6 +789,118 @@ mlh_status mlh_fri_prover_open_query(mlh_ctx* ctx, const mlh_fri_prover* p, uint
   if (!ctx || !p || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
   if (index >= (1ull << (p->log_code - 1))) return fail(ctx, MLH_ERR_INVALID, "index out of bounds");
   return gather_queries(ctx, p, &index, 1, out);
+}
+
+mlh_status mlh_fri_prover_open_queries(mlh_ctx* ctx, const mlh_fri_prover* p,
+                                       const uint64_t* idx, uint32_t nq, uint8_t* out) {
+  if (!ctx || !p || !idx || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  for (uint32_t q = 0; q < nq; ++q)
+    if (idx[q] >= (1ull << (p->log_code - 1))) return fail(ctx, MLH_ERR_INVALID, "index out of bounds");
+  if (nq == 0) return MLH_OK;
+  return gather_queries(ctx, p, idx, nq, out);
+}
+
+// ---------------------------------------------------------------------------
+// sharded building blocks (dist.hip; orchestration in multilinear_amd/dist.py)
+// ---------------------------------------------------------------------------
+mlh_status mlh_shard_ntt_cross(mlh_ctx* ctx, const void* dev_in, void* dev_out, uint32_t log_n,
+                               uint32_t log_p, uint32_t rank, const uint8_t gen[16], int inverse) {
+  if (!ctx || !dev_in || !dev_out || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_p < 1 || log_p > 4 || log_n < 2 * log_p || log_n > 40)
+    return fail(ctx, MLH_ERR_INVALID, "need 1 <= log_p <= 4 and log_n >= 2 log_p");
+  if (rank >> log_p) return fail(ctx, MLH_ERR_INVALID, "rank out of range");
+  if (dev_in == dev_out) return fail(ctx, MLH_ERR_INVALID, "shard_ntt_cross is out of place");
+  const u128 g = h_load(gen);
+  if (!check_generator(g, log_n)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != n");
+  const uint64_t P = 1ull << log_p, S = 1ull << (log_n - 2 * log_p);
+  const u128 w = inverse ? h_inv(g) : g;
+  const fe *tlo, *thi, *wp;
+  MLH_TRY(get_table(ctx, w, 4096, 1, &tlo));
+  MLH_TRY(get_table(ctx, h_pow(w, 4096), hi_count(log_n - log_p), 1, &thi));
+  MLH_TRY(get_table(ctx, h_pow(w, 1ull << (log_n - log_p)), P / 2, 1, &wp));
+  const u128 scale = inverse ? h_inv((u128)P) : (u128)1;
+  static const char* labs[2][5] = {{"", "shard_dft<1,0>", "shard_dft<2,0>", "shard_dft<3,0>", "shard_dft<4,0>"},
+                                   {"", "shard_dft<1,1>", "shard_dft<2,1>", "shard_dft<3,1>", "shard_dft<4,1>"}};
+  ProfScope ps(ctx, labs[inverse ? 1 : 0][log_p]);
+  HIP_TRY(ctx, launch_shard_dft(reinterpret_cast<const fe*>(dev_in), reinterpret_cast<fe*>(dev_out),
+                                S, (uint64_t)rank * S, log_p, inverse != 0, tlo, thi, wp,
+                                to_fe(scale), ctx->stream));
+  ps.end();
+  return MLH_OK;
+}
+
+static mlh_status shard_fold_args(mlh_ctx* ctx, const void* a, const void* b, const uint8_t* r,
+                                  uint32_t log_local, uint32_t k, uint32_t log_domain,
+                                  uint32_t log_s, uint32_t log_p, uint32_t rank, ShardMap* m) {
+  if (!ctx || !a || !b || !r) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_domain > 40 || log_p > 4 || (rank >> log_p) || log_local < 1 ||
+      log_local + log_p + k != log_domain)
+    return fail(ctx, MLH_ERR_INVALID, "local layer must be 2^(log_domain - k - log_p)");
+  if (log_s + 1 > log_local && log_p > 0)
+    return fail(ctx, MLH_ERR_INVALID, "pairs not local: layer spans < 2 blocks per rank");
+  m->log_s = log_p ? log_s : 40;
+  m->log_p = log_p;
+  m->rank = rank;
+  return MLH_OK;
+}
+
+mlh_status mlh_shard_fri_fold(mlh_ctx* ctx, const void* dev_layer, uint32_t log_local, uint32_t k,
+                              uint32_t log_domain, const uint8_t r[16], void* dev_next,
+                              uint32_t log_s, uint32_t log_p, uint32_t rank) {
+  ShardMap m;
+  MLH_TRY(shard_fold_args(ctx, dev_layer, dev_next, r, log_local, k, log_domain, log_s, log_p,
+                          rank, &m));
+  const fe *tlo, *thi;
+  MLH_TRY(fold_tables(ctx, log_domain, &tlo, &thi));
+  HIP_TRY(ctx, launch_fri_fold(reinterpret_cast<const fe*>(dev_layer), 1ull << log_local,
+                               reinterpret_cast<fe*>(dev_next), to_fe(h_load(r)), tlo, thi, k,
+                               1ull << log_domain, ctx->stream, m));
+  return MLH_OK;
+}
+
+mlh_status mlh_shard_fri_fold_commit(mlh_ctx* ctx, const void* dev_layer, uint32_t log_local,
+                                     uint32_t k, uint32_t log_domain, const uint8_t r[16],
+                                     void* dev_next, void* dev_tree, uint32_t log_s,
+                                     uint32_t log_p, uint32_t rank) {
+  ShardMap m;
+  MLH_TRY(shard_fold_args(ctx, dev_layer, dev_next, r, log_local, k, log_domain, log_s, log_p,
+                          rank, &m));
+  if (!dev_tree) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_local < 2 || (log_p && log_s + 2 > log_local))
+    return fail(ctx, MLH_ERR_INVALID, "folded layer's pairs are not local");
+  const fe *tlo, *thi;
+  MLH_TRY(fold_tables(ctx, log_domain, &tlo, &thi));
+  uint8_t* tree = reinterpret_cast<uint8_t*>(dev_tree);
+  HIP_TRY(ctx, launch_fri_fold_leaves(reinterpret_cast<const fe*>(dev_layer), 1ull << log_local,
+                                      reinterpret_cast<fe*>(dev_next), tree, to_fe(h_load(r)),
+                                      tlo, thi, k, 1ull << log_domain, ctx->stream, m));
+  HIP_TRY(ctx, launch_merkle_levels(tree, 1ull << (log_local - 2), ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_merkle_open_pairs(mlh_ctx* ctx, const void* dev_values, uint32_t log_n,
+                                 const void* dev_tree, uint32_t levels, const uint64_t* idx,
+                                 uint32_t nq, uint8_t* out) {
+  if (!ctx || !dev_values || !dev_tree || (nq && (!idx || !out)))
+    return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_n < 1 || log_n > 40 || levels > log_n - 1)
+    return fail(ctx, MLH_ERR_INVALID, "levels must be <= log_n - 1");
+  const uint64_t half = 1ull << (log_n - 1);
+  for (uint32_t q = 0; q < nq; ++q)
+    if (idx[q] >= half) return fail(ctx, MLH_ERR_INVALID, "index out of bounds");
+  if (nq == 0) return MLH_OK;
+  const uint64_t rec = 32ull * (1 + levels);
+  PoolBuf didx(ctx), dout(ctx);
+  MLH_TRY(didx.alloc(nq * sizeof(uint64_t)));
+  MLH_TRY(dout.alloc(nq * rec));
+  HIP_TRY(ctx, hipMemcpyAsync(didx.p, idx, nq * sizeof(uint64_t), hipMemcpyHostToDevice,
+                              ctx->stream));
+  HIP_TRY(ctx, launch_open_pairs(reinterpret_cast<const fe*>(dev_values), half,
+                                 reinterpret_cast<const uint8_t*>(dev_tree), levels,
+                                 didx.as<uint64_t>(), nq, dout.as<uint8_t>(), ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(out, dout.p, nq * rec, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
 }
 
 mlh_status mlh_fri_prove(mlh_ctx* ctx, const void* dev_code, uint32_t log_code, mlh_transcript* tr,

@@ -9,6 +9,9 @@
 //
 // * the twiddle comes from a two-level table of g^-1 (T_lo[e & 4095] *
 //   T_hi[e >> 12]), no 2^25-entry gen_pows array in HBM;
+// * a sharded layer (ShardMap, block-cyclic over ranks) folds with the same
+//   kernels: the pair partner is local, only the twiddle exponent needs the
+//   global index;
 // * `* 1/2` is a shift (x even: x >> 1, odd: (x + M) >> 1), not a modmul;
 // * fold_leaves fuses the fold with the next layer's Merkle leaf hash: lane j
 //   produces next[j] and next[j + n/4] (from pairs j and j + n/4), stores
@@ -32,26 +35,27 @@ __device__ __forceinline__ fe twiddle(const fe* tlo, const fe* thi, uint64_t e) 
 
 __global__ void __launch_bounds__(256)
 fri_fold_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next, fe r,
-                const fe* __restrict__ tlo, const fe* __restrict__ thi, uint32_t k, uint64_t n0) {
+                const fe* __restrict__ tlo, const fe* __restrict__ thi, uint32_t k, uint64_t n0,
+                ShardMap map) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t h = n / 2;
   if (i >= h) return;
   const fe a = fe_load(layer + i), b = fe_load(layer + i + h);
-  const fe tw = twiddle(tlo, thi, (i << k) & (n0 - 1));
+  const fe tw = twiddle(tlo, thi, (map.global(i) << k) & (n0 - 1));
   fe_store(next + i, fold_one(a, b, r, tw));
 }
 
 __global__ void __launch_bounds__(256)
 fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next,
                        uint8_t* __restrict__ leaves, fe r, const fe* __restrict__ tlo,
-                       const fe* __restrict__ thi, uint32_t k, uint64_t n0) {
+                       const fe* __restrict__ thi, uint32_t k, uint64_t n0, ShardMap map) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t h = n / 2, q = n / 4;
   if (j >= q) return;
   const fe a0 = fe_load(layer + j), b0 = fe_load(layer + j + h);
   const fe a1 = fe_load(layer + j + q), b1 = fe_load(layer + j + q + h);
-  const fe x0 = fold_one(a0, b0, r, twiddle(tlo, thi, (j << k) & (n0 - 1)));
-  const fe x1 = fold_one(a1, b1, r, twiddle(tlo, thi, ((j + q) << k) & (n0 - 1)));
+  const fe x0 = fold_one(a0, b0, r, twiddle(tlo, thi, (map.global(j) << k) & (n0 - 1)));
+  const fe x1 = fold_one(a1, b1, r, twiddle(tlo, thi, (map.global(j + q) << k) & (n0 - 1)));
   fe_store(next + j, x0);
   fe_store(next + j + q, x1);
   uint32_t m[8];
@@ -64,19 +68,20 @@ fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict_
 }
 
 hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe* tlo_inv,
-                           const fe* thi_inv, uint32_t k, uint64_t n0, hipStream_t st) {
+                           const fe* thi_inv, uint32_t k, uint64_t n0, hipStream_t st,
+                           ShardMap map) {
   const uint64_t h = n / 2;
   hipLaunchKernelGGL(fri_fold_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, st, layer,
-                     n, next, r, tlo_inv, thi_inv, k, n0);
+                     n, next, r, tlo_inv, thi_inv, k, n0, map);
   return hipGetLastError();
 }
 
 hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t* leaves, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
-                                  hipStream_t st) {
+                                  hipStream_t st, ShardMap map) {
   const uint64_t q = n / 4;
   hipLaunchKernelGGL(fri_fold_leaves_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, st,
-                     layer, n, next, leaves, r, tlo_inv, thi_inv, k, n0);
+                     layer, n, next, leaves, r, tlo_inv, thi_inv, k, n0, map);
   return hipGetLastError();
 }
 

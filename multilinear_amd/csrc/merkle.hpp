@@ -14,12 +14,28 @@ hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t b
                              uint32_t m, uint64_t count, uint8_t* leaves, hipStream_t st);
 hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st);
 
+// Block-cyclic shard layout of a layer spread over 2^log_p ranks: local
+// index l of rank `rank` holds global index
+//   ((l >> log_s) << (log_s + log_p)) | (rank << log_s) | (l & (2^log_s - 1))
+// (blocks of 2^log_s consecutive elements dealt round-robin to the ranks).
+// log_p = 0, log_s >= 40 is the identity (single GPU).
+struct ShardMap {
+  uint32_t log_s = 40;
+  uint32_t log_p = 0;
+  uint64_t rank = 0;
+  __host__ __device__ uint64_t global(uint64_t l) const {
+    return ((l >> log_s) << (log_s + log_p)) | (rank << log_s) | (l & ((1ull << log_s) - 1));
+  }
+};
+
 // FRI fold (fri.hip).  tables: two-level powers of g^-1 (g of order n0).
+// n is the LOCAL layer length; the twiddle exponent uses map.global(i).
 hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe* tlo_inv,
-                           const fe* thi_inv, uint32_t k, uint64_t n0, hipStream_t st);
+                           const fe* thi_inv, uint32_t k, uint64_t n0, hipStream_t st,
+                           ShardMap map = ShardMap());
 // Fold and hash the next layer's leaves (pairs (next[j], next[j + n/4])).
 hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t* leaves, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
-                                  hipStream_t st);
+                                  hipStream_t st, ShardMap map = ShardMap());
 
 }  // namespace mlh

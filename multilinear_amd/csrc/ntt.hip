@@ -47,6 +47,9 @@ struct PassGeom {
   uint64_t stride;      // W_p (elements between consecutive rows of this digit)
   uint64_t S;           // R_1*...*R_{p-1}
   uint32_t direct;      // 1: twiddle = tdir[jrest*k] (table of w^(S t), t < N/S)
+  uint64_t tpv;         // tiles per vector (batched transforms: blockIdx.x = b*tpv + tile)
+  uint64_t in_vstride;  // elements between consecutive input vectors
+  uint64_t out_vstride; // elements between consecutive output vectors
 };
 
 // Last pass: natural output index is K = k_1 + R_1*rev(mid) + (N/R_P)*k_P,
@@ -85,7 +88,10 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   const int c = tid % kCols;
   const int t = tid / kCols;
   const uint64_t N = 1ull << g.log_n;
-  const uint64_t tile = blockIdx.x;
+  const uint64_t vec = blockIdx.x / g.tpv;
+  const uint64_t tile = blockIdx.x % g.tpv;
+  in += vec * g.in_vstride;
+  out += vec * g.out_vstride;
 
   // ---- tile geometry -----------------------------------------------------
   uint64_t base, jrest = 0, k1 = 0, mid = 0;
@@ -242,6 +248,8 @@ ntt_small_kernel(const fe* __restrict__ in, fe* __restrict__ out, const fe* __re
                  uint32_t log_n, uint32_t in_len, fe scale, int apply_scale) {
   __shared__ fe lds[1024];
   const uint32_t N = 1u << log_n;
+  in += (uint64_t)blockIdx.x * in_len;
+  out += (uint64_t)blockIdx.x * N;
   for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
     const uint32_t src = bitrev(i, (int)log_n);
     lds[i] = src < in_len ? fe_load(in + src) : fe_zero();
@@ -345,10 +353,10 @@ void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr) {
 }
 
 hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n, uint64_t in_len,
-                            fe scale, bool apply_scale, hipStream_t st) {
+                            fe scale, bool apply_scale, hipStream_t st, uint64_t batch) {
   const uint32_t N = 1u << log_n;
   const uint32_t threads = N / 2 < 64 ? 64 : (N / 2 > 512 ? 512 : N / 2);
-  hipLaunchKernelGGL(ntt_small_kernel, dim3(1), dim3(threads), 0, st, in, out, tw, log_n,
+  hipLaunchKernelGGL(ntt_small_kernel, dim3((unsigned)batch), dim3(threads), 0, st, in, out, tw, log_n,
                      (uint32_t)in_len, scale, apply_scale ? 1 : 0);
   return hipGetLastError();
 }
@@ -360,7 +368,8 @@ void ntt_pass_label(const NttTables& tb, uint32_t p, bool zero_top, char* buf, s
 }
 
 hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables& tb,
-                             uint32_t log_n, bool zero_top, hipStream_t st, hipEvent_t* ev) {
+                             uint32_t log_n, bool zero_top, hipStream_t st, hipEvent_t* ev,
+                             uint64_t batch) {
   PassGeom g;
   g.log_n = log_n;
   g.nradix = tb.nradix;
@@ -376,7 +385,10 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
     g.S = S;
     g.direct = tb.tdir[p] != nullptr ? 1u : 0u;
     const bool last = (p + 1 == tb.nradix);
-    const uint64_t tiles = N / ((uint64_t)kCols << lr);
+    g.tpv = N / ((uint64_t)kCols << lr);
+    const uint64_t tiles = g.tpv * batch;
+    g.in_vstride = (p == 0) ? (zero_top ? N / 2 : N) : N;
+    g.out_vstride = N;
     // pass 0: in -> scratch; middle passes in place on scratch; the last pass
     // (a digit-reversal permutation of its tiles) scratch -> out.  The last
     // pass can never run in place: a block would overwrite tiles that other,

@@ -1,0 +1,449 @@
+"""Sharded NTT, Reed-Solomon encoding and FRI prove: one process per GPU.
+
+The reference (fr34za/multilinear) is single-node CPU code; its prover API is
+``Polynomial::ntt`` / ``reed_solomon`` (src/ntt/mod.rs:69-108, src/fri/mod.rs:19-28)
+and ``FriProof::prove`` (src/fri/mod.rs:261-285).  This module runs the same
+computations on P = 2^p GPUs with rank-local HIP kernels (libmlhip
+``mlh_shard_*``) between torch.distributed collectives (RCCL over xGMI for
+``nccl``; ``gloo`` for the CPU tests).  The proof it returns is byte-for-byte the
+single-GPU / reference proof of the same (natural order) codeword.
+
+Shard layouts ("Multi-GPU").  A vector of n = 2^log_n elements is
+spread block-cyclically with block S = 2^log_s: local index l of rank r holds
+global index ``((l >> log_s) << (log_s + p)) | (r << log_s) | (l mod S)``.
+
+* ``ntt`` / ``reed_solomon`` take the cyclic layout (S = 1: rank g holds
+  x[g], x[g+P], ...) and return block S = n / P^2 after ONE all-to-all:
+  local NTT of length n/P with generator w^P, all-to-all of contiguous
+  chunks, then a length-P DFT per column with twiddle w^(g j)
+  (``mlh_shard_ntt_cross``).
+* In the block-(n/P^2) layout every FRI pair (i, i + n/2) is local and every
+  aligned run of S leaves is a local Merkle subtree, so each FRI layer folds
+  and hashes locally; only the level-log_s subtree roots (P * T/2 digests,
+  T = local blocks) are all-gathered and the few top levels hashed on the host
+  (SURVEY.md 8(e) "the host hashes the top log2 P levels").
+* Each fold halves the number of local blocks T.  When T reaches 1 the layer is
+  in natural block order (rank r holds [r n/P, (r+1) n/P)); one all-to-all of
+  that (P times smaller) layer re-deals it with block n/P^2 and the local
+  folding continues.  Below ``gather_log`` the layer is all-gathered and the
+  remaining layers run replicated on every rank.
+* Query openings: the owning rank reads the pair and the subtree siblings from
+  HBM (``mlh_merkle_open_pairs``), the top siblings come from the host top
+  levels; the records are combined with one all-gather.
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+
+from . import _lib
+from .device import check, context, fe_bytes, lib, ptr
+
+M = 340282366920938463463374557953744961537
+LOG_BLOWUP = _lib.LOG_BLOWUP
+NUM_QUERIES = _lib.NUM_QUERIES
+
+
+def _log2(n):
+    if n < 1 or n & (n - 1):
+        raise ValueError("size must be a power of two")
+    return n.bit_length() - 1
+
+
+# ---------------------------------------------------------------------------
+# transport
+# ---------------------------------------------------------------------------
+
+class Transport:
+    """The collectives of the sharded path, on torch.distributed.
+
+    ``host_staged`` copies device tensors through host memory around each
+    collective (gloo with GPU buffers, e.g. several ranks sharing one GPU in
+    the tests); with ``nccl`` (RCCL) tensors go device to device over xGMI."""
+
+    def __init__(self, group=None, host_staged=False):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.host_staged = host_staged
+        if self.world & (self.world - 1) or self.world > 16:
+            raise ValueError("world size must be a power of two <= 16")
+
+    def _stage(self, t):
+        return t.cpu() if self.host_staged else t
+
+    def all_to_all(self, t):
+        """Chunk i of ``t`` (dim 0 split in world equal parts) goes to rank i;
+        chunk i of the result came from rank i."""
+        import torch
+
+        src = self._stage(t)
+        out = torch.empty_like(src)
+        self.dist.all_to_all_single(out, src.contiguous(), group=self.group)
+        return out.to(t.device) if self.host_staged else out
+
+    def all_gather(self, t):
+        """Concatenation over ranks (rank order) along dim 0."""
+        import torch
+
+        src = self._stage(t).contiguous()
+        out = torch.empty((self.world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype,
+                          device=src.device)
+        self.dist.all_gather_into_tensor(out, src, group=self.group)
+        return out.to(t.device) if self.host_staged else out
+
+    def gather_bytes(self, data: bytes):
+        """All-gather equal-length host byte strings -> list per rank."""
+        import torch
+
+        dev = "cpu" if self.host_staged or self.dist.get_backend(self.group) == "gloo" else \
+            "cuda:%d" % torch.cuda.current_device()
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev) if data else \
+            torch.zeros(0, dtype=torch.uint8, device=dev)
+        g = self.all_gather(t).cpu().numpy().tobytes()
+        n = len(data)
+        return [g[i * n:(i + 1) * n] for i in range(self.world)]
+
+
+# ---------------------------------------------------------------------------
+# rank-local HIP operations (libmlhip)
+# ---------------------------------------------------------------------------
+
+class HipOps:
+    """Rank-local steps on device tensors: field vectors (n, 4) int32, trees
+    uint8 ((2L - 1) * 32,).  Every call is a libmlhip kernel launch."""
+
+    def __init__(self, device=0):
+        self.device = device
+
+    def _ctx(self):
+        return context(self.device)
+
+    def empty(self, n):
+        import torch
+
+        return torch.empty((n, 4), dtype=torch.int32, device="cuda:%d" % self.device)
+
+    def empty_tree(self, leaves):
+        import torch
+
+        return torch.empty(int(lib().mlh_merkle_layers_bytes(leaves)), dtype=torch.uint8,
+                           device="cuda:%d" % self.device)
+
+    def ntt(self, x, gen, inverse=False):
+        c = self._ctx()
+        out = self.empty(x.shape[0])
+        fn = lib().mlh_intt if inverse else lib().mlh_ntt
+        check(fn(c, ptr(x), ptr(out), _log2(x.shape[0]), fe_bytes(gen)), c)
+        return out
+
+    def reed_solomon(self, coeffs, gen):
+        c = self._ctx()
+        out = self.empty(2 * coeffs.shape[0])
+        check(lib().mlh_reed_solomon(c, ptr(coeffs), _log2(coeffs.shape[0]), fe_bytes(gen),
+                                     ptr(out)), c)
+        return out
+
+    def cross(self, x, log_n, log_p, rank, gen, inverse):
+        c = self._ctx()
+        out = self.empty(x.shape[0])
+        check(lib().mlh_shard_ntt_cross(c, ptr(x), ptr(out), log_n, log_p, rank, fe_bytes(gen),
+                                        1 if inverse else 0), c)
+        return out
+
+    def commit_pairs(self, values):
+        c = self._ctx()
+        n = values.shape[0]
+        tree = self.empty_tree(n // 2)
+        check(lib().mlh_merkle_commit_pairs(c, ptr(values), _log2(n), ptr(tree), None), c)
+        return tree
+
+    def fold(self, values, k, log_domain, r, log_s, log_p, rank):
+        c = self._ctx()
+        n = values.shape[0]
+        out = self.empty(n // 2)
+        check(lib().mlh_shard_fri_fold(c, ptr(values), _log2(n), k, log_domain, fe_bytes(r),
+                                       ptr(out), log_s, log_p, rank), c)
+        return out
+
+    def fold_commit(self, values, k, log_domain, r, log_s, log_p, rank):
+        c = self._ctx()
+        n = values.shape[0]
+        out = self.empty(n // 2)
+        tree = self.empty_tree(n // 4)
+        check(lib().mlh_shard_fri_fold_commit(c, ptr(values), _log2(n), k, log_domain,
+                                              fe_bytes(r), ptr(out), ptr(tree), log_s, log_p,
+                                              rank), c)
+        return out, tree
+
+    def tree_level(self, tree, leaves, level):
+        """Digests of one level of a flattened tree (leaves first) -> bytes."""
+        off = sum(leaves >> i for i in range(level))
+        cnt = leaves >> level
+        return tree[32 * off:32 * (off + cnt)].cpu().numpy().tobytes()
+
+    def open_pairs(self, values, tree, levels, idx):
+        c = self._ctx()
+        nq = len(idx)
+        rec = 32 * (1 + levels)
+        out = (ctypes.c_uint8 * max(1, nq * rec))()
+        ia = (ctypes.c_uint64 * max(1, nq))(*idx)
+        check(lib().mlh_merkle_open_pairs(c, ptr(values), _log2(values.shape[0]), ptr(tree),
+                                          levels, ia, nq, out), c)
+        raw = bytes(out)
+        return [raw[q * rec:(q + 1) * rec] for q in range(nq)]
+
+    def to_host(self, values):
+        return values.cpu().contiguous().numpy().view(np.uint32).reshape(-1, 4)
+
+    def sync(self):
+        import torch
+
+        torch.cuda.synchronize(self.device)
+
+
+# ---------------------------------------------------------------------------
+# layouts
+# ---------------------------------------------------------------------------
+
+def block_owner(i, log_s, log_p):
+    """(rank, local index) of global index i in the block-(2^log_s) layout."""
+    r = (i >> log_s) & ((1 << log_p) - 1)
+    l = ((i >> (log_s + log_p)) << log_s) | (i & ((1 << log_s) - 1))
+    return r, l
+
+
+def shard_cyclic(x, world, rank):
+    """Host helper: rank's part of a natural-order array in the cyclic layout."""
+    return np.ascontiguousarray(x[rank::world])
+
+
+def shard_blocks(x, world, rank, log_s):
+    """Host helper: rank's part of a natural-order array in the block layout."""
+    S = 1 << log_s
+    return np.ascontiguousarray(x.reshape(-1, world, S, *x.shape[1:])[:, rank].reshape(
+        -1, *x.shape[1:]))
+
+
+def unshard_blocks(parts, log_s):
+    """Host helper: natural order from all ranks' block-layout parts."""
+    S = 1 << log_s
+    P = len(parts)
+    st = np.stack([p.reshape(-1, S, *p.shape[1:]) for p in parts], axis=1)
+    return st.reshape(-1, *parts[0].shape[1:])
+
+
+def cross_log_s(log_n, log_p):
+    return log_n - 2 * log_p
+
+
+# ---------------------------------------------------------------------------
+# sharded NTT / RS
+# ---------------------------------------------------------------------------
+
+def ntt(x_local, log_n, gen, tp, ops):
+    """Polynomial::ntt (ntt/mod.rs:69-110) of a 2^log_n vector in the cyclic
+    layout -> evaluations in the block-(2^log_n / P^2) layout."""
+    P = tp.world
+    if P == 1:
+        return ops.ntt(x_local, gen)
+    z = ops.ntt(x_local, pow(gen, P, M))
+    recv = tp.all_to_all(z)
+    return ops.cross(recv, log_n, _log2(P), tp.rank, gen, False)
+
+
+def intt(X_local, log_n, gen, tp, ops):
+    """LagrangePolynomial::intt (ntt/mod.rs:132-173): block-(n/P^2) layout in,
+    cyclic layout out."""
+    P = tp.world
+    if P == 1:
+        return ops.ntt(X_local, gen, inverse=True)
+    y = ops.cross(X_local, log_n, _log2(P), tp.rank, gen, True)
+    z = tp.all_to_all(y)
+    return ops.ntt(z, pow(gen, P, M), inverse=True)
+
+
+def reed_solomon(coeffs_local, log_n, gen, tp, ops):
+    """reed_solomon (fri/mod.rs:19-28) of 2^log_n coefficients in the cyclic
+    layout -> the 2^(log_n+1) codeword in the block-(2^(log_n+1) / P^2) layout."""
+    P = tp.world
+    if P == 1:
+        return ops.reed_solomon(coeffs_local, gen)
+    z = ops.reed_solomon(coeffs_local, pow(gen, P, M))
+    recv = tp.all_to_all(z)
+    return ops.cross(recv, log_n + LOG_BLOWUP, _log2(P), tp.rank, gen, False)
+
+
+# ---------------------------------------------------------------------------
+# sharded FRI prove
+# ---------------------------------------------------------------------------
+
+def _hash_node(a, b):
+    return hashlib.sha256(a + b).digest()
+
+
+class _Layer:
+    """One FRI layer: local values + local tree; ``log_p == 0`` = replicated."""
+
+    def __init__(self, values, tree, log_n, log_p, log_s, rank):
+        self.values, self.tree = values, tree
+        self.log_n, self.log_p, self.log_s, self.rank = log_n, log_p, log_s, rank
+        # tree levels held locally (siblings below this come from HBM)
+        self.sub_levels = log_s if log_p else log_n - 1
+        self.top = []  # host levels sub_levels .. root (lists of digests)
+
+    @property
+    def local_leaves(self):
+        return 1 << (self.log_n - 1 - self.log_p)
+
+    def root(self):
+        return self.top[-1][0]
+
+
+def _commit_top(layer, tp, ops):
+    """Combine the level-log_s subtree roots of all ranks; hash to the root."""
+    nodes_local = ops.tree_level(layer.tree, layer.local_leaves, layer.sub_levels)
+    if layer.log_p == 0:
+        layer.top = [[nodes_local[i:i + 32] for i in range(0, len(nodes_local), 32)]]
+        return
+    per_rank = tp.gather_bytes(nodes_local)
+    P, half_t = tp.world, len(nodes_local) // 32
+    level = [per_rank[h][32 * t:32 * t + 32] for t in range(half_t) for h in range(P)]
+    top = [level]
+    while len(top[-1]) > 1:
+        cur = top[-1]
+        top.append([_hash_node(cur[2 * i], cur[2 * i + 1]) for i in range(len(cur) // 2)])
+    layer.top = top
+
+
+def _open(layer, idx, tp, ops):
+    """Query records of one layer for the global leaf indices idx: this rank's
+    part (owned sharded leaves; all of them when replicated), others zero."""
+    leaves = 1 << (layer.log_n - 1)
+    rec_len = 32 * (1 + layer.log_n - 1)
+    out = [None] * len(idx)
+    mine, loc = [], []
+    for q, i in enumerate(idx):
+        i %= leaves
+        if layer.log_p:
+            r, l = block_owner(i, layer.log_s, layer.log_p)
+            if r != layer.rank:
+                continue
+        else:
+            l = i
+        mine.append(q)
+        loc.append(l)
+    recs = ops.open_pairs(layer.values, layer.tree, layer.sub_levels, loc) if loc else []
+    for q, rec in zip(mine, recs):
+        i = idx[q] % leaves
+        sibs = []
+        for lv in range(len(layer.top) - 1):
+            node = (i >> (layer.sub_levels + lv)) ^ 1
+            sibs.append(layer.top[lv][node])
+        out[q] = rec + b"".join(sibs)
+        assert len(out[q]) == rec_len
+    return [o if o is not None else bytes(rec_len) for o in out]
+
+
+def fri_prove(code_local, log_code, transcript, tp, ops, gather_log=16):
+    """FriProof::prove (fri/mod.rs:261-285) of a 2^log_code codeword held in
+    the block-(2^log_code / P^2) layout (``reed_solomon``'s output).
+
+    Every rank returns the same proof; it equals the single-GPU proof of the
+    natural-order codeword byte for byte."""
+    from .fri import FriProof
+
+    P, rank = tp.world, tp.rank
+    log_p = _log2(P)
+    if log_code < 2:
+        raise ValueError("log_code must be >= 2")
+    if log_p and log_code - 2 * log_p < 0:
+        raise ValueError("codeword too small for the world size")
+    gather_log = max(gather_log, 2 * log_p + 2)
+    n0 = log_code
+    if log_p and log_code > gather_log:
+        lay = _Layer(code_local, None, log_code, log_p, cross_log_s(log_code, log_p), rank)
+    else:
+        if log_p:
+            code_local = _to_natural(code_local, log_code, log_p, cross_log_s(log_code, log_p),
+                                     tp, ops)
+        lay = _Layer(code_local, None, log_code, 0, 0, rank)
+    lay.tree = ops.commit_pairs(lay.values)
+    _commit_top(lay, tp, ops)
+    layers = [lay]
+    transcript.absorb(lay.root())
+    last = None
+    for k in range(log_code - LOG_BLOWUP):
+        cur = layers[-1]
+        if (1 << cur.log_n) <= (1 << LOG_BLOWUP):
+            break
+        r = transcript.next_challenge()
+        log_next = cur.log_n - 1
+        if (1 << log_next) == (1 << LOG_BLOWUP):  # fri/mod.rs:116-126
+            nx = ops.fold(cur.values, k, n0, r, 40, 0, 0)
+            vals = ops.to_host(nx)
+            if not (vals[0] == vals[1]).all():
+                raise _lib.MlhError(_lib.MLH_ERR_NOT_RS_CODE, "not an RS code")
+            last = vals[0].tobytes()
+            transcript.absorb(last)
+            break
+        if cur.log_p == 0:
+            nv, tree = ops.fold_commit(cur.values, k, n0, r, 40, 0, 0)
+            lay = _Layer(nv, tree, log_next, 0, 0, rank)
+        elif log_next - cur.log_p - cur.log_s >= 1:  # >= 2 local blocks: pairs local
+            nv, tree = ops.fold_commit(cur.values, k, n0, r, cur.log_s, cur.log_p, rank)
+            lay = _Layer(nv, tree, log_next, cur.log_p, cur.log_s, rank)
+        else:  # folded layer is in natural block order: re-deal or gather
+            nv = ops.fold(cur.values, k, n0, r, cur.log_s, cur.log_p, rank)
+            if log_next > gather_log:
+                nv = tp.all_to_all(nv)
+                lay = _Layer(nv, None, log_next, log_p, cross_log_s(log_next, log_p), rank)
+            else:
+                nv = tp.all_gather(nv)
+                lay = _Layer(nv, None, log_next, 0, 0, rank)
+            lay.tree = ops.commit_pairs(lay.values)
+        _commit_top(lay, tp, ops)
+        layers.append(lay)
+        transcript.absorb(lay.root())
+    if last is None:
+        raise _lib.MlhError(_lib.MLH_ERR_INVALID, "fold produced no last element")
+
+    idx = []
+    for _ in range(NUM_QUERIES):  # fri/mod.rs:266-277
+        i = int.from_bytes(transcript.random()[:8], "little") % (1 << (log_code - 1))
+        idx.append(i)
+        transcript.absorb(i.to_bytes(8, "little"))
+    per_layer = [_open(l, idx, tp, ops) for l in layers]
+    mine = b"".join(per_layer[t][q] for q in range(NUM_QUERIES) for t in range(len(layers)))
+    if P > 1:
+        parts = tp.gather_bytes(mine)
+        acc = np.zeros(len(mine), dtype=np.uint8)
+        for p in parts:
+            acc |= np.frombuffer(p, dtype=np.uint8)
+        qraw = acc.tobytes()
+    else:
+        qraw = mine
+
+    proof = FriProof(log_code)
+    assert len(qraw) == proof.qbytes * NUM_QUERIES
+    proof.c.log_code = log_code
+    proof.c.num_trees = len(layers)
+    proof.c.num_queries = NUM_QUERIES
+    ctypes.memmove(proof._commit, b"".join(l.root() for l in layers), 32 * len(layers))
+    ctypes.memmove(proof._q, qraw, len(qraw))
+    for q, i in enumerate(idx):
+        proof._idx[q] = i
+    proof.c.last_elem[:] = list(last)
+    proof.c.last_random[:] = list(transcript.random())
+    return proof
+
+
+def _to_natural(values, log_n, log_p, log_s, tp, ops):
+    """Gather a block-layout vector to natural order on every rank."""
+    g = tp.all_gather(values)  # [rank][T][S]
+    S = 1 << log_s
+    P = 1 << log_p
+    return g.reshape(P, -1, S, 4).transpose(0, 1).reshape(-1, 4).contiguous()

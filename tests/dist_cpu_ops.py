@@ -1,0 +1,105 @@
+"""CPU stand-in for multilinear_amd.dist.HipOps (test infrastructure only).
+
+Lets the gloo world_size>1 CPU tests drive the real sharded orchestration
+(multilinear_amd/dist.py: layouts, all-to-all / all-gather exchanges, subtree
+root combination, query ownership) with every rank-local step computed by the
+oracle: C-oracle NTT / RS / Merkle, and the defining formulas of the
+cross-shard DFT and the index-mapped fold written out in Python ints."""
+import numpy as np
+import torch
+
+from multilinear_amd import dist as D
+from oracle import coracle as C
+from oracle import field as F
+
+INV2 = F.inv(2)
+
+
+def _ints(t):
+    a = t.contiguous().numpy().view(np.uint32).reshape(-1, 4)
+    return F.from_limbs(a)
+
+
+def _tensor(vals):
+    return torch.from_numpy(F.to_limbs(vals).view(np.int32).reshape(-1, 4).copy())
+
+
+def _limbs(t):
+    return t.contiguous().numpy().view(np.uint32).reshape(-1, 4)
+
+
+class CpuOps(D.HipOps):
+    def __init__(self):
+        super().__init__(device=None)
+
+    def empty(self, n):
+        return torch.zeros((n, 4), dtype=torch.int32)
+
+    def ntt(self, x, gen, inverse=False):
+        n = x.shape[0]
+        return torch.from_numpy(C.ntt(_limbs(x), n.bit_length() - 1, gen, inverse).view(np.int32))
+
+    def reed_solomon(self, coeffs, gen):
+        n = coeffs.shape[0]
+        return torch.from_numpy(C.reed_solomon(_limbs(coeffs), n.bit_length() - 1, gen).view(np.int32))
+
+    def cross(self, x, log_n, log_p, rank, gen, inverse):
+        P = 1 << log_p
+        S = 1 << (log_n - 2 * log_p)
+        rows = _ints(x)
+        w = F.inv(gen) if inverse else gen
+        wP = F.fpow(w, 1 << (log_n - log_p))
+        out = [0] * (P * S)
+        for jl in range(S):
+            j = rank * S + jl
+            col = [rows[a * S + jl] for a in range(P)]
+            for b in range(P):
+                if not inverse:  # X[t] = sum_g wP^(g t) w^(g j) R[g]
+                    v = sum(F.fpow(wP, a * b) * F.fpow(w, a * j) * col[a] for a in range(P))
+                else:  # Z[g] = 1/P w^(-g j) sum_t wP^(-g t) X[t]
+                    v = F.inv(P) * F.fpow(w, b * j) * sum(F.fpow(wP, a * b) * col[a] for a in range(P))
+                out[b * S + jl] = v % F.M
+        return _tensor(out)
+
+    def commit_pairs(self, values):
+        n = values.shape[0]
+        return torch.from_numpy(C.merkle_commit_pairs(_limbs(values), n.bit_length() - 1).reshape(-1))
+
+    def fold(self, values, k, log_domain, r, log_s, log_p, rank):
+        v = _ints(values)
+        n = len(v)
+        ginv = F.inv(F.pow_2_generator(log_domain))
+        out = []
+        for l in range(n // 2):
+            if log_p:
+                gi = ((l >> log_s) << (log_s + log_p)) | (rank << log_s) | (l & ((1 << log_s) - 1))
+            else:
+                gi = l
+            a, b = v[l], v[l + n // 2]
+            tw = F.fpow(ginv, (gi << k) % (1 << log_domain))
+            out.append(((a + b) + r * ((a - b) * tw % F.M)) * INV2 % F.M)
+        return _tensor(out)
+
+    def fold_commit(self, values, k, log_domain, r, log_s, log_p, rank):
+        nx = self.fold(values, k, log_domain, r, log_s, log_p, rank)
+        return nx, self.commit_pairs(nx)
+
+    def open_pairs(self, values, tree, levels, idx):
+        v = _limbs(values)
+        half = v.shape[0] // 2
+        t = tree.numpy().reshape(-1, 32)
+        recs = []
+        for i in idx:
+            rec = v[i].tobytes() + v[i + half].tobytes()
+            off = 0
+            for lv in range(levels):
+                rec += t[off + ((i >> lv) ^ 1)].tobytes()
+                off += half >> lv
+            recs.append(rec)
+        return recs
+
+    def to_host(self, values):
+        return _limbs(values)
+
+    def sync(self):
+        pass
