@@ -34,6 +34,7 @@
 
 using namespace mlh;
 
+
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------
@@ -41,8 +42,12 @@ struct TableKey {
   u128 base;
   uint64_t count;
   u128 scale;
+  int expand;
+  uint64_t cols = 0;  // 2D tables: count = rows, entry (k, j) = base^(k j mult)
+  uint64_t mult = 0;
   bool operator<(const TableKey& o) const {
-    return std::tie(base, count, scale) < std::tie(o.base, o.count, o.scale);
+    return std::tie(base, count, scale, expand, cols, mult) <
+           std::tie(o.base, o.count, o.scale, o.expand, o.cols, o.mult);
   }
 };
 
@@ -198,17 +203,36 @@ struct PoolBuf {
   }
 };
 
-// table[t] = base^t * scale, t < count, cached per context
-static mlh_status get_table(mlh_ctx* ctx, u128 base, uint64_t count, u128 scale, const fe** out) {
-  TableKey k{base, count, scale};
+// table[t] = base^t * scale, t < count, cached per context.  expand: 4 fe per
+// entry (t * 2^(32k), k < 4) for fe_mul_pre.
+static mlh_status get_table(mlh_ctx* ctx, u128 base, uint64_t count, u128 scale, const fe** out,
+                            bool expand = false) {
+  TableKey k{base, count, scale, expand ? 1 : 0};
   auto it = ctx->tables.find(k);
   if (it != ctx->tables.end()) {
     *out = it->second;
     return MLH_OK;
   }
   fe* d = nullptr;
-  HIP_TRY(ctx, hipMalloc(&d, count * sizeof(fe)));
-  HIP_TRY(ctx, launch_pow_table(d, to_fe(base), to_fe(scale), count, ctx->stream));
+  HIP_TRY(ctx, hipMalloc(&d, count * sizeof(fe) * (expand ? 4 : 1)));
+  HIP_TRY(ctx, launch_pow_table(d, to_fe(base), to_fe(scale), count, ctx->stream, expand));
+  ctx->tables[k] = d;
+  *out = d;
+  return MLH_OK;
+}
+
+// 2D table[k * cols + j] = base^(k j mult) * scale, k < rows, cached per context
+static mlh_status get_table2d(mlh_ctx* ctx, u128 base, uint64_t rows, uint64_t cols,
+                              uint64_t mult, u128 scale, const fe** out) {
+  TableKey k{base, rows, scale, 0, cols, mult};
+  auto it = ctx->tables.find(k);
+  if (it != ctx->tables.end()) {
+    *out = it->second;
+    return MLH_OK;
+  }
+  fe* d = nullptr;
+  HIP_TRY(ctx, hipMalloc(&d, rows * cols * sizeof(fe)));
+  HIP_TRY(ctx, launch_pow_table2d(d, to_fe(base), to_fe(scale), rows, cols, mult, ctx->stream));
   ctx->tables[k] = d;
   *out = d;
   return MLH_OK;
@@ -234,20 +258,21 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
   ntt_plan_radices(log_n, &tb->nradix, tb->logr);
   for (uint32_t p = 0; p < tb->nradix; ++p) {
     const uint64_t R = 1ull << tb->logr[p];
-    MLH_TRY(get_table(ctx, h_pow(w, N / R), R / 2, 1, &tb->tw[p]));
+    MLH_TRY(get_table(ctx, h_pow(w, N / R), R / 2, 1, &tb->tw[p], true));
   }
-  {
-    uint64_t S = 1;
-    for (uint32_t p = 0; p + 1 < tb->nradix; ++p) {  // the last pass has no twiddle
-      const uint64_t span = N / S;
-      if (span <= kDirectMax)
-        MLH_TRY(get_table(ctx, h_pow(w, S), span, p == 0 ? scale : (u128)1, &tb->tdir[p]));
-      S <<= tb->logr[p];
-    }
+  uint64_t S = 1;
+  for (uint32_t p = 0; p + 1 < tb->nradix; ++p) {  // the last pass has no twiddle
+    const uint64_t R = 1ull << tb->logr[p];
+    const uint32_t logw = log_n - (uint32_t)__builtin_ctzll(S) - tb->logr[p];
+    const uint32_t loga = logw < kTwLogA ? logw : kTwLogA;
+    const u128 ws = h_pow(w, S);
+    tb->loga[p] = loga;
+    MLH_TRY(get_table2d(ctx, ws, R, 1ull << loga, 1, p == 0 ? scale : (u128)1, &tb->ta[p]));
+    tb->tb[p] = nullptr;
+    if (logw > loga)
+      MLH_TRY(get_table2d(ctx, ws, R, 1ull << (logw - loga), 1ull << loga, 1, &tb->tb[p]));
+    S <<= tb->logr[p];
   }
-  MLH_TRY(get_table(ctx, w, 4096, scale, &tb->tlo0));
-  MLH_TRY(get_table(ctx, w, 4096, 1, &tb->tlo));
-  MLH_TRY(get_table(ctx, h_pow(w, 4096), hi_count(log_n), 1, &tb->thi));
   return MLH_OK;
 }
 

@@ -119,6 +119,15 @@ __device__ __forceinline__ fe fe_half(const fe& x) {
   return r;
 }
 
+// 16-byte vector load/store of one element (global_load_dwordx4).
+__device__ __forceinline__ fe fe_load(const fe* p) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  return fe{{v.x, v.y, v.z, v.w}};
+}
+__device__ __forceinline__ void fe_store(fe* p, const fe& x) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(x.w[0], x.w[1], x.w[2], x.w[3]);
+}
+
 // acc += a*b with the 64-bit carry-out of v_mad_u64_u32 (an SGPR lane mask)
 // counted into c2 by v_addc.  hipcc never uses that carry-out on its own and
 // instead shuffles {x, 0} register pairs (~37 v_mov per product).
@@ -227,6 +236,65 @@ __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
   return reduce_wide(r);
 }
 
+// a * w for a twiddle w supplied as its limb-shifted multiples
+// B_k = w * 2^(32k) mod M (k = 0..3, canonical; "expanded" tables):
+//   a * w = sum_k a_k * B_k   (< 2^162: four 32x128 rows summed column-wise)
+// then one fold of the top T < 2^34: T * 2^128 = T * 0x2D00 * 2^32 - T.
+// 17 v_mad_u64_u32 instead of 16 + 8 for the 256-bit product + two folds.
+__device__ __forceinline__ fe fe_mul_pre_r(const fe& a, const fe& B0, const fe& B1, const fe& B2,
+                                           const fe& B3) {
+  uint64_t acc;
+  uint32_t c2, r0, r1, r2, r3;
+  acc = (uint64_t)a.w[0] * B0.w[0];
+  c2 = 0;
+  mac_carry(acc, a.w[1], B1.w[0], c2);
+  mac_carry(acc, a.w[2], B2.w[0], c2);
+  mac_carry(acc, a.w[3], B3.w[0], c2);
+  r0 = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);  // < 2^34: the next first MAC cannot overflow
+  acc = (uint64_t)a.w[0] * B0.w[1] + acc;
+  c2 = 0;
+  mac_carry(acc, a.w[1], B1.w[1], c2);
+  mac_carry(acc, a.w[2], B2.w[1], c2);
+  mac_carry(acc, a.w[3], B3.w[1], c2);
+  r1 = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);
+  acc = (uint64_t)a.w[0] * B0.w[2] + acc;
+  c2 = 0;
+  mac_carry(acc, a.w[1], B1.w[2], c2);
+  mac_carry(acc, a.w[2], B2.w[2], c2);
+  mac_carry(acc, a.w[3], B3.w[2], c2);
+  r2 = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);
+  acc = (uint64_t)a.w[0] * B0.w[3] + acc;
+  c2 = 0;
+  mac_carry(acc, a.w[1], B1.w[3], c2);
+  mac_carry(acc, a.w[2], B2.w[3], c2);
+  mac_carry(acc, a.w[3], B3.w[3], c2);
+  r3 = (uint32_t)acc;
+  const uint32_t t_lo = (uint32_t)(acc >> 32), t_hi = c2;  // T = t_lo + t_hi 2^32 < 2^34
+  // value = r + T*0x2D00*2^32 - T  (>= 0, < 2^128 + 2^80)
+  const uint64_t v = (uint64_t)t_lo * kCmul;
+  const uint32_t vh = (uint32_t)(v >> 32) + __umul24(t_hi, kCmul);
+  uint32_t k, b;
+  fe s;
+  s.w[0] = r0;
+  s.w[1] = addc(r1, (uint32_t)v, 0u, &k);
+  s.w[2] = addc(r2, vh, k, &k);
+  s.w[3] = addc(r3, 0u, k, &k);
+  uint32_t hi = k;
+  s.w[0] = subb(s.w[0], t_lo, 0u, &b);
+  s.w[1] = subb(s.w[1], t_hi, b, &b);
+  s.w[2] = subb(s.w[2], 0u, b, &b);
+  s.w[3] = subb(s.w[3], 0u, b, &b);
+  hi -= b;  // value = s + hi*2^128, hi in {0,1}
+  return canon_with_carry(s, hi);
+}
+
+__device__ __forceinline__ fe fe_mul_pre(const fe& a, const fe* B) {
+  return fe_mul_pre_r(a, fe_load(B), fe_load(B + 1), fe_load(B + 2), fe_load(B + 3));
+}
+
 __device__ __forceinline__ fe fe_sqr(const fe& a) { return fe_mul(a, a); }
 
 __device__ __forceinline__ fe fe_pow(fe base, uint64_t e) {
@@ -237,15 +305,6 @@ __device__ __forceinline__ fe fe_pow(fe base, uint64_t e) {
     e >>= 1;
   }
   return acc;
-}
-
-// 16-byte vector load/store of one element (global_load_dwordx4).
-__device__ __forceinline__ fe fe_load(const fe* p) {
-  const uint4 v = *reinterpret_cast<const uint4*>(p);
-  return fe{{v.x, v.y, v.z, v.w}};
-}
-__device__ __forceinline__ void fe_store(fe* p, const fe& x) {
-  *reinterpret_cast<uint4*>(p) = make_uint4(x.w[0], x.w[1], x.w[2], x.w[3]);
 }
 
 }  // namespace mlh

@@ -46,7 +46,7 @@ struct PassGeom {
   uint32_t logr[kMaxPasses];
   uint64_t stride;      // W_p (elements between consecutive rows of this digit)
   uint64_t S;           // R_1*...*R_{p-1}
-  uint32_t direct;      // 1: twiddle = tdir[jrest*k] (table of w^(S t), t < N/S)
+  uint32_t loga;        // inter-pass twiddle split jrest = jh * 2^loga + jl
   uint64_t tpv;         // tiles per vector (batched transforms: blockIdx.x = b*tpv + tile)
   uint64_t in_vstride;  // elements between consecutive input vectors
   uint64_t out_vstride; // elements between consecutive output vectors
@@ -67,7 +67,7 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
   return rev;
 }
 
-// TW: 0 = two-level twiddle (T_lo * T_hi), 1 = direct table, 2 = none (last pass)
+// TW: 0 = two-table twiddle (TA * TB), 1 = one table (TA; W <= 2^8), 2 = none (last pass)
 // waves per SIMD the LDS tile allows (160 KiB/CU): caps VGPRs to match
 constexpr int pass_waves_per_simd(int logr) {
   return logr == 8 ? 5 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2));
@@ -77,8 +77,7 @@ template <int LOGR, int TW, bool ZERO_TOP>
 __global__ void __launch_bounds__(kCols * (1 << LOGR) / kEPT,
                                   TW == 2 ? 1 : pass_waves_per_simd(LOGR))
 ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
-                const fe* __restrict__ tlo, const fe* __restrict__ thi,
-                const fe* __restrict__ tdir, PassGeom g) {
+                const fe* __restrict__ ta, const fe* __restrict__ tb, PassGeom g) {
   constexpr int R = 1 << LOGR;
   constexpr int TPC = R / kEPT;  // threads per column
   constexpr bool LAST = TW == 2;
@@ -159,11 +158,11 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
           fe v = x[e1];
           if (s > 0) {
             // phase 1 (s0 == 0): j is a compile-time function of i -> uniform load
-            const fe w = tw[j << (LOGR - 1 - s)];
+            const fe* w = tw + 4 * (j << (LOGR - 1 - s));  // expanded table
             if (s0 == 0) {
-              if ((i & ((1 << s) - 1)) != 0) v = fe_mul(v, w);
+              if ((i & ((1 << s) - 1)) != 0) v = fe_mul_pre(v, w);
             } else {
-              v = fe_mul(v, w);
+              v = fe_mul_pre(v, w);
             }
           }
           const fe u = x[e0];
@@ -226,14 +225,11 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     const uint64_t k = pos[e];
     fe v = x[e];
     if (!LAST) {
-      fe w;
-      if (TW == 1) {
-        w = tdir[jrest * k];  // one lookup: w^(S * jrest * k)
-      } else {
-        const uint64_t ex = (jrest * k * g.S) & (N - 1);
-        w = fe_mul(tlo[ex & 4095], thi[ex >> 12]);
-      }
-      v = fe_mul(v, w);
+      // w_S^(jrest k) = TA[k][jl] * TB[k][jh]: the 8 columns of a tile are
+      // 8 consecutive jl, so a wave's lanes read 8 runs of 128 B per table
+      const uint64_t jl = jrest & ((1ull << g.loga) - 1);
+      v = fe_mul(v, ta[(k << g.loga) + jl]);
+      if (TW == 0) v = fe_mul(v, tb[k * (g.stride >> g.loga) + (jrest >> g.loga)]);
       fe_store(dst + k * rstride, v);
     } else {
       fe_store(out + kbase + (k << kshift), v);
@@ -275,13 +271,40 @@ ntt_small_kernel(const fe* __restrict__ in, fe* __restrict__ out, const fe* __re
   }
 }
 
-// table[t] = base^t, t < count (twiddle tables; one-time per context).
-__global__ void pow_table_kernel(fe* __restrict__ out, fe base, fe scale, uint64_t count) {
+// table[t] = base^t * scale, t < count (twiddle tables; one-time per context).
+// expand: entry t is the 4 limb-shifted multiples v * 2^(32k) (fe_mul_pre).
+__global__ void pow_table_kernel(fe* __restrict__ out, fe base, fe scale, uint64_t count,
+                                 int expand) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= count) return;
   fe v = fe_pow(base, t);
   v = fe_mul(v, scale);
-  fe_store(out + t, v);
+  if (!expand) {
+    fe_store(out + t, v);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    fe_store(out + 4 * t + k, v);
+    v = fe_mul(v, fe{{0u, 1u, 0u, 0u}});  // * 2^32
+  }
+}
+
+// 2D table out[k * cols + j] = base^(k * j * mult) * scale (inter-pass twiddles).
+__global__ void pow_table2d_kernel(fe* __restrict__ out, fe base, fe scale, uint64_t rows,
+                                   uint64_t cols, uint64_t mult) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * cols) return;
+  const uint64_t k = t / cols, j = t % cols;
+  fe_store(out + t, fe_mul(fe_pow(base, k * j * mult), scale));
+}
+
+hipError_t launch_pow_table2d(fe* out, fe base, fe scale, uint64_t rows, uint64_t cols,
+                              uint64_t mult, hipStream_t st) {
+  const uint64_t n = rows * cols;
+  hipLaunchKernelGGL(pow_table2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out,
+                     base, scale, rows, cols, mult);
+  return hipGetLastError();
 }
 
 // gen_pows[i] = g^i for i < count (NttField::pow_2_generator_powers,
@@ -297,27 +320,27 @@ __global__ void pow_series_kernel(fe* __restrict__ out, const fe* __restrict__ t
 
 template <int LOGR>
 static hipError_t launch_pass(bool last, bool zero_top, const fe* in, fe* out, const fe* tw,
-                              const fe* tlo, const fe* thi, const fe* tdir, const PassGeom& g,
-                              uint64_t tiles, hipStream_t st) {
+                              const fe* ta, const fe* tb, const PassGeom& g, uint64_t tiles,
+                              hipStream_t st) {
   constexpr int threads = kCols * (1 << LOGR) / kEPT;
   const dim3 grid((unsigned)tiles), blk(threads);
   if (last) {
-    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 2, false>), grid, blk, 0, st, in, out, tw, tlo, thi,
-                       tdir, g);
-  } else if (tdir) {
+    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 2, false>), grid, blk, 0, st, in, out, tw, ta, tb,
+                       g);
+  } else if (!tb) {
     if (zero_top)
-      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 1, true>), grid, blk, 0, st, in, out, tw, tlo, thi,
-                         tdir, g);
+      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 1, true>), grid, blk, 0, st, in, out, tw, ta, tb,
+                         g);
     else
-      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 1, false>), grid, blk, 0, st, in, out, tw, tlo,
-                         thi, tdir, g);
+      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 1, false>), grid, blk, 0, st, in, out, tw, ta, tb,
+                         g);
   } else {
     if (zero_top)
-      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 0, true>), grid, blk, 0, st, in, out, tw, tlo, thi,
-                         tdir, g);
+      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 0, true>), grid, blk, 0, st, in, out, tw, ta, tb,
+                         g);
     else
-      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 0, false>), grid, blk, 0, st, in, out, tw, tlo,
-                         thi, tdir, g);
+      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 0, false>), grid, blk, 0, st, in, out, tw, ta, tb,
+                         g);
   }
   return hipGetLastError();
 }
@@ -363,7 +386,7 @@ hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n,
 
 void ntt_pass_label(const NttTables& tb, uint32_t p, bool zero_top, char* buf, size_t n) {
   const bool last = p + 1 == tb.nradix;
-  const int tw = last ? 2 : (tb.tdir[p] ? 1 : 0);
+  const int tw = last ? 2 : (tb.tb[p] ? 0 : 1);
   snprintf(buf, n, "ntt_pass<%u,%d,%d>", tb.logr[p], tw, (zero_top && p == 0) ? 1 : 0);
 }
 
@@ -383,7 +406,7 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
     g.p = p;
     g.stride = W;
     g.S = S;
-    g.direct = tb.tdir[p] != nullptr ? 1u : 0u;
+    g.loga = tb.loga[p];
     const bool last = (p + 1 == tb.nradix);
     g.tpv = N / ((uint64_t)kCols << lr);
     const uint64_t tiles = g.tpv * batch;
@@ -396,16 +419,15 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
     const fe* src = (p == 0) ? in : scratch;
     fe* dst = last ? out : scratch;
     const bool zt = zero_top && p == 0;
-    const fe* tl = (p == 0) ? tb.tlo0 : tb.tlo;  // n^-1 scale applied once
     if (ev) (void)hipEventRecord(ev[p], st);
     hipError_t e;
     switch (lr) {
-      case 4: e = launch_pass<4>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
-      case 5: e = launch_pass<5>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
-      case 6: e = launch_pass<6>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
-      case 7: e = launch_pass<7>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
-      case 8: e = launch_pass<8>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
-      case 9: e = launch_pass<9>(last, zt, src, dst, tb.tw[p], tl, tb.thi, tb.tdir[p], g, tiles, st); break;
+      case 4: e = launch_pass<4>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 5: e = launch_pass<5>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 6: e = launch_pass<6>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 7: e = launch_pass<7>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 8: e = launch_pass<8>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 9: e = launch_pass<9>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
       default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;
@@ -419,9 +441,11 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
   return hipSuccess;
 }
 
-hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st) {
+hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st,
+                            bool expand) {
   const unsigned blocks = (unsigned)((count + 255) / 256);
-  hipLaunchKernelGGL(pow_table_kernel, dim3(blocks), dim3(256), 0, st, out, base, scale, count);
+  hipLaunchKernelGGL(pow_table_kernel, dim3(blocks), dim3(256), 0, st, out, base, scale, count,
+                     expand ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -8,21 +8,23 @@
 namespace mlh {
 
 constexpr int kMaxPasses = 6;
-constexpr uint64_t kDirectMax = 1ull << 16;  // 1 MiB direct twiddle tables
+constexpr uint32_t kTwLogA = 8;  // inter-pass twiddle split: TA covers 2^8 columns
 
 // Device twiddle tables for one (log_n, generator, direction).
 struct NttTables {
   uint32_t log_n = 0;
   uint32_t nradix = 0;
   uint32_t logr[kMaxPasses] = {0};
-  const fe* tw[kMaxPasses] = {nullptr};  // per pass: w_R^t, t < R/2
-  const fe* tlo0 = nullptr;              // pass 0: w^t * scale, t < 4096
-  const fe* tlo = nullptr;               // passes > 0: w^t, t < 4096
-  const fe* thi = nullptr;               // w^(4096 t), t < ceil(N/4096)
+  // stage twiddles, EXPANDED (4 fe per entry: the limb-shifted multiples
+  // consumed by fe_mul_pre): per pass w_R^t, t < R/2
+  const fe* tw[kMaxPasses] = {nullptr};
+  // inter-pass twiddle of pass p (not last): w_S^(jrest k), jrest < W, k < R,
+  // jrest = jh 2^loga + jl: TA[k][jl] = w_S^(k jl) (x n^-1 on pass 0 of the
+  // inverse), TB[k][jh] = w_S^(k jh 2^loga); TB = null when W <= 2^loga.
+  const fe* ta[kMaxPasses] = {nullptr};
+  const fe* tb[kMaxPasses] = {nullptr};
+  uint32_t loga[kMaxPasses] = {0};
   const fe* tw_small = nullptr;          // N <= 2^10: w^t, t < N/2
-  // per pass with N/S <= kDirectMax: w^(S t) (x scale on pass 0), t < N/S --
-  // the inter-pass twiddle becomes one lookup instead of lookup*lookup
-  const fe* tdir[kMaxPasses] = {nullptr};
   fe scale;                              // n^-1 (inverse) or 1
   bool inverse = false;
 };
@@ -41,7 +43,10 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
                              hipEvent_t* ev = nullptr, uint64_t batch = 1);
 // rocprof-style kernel label of pass p ("ntt_pass<8,0,0>")
 void ntt_pass_label(const NttTables& tb, uint32_t p, bool zero_top, char* buf, size_t n);
-hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st);
+hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st,
+                            bool expand = false);
+hipError_t launch_pow_table2d(fe* out, fe base, fe scale, uint64_t rows, uint64_t cols,
+                              uint64_t mult, hipStream_t st);
 hipError_t launch_pow_series(fe* out, const fe* tlo, const fe* thi, uint64_t count,
                              hipStream_t st);
 
