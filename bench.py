@@ -78,8 +78,8 @@ def load_pmc(kernel, log_n):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("kernel") == kernel and d.get("log_n") == log_n:
-        return d.get("traffic_bytes_per_launch")
+    if d.get("log_n") == log_n and kernel in d.get("kernels", {}):
+        return d["kernels"][kernel].get("traffic_bytes_per_launch")
     return None
 
 
@@ -275,7 +275,10 @@ def main():
         result["sumcheck_hbm_frac"] = sc_bytes / (sc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
 
     if not args.no_extras and args.fri_log:
-        result.update(config5(args, lib, ctx, local, world, rank, barrier))
+        try:
+            result.update(config5(args, lib, ctx, local, world, rank, barrier))
+        except Exception as e:  # keep the headline line; report the failure
+            result["config5_error"] = "%s: %s" % (type(e).__name__, e)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(log_n)

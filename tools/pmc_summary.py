@@ -17,7 +17,13 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL_PREFIX = {"ntt_pass<8,0,0>": "void mlh::ntt_pass_kernel<8, false, false>"}
+LABELS = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(3) for z in range(2)]
+
+
+def prefix(label):
+    """kernel-timer label "ntt_pass<8,0,0>" -> demangled rocprof kernel name prefix"""
+    r, tw, z = label[len("ntt_pass<"):-1].split(",")
+    return "void mlh::ntt_pass_kernel<%s, %s, %s>" % (r, tw, "true" if z == "1" else "false")
 
 
 def per_kernel(path, counter):
@@ -36,26 +42,24 @@ def main():
     shutil.copy(os.path.join(kdir, "run_kernel_stats.csv"), os.path.join(prof, "%s_kernel_stats.csv" % tag))
     fetch = per_kernel(os.path.join(fdir, "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(wdir, "run_counter_collection.csv"), "WRITE_SIZE")
-    out = {}
-    for label, prefix in KERNEL_PREFIX.items():
-        fk = [v for k, vs in fetch.items() if k.startswith(prefix) for v in vs]
-        wk = [v for k, vs in write.items() if k.startswith(prefix) for v in vs]
+    out = {"log_n": log_n, "round": tag,
+           "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts "
+                         "half of a wide stream)",
+           "alg_bytes_per_launch": 32 * (1 << log_n), "kernels": {}}
+    for label in LABELS:
+        pre = prefix(label)
+        fk = [v for k, vs in fetch.items() if k.startswith(pre) for v in vs]
+        wk = [v for k, vs in write.items() if k.startswith(pre) for v in vs]
         if not fk or not wk:
             continue
         f_kib = sum(fk) / len(fk)
         w_kib = sum(wk) / len(wk)
-        traffic = (2.0 * f_kib + w_kib) * 1024.0
-        out = {
-            "kernel": label,
-            "log_n": log_n,
-            "round": tag,
+        out["kernels"][label] = {
             "launches_fetch_pass": len(fk),
             "launches_write_pass": len(wk),
             "FETCH_SIZE_KiB_avg": f_kib,
             "WRITE_SIZE_KiB_avg": w_kib,
-            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half of a wide stream)",
-            "traffic_bytes_per_launch": traffic,
-            "alg_bytes_per_launch": 32 * (1 << log_n),
+            "traffic_bytes_per_launch": (2.0 * f_kib + w_kib) * 1024.0,
         }
     with open(os.path.join(prof, "pmc_ntt.json"), "w") as f:
         json.dump(out, f, indent=1)
