@@ -31,6 +31,7 @@
 #include "ntt.hpp"
 #include "sha256.hpp"
 #include "sumcheck.hpp"
+#include "transcript_dev.hpp"
 
 using namespace mlh;
 
@@ -670,26 +671,112 @@ mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
   return MLH_OK;
 }
 
+}  // extern "C"
+
+// FriProverData::fold (fri/mod.rs:136-145) with the transcript on the device:
+// every round's challenge is derived on the GPU from the root just written,
+// so the whole commit phase is one stream of kernels with a single sync at
+// the end; the host transcript then replays the same absorbs (root_0,
+// root_1, ..., last element) and ends in the identical state.
+static_assert(sizeof(DevSha) == sizeof(HostSha256), "transcript layouts differ");
+
+static mlh_status fri_fold_device(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                                  mlh_transcript* tr, mlh_fri_prover** out) {
+  if (!ctx || !dev_code || !tr || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_code < 2 || log_code > 40)
+    return fail(ctx, log_code < 2 ? MLH_ERR_INVALID : MLH_ERR_NOT_POW2,
+                "fold needs 4 <= code length <= 2^40");
+  std::unique_ptr<mlh_fri_prover> p(new mlh_fri_prover());
+  p->ctx = ctx;
+  p->log_code = log_code;
+  const fe *tlo, *thi;
+  MLH_TRY(fold_tables(ctx, log_code, &tlo, &thi));
+  const uint32_t steps = log_code - MLH_LOG_BLOWUP;
+  // device scratch: transcript state, one challenge per round, last pair, flag
+  PoolBuf scratch(ctx);
+  const size_t off_r = 128, off_last = off_r + 16 * (steps + 1), off_flag = off_last + 16;
+  MLH_TRY(scratch.alloc(off_flag + 16));
+  uint8_t* sb = scratch.as<uint8_t>();
+  DevSha* dt = reinterpret_cast<DevSha*>(sb);
+  fe* rbuf = reinterpret_cast<fe*>(sb + off_r);
+  memcpy(ctx->pinned, &tr->sha, sizeof(DevSha));
+  HIP_TRY(ctx, hipMemcpyAsync(dt, ctx->pinned, sizeof(DevSha), hipMemcpyHostToDevice, ctx->stream));
+
+  FriLayer l0;
+  l0.values = reinterpret_cast<const fe*>(dev_code);
+  l0.log_n = log_code;
+  {
+    const uint64_t L = 1ull << (log_code - 1);
+    void* tree;
+    MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
+    l0.tree = reinterpret_cast<uint8_t*>(tree);
+    p->layers.push_back(l0);
+    HIP_TRY(ctx, launch_leaf_pairs(l0.values, L, l0.tree, ctx->stream));
+    HIP_TRY(ctx, launch_merkle_levels(l0.tree, L, ctx->stream));
+    HIP_TRY(ctx, launch_transcript_absorb(dt, l0.tree + (2 * L - 2) * 32, 32, rbuf, ctx->stream));
+  }
+  bool done = false;
+  for (uint32_t k = 0; k < steps && !done; ++k) {
+    const FriLayer cur = p->layers.back();
+    const uint32_t log_n = cur.log_n;
+    const uint64_t half_n = 1ull << (log_n - 1);
+    void* vals;
+    MLH_TRY(pool_alloc(ctx, half_n * sizeof(fe), &vals));
+    if (half_n == (1ull << MLH_LOG_BLOWUP)) {  // fri/mod.rs:116-126
+      HIP_TRY(ctx, launch_fri_fold(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), fe{},
+                                   tlo, thi, k, 1ull << log_code, ctx->stream, ShardMap(),
+                                   rbuf + k));
+      HIP_TRY(ctx, launch_fri_last(reinterpret_cast<const fe*>(vals), dt,
+                                   reinterpret_cast<uint32_t*>(sb + off_flag),
+                                   reinterpret_cast<fe*>(sb + off_last), ctx->stream));
+      pool_free(ctx, vals);
+      done = true;
+      break;
+    }
+    FriLayer nx;
+    nx.log_n = log_n - 1;
+    nx.owned_values = vals;
+    nx.values = reinterpret_cast<const fe*>(vals);
+    const uint64_t L = half_n / 2;
+    void* tree;
+    MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
+    nx.tree = reinterpret_cast<uint8_t*>(tree);
+    p->layers.push_back(nx);
+    HIP_TRY(ctx, launch_fri_fold_leaves(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
+                                        nx.tree, fe{}, tlo, thi, k, 1ull << log_code, ctx->stream,
+                                        ShardMap(), rbuf + k));
+    HIP_TRY(ctx, launch_merkle_levels(nx.tree, L, ctx->stream));
+    HIP_TRY(ctx, launch_transcript_absorb(dt, nx.tree + (2 * L - 2) * 32, 32, rbuf + k + 1,
+                                          ctx->stream));
+  }
+  if (!done) return fail(ctx, MLH_ERR_INVALID, "fold produced no last element");
+  // one sync: roots, last element, RS flag
+  const size_t nt = p->layers.size();
+  for (size_t t = 0; t < nt; ++t) {
+    const uint64_t L = 1ull << (p->layers[t].log_n - 1);
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 32 * t, p->layers[t].tree + (2 * L - 2) * 32, 32,
+                                hipMemcpyDeviceToHost, ctx->stream));
+  }
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 32 * nt, sb + off_last, 32, hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (size_t t = 0; t < nt; ++t) memcpy(p->layers[t].root, ctx->pinned + 32 * t, 32);
+  uint32_t flag;
+  memcpy(&flag, ctx->pinned + 32 * nt + 16, 4);
+  if (flag) return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
+  memcpy(p->last, ctx->pinned + 32 * nt, 16);
+  p->has_last = true;
+  for (size_t t = 0; t < nt; ++t) mlh_transcript_absorb(tr, p->layers[t].root, 32);
+  mlh_transcript_absorb(tr, p->last, 16);
+  *out = p.release();
+  return MLH_OK;
+}
+
+extern "C" {
+
 mlh_status mlh_fri_prover_fold(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
                                mlh_transcript* tr, mlh_fri_prover** out) {
-  mlh_fri_prover* p = nullptr;
-  MLH_TRY(mlh_fri_prover_init(ctx, dev_code, log_code, tr, &p));
-  const uint32_t steps = log_code - MLH_LOG_BLOWUP;
-  for (uint32_t k = 0; k < steps; ++k) {
-    uint8_t r[16];
-    mlh_transcript_next_challenge(tr, r);
-    mlh_status s = mlh_fri_prover_fold_step(ctx, p, k, r, tr);
-    if (s != MLH_OK) {
-      mlh_fri_prover_destroy(p);
-      return s;
-    }
-  }
-  if (!p->has_last) {
-    mlh_fri_prover_destroy(p);
-    return fail(ctx, MLH_ERR_INVALID, "fold produced no last element (log_code < 2)");
-  }
-  *out = p;
-  return MLH_OK;
+  return fri_fold_device(ctx, dev_code, log_code, tr, out);
 }
 
 uint32_t mlh_fri_prover_num_trees(const mlh_fri_prover* p) {

@@ -20,6 +20,7 @@
 #include "field.hpp"
 #include "merkle.hpp"
 #include "sha256.hpp"
+#include "transcript_dev.hpp"
 
 namespace mlh {
 
@@ -36,7 +37,8 @@ __device__ __forceinline__ fe twiddle(const fe* tlo, const fe* thi, uint64_t e) 
 __global__ void __launch_bounds__(256)
 fri_fold_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next, fe r,
                 const fe* __restrict__ tlo, const fe* __restrict__ thi, uint32_t k, uint64_t n0,
-                ShardMap map) {
+                ShardMap map, const fe* __restrict__ rp) {
+  if (rp) r = fe_load(rp);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t h = n / 2;
   if (i >= h) return;
@@ -48,7 +50,9 @@ fri_fold_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next,
 __global__ void __launch_bounds__(256)
 fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next,
                        uint8_t* __restrict__ leaves, fe r, const fe* __restrict__ tlo,
-                       const fe* __restrict__ thi, uint32_t k, uint64_t n0, ShardMap map) {
+                       const fe* __restrict__ thi, uint32_t k, uint64_t n0, ShardMap map,
+                       const fe* __restrict__ rp) {
+  if (rp) r = fe_load(rp);
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t h = n / 2, q = n / 4;
   if (j >= q) return;
@@ -69,19 +73,54 @@ fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict_
 
 hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe* tlo_inv,
                            const fe* thi_inv, uint32_t k, uint64_t n0, hipStream_t st,
-                           ShardMap map) {
+                           ShardMap map, const fe* r_dev) {
   const uint64_t h = n / 2;
   hipLaunchKernelGGL(fri_fold_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, st, layer,
-                     n, next, r, tlo_inv, thi_inv, k, n0, map);
+                     n, next, r, tlo_inv, thi_inv, k, n0, map, r_dev);
   return hipGetLastError();
 }
 
 hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t* leaves, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
-                                  hipStream_t st, ShardMap map) {
+                                  hipStream_t st, ShardMap map, const fe* r_dev) {
   const uint64_t q = n / 4;
   hipLaunchKernelGGL(fri_fold_leaves_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, st,
-                     layer, n, next, leaves, r, tlo_inv, thi_inv, k, n0, map);
+                     layer, n, next, leaves, r, tlo_inv, thi_inv, k, n0, map, r_dev);
+  return hipGetLastError();
+}
+
+}  // namespace mlh
+
+// ---- device transcript steps (transcript_dev.hpp) ---------------------------
+namespace mlh {
+
+__global__ void transcript_absorb_kernel(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out) {
+  if (threadIdx.x != 0) return;
+  DevSha s = *t;
+  dsha_update(s, src, n);
+  *t = s;
+  if (r_out) fe_store(r_out, dsha_challenge(s));
+}
+
+hipError_t launch_transcript_absorb(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out,
+                                    hipStream_t st) {
+  hipLaunchKernelGGL(transcript_absorb_kernel, dim3(1), dim3(64), 0, st, t, src, n, r_out);
+  return hipGetLastError();
+}
+
+__global__ void fri_last_kernel(const fe* vals, DevSha* t, uint32_t* flag, fe* last_out) {
+  if (threadIdx.x != 0) return;
+  const fe a = fe_load(vals), b = fe_load(vals + 1);
+  *flag = fe_eq(a, b) ? 0u : 1u;
+  fe_store(last_out, a);
+  DevSha s = *t;
+  dsha_update(s, reinterpret_cast<const uint8_t*>(last_out), 16);
+  *t = s;
+}
+
+hipError_t launch_fri_last(const fe* vals, DevSha* t, uint32_t* flag, fe* last_out,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(fri_last_kernel, dim3(1), dim3(64), 0, st, vals, t, flag, last_out);
   return hipGetLastError();
 }
 

@@ -29,13 +29,15 @@ struct ShardMap {
 };
 
 // FRI fold (fri.hip).  tables: two-level powers of g^-1 (g of order n0).
+// r_dev (optional): read the challenge from device memory instead of r.
 // n is the LOCAL layer length; the twiddle exponent uses map.global(i).
 hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe* tlo_inv,
                            const fe* thi_inv, uint32_t k, uint64_t n0, hipStream_t st,
-                           ShardMap map = ShardMap());
+                           ShardMap map = ShardMap(), const fe* r_dev = nullptr);
 // Fold and hash the next layer's leaves (pairs (next[j], next[j + n/4])).
 hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t* leaves, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
-                                  hipStream_t st, ShardMap map = ShardMap());
+                                  hipStream_t st, ShardMap map = ShardMap(),
+                                  const fe* r_dev = nullptr);
 
 }  // namespace mlh

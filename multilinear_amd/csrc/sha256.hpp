@@ -1,5 +1,6 @@
 // SHA-256 compression on gfx950 VALU (FIPS 180-4), one message per lane.
 //
+// Sigma/sigma 3-way XORs are single v_bitop3_b32 (gfx950).
 // Reference: the sha2 0.10.8 crate (Cargo.lock:261-269) used by
 // src/merkle_tree/mod.rs:178-189 (hash_leaf / hash_node) and
 // src/transcript.rs.  Rotations are v_alignbit_b32, Ch/Maj are v_bfi_b32,
@@ -14,6 +15,11 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) {
   return __builtin_amdgcn_alignbit(x, x, n);
 }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+// a ^ b ^ c in one full-rate v_bitop3_b32 (truth table 0x96); hipcc emits two
+// v_xor_b32 for the Sigma/sigma functions otherwise.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
 #define MLH_SHA_K                                                                               \
   {0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,   \
@@ -45,14 +51,14 @@ __device__ __forceinline__ void sha256_compress(Sha256State& st, uint32_t w[16])
   for (int t = 0; t < 64; ++t) {
     if (t >= 16) {
       const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-      const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
       w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
     }
-    const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
     const uint32_t ch = (e & f) ^ (~e & g);
     const uint32_t t1 = h + S1 + ch + K[t] + w[t & 15];
-    const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
     const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
     const uint32_t t2 = S0 + maj;
     h = g;
@@ -74,12 +80,54 @@ __device__ __forceinline__ void sha256_compress(Sha256State& st, uint32_t w[16])
   st.h[7] += h;
 }
 
-// Compression of the constant padding block of a 64-byte message
-// (0x80, zeros, bit length 512): its message schedule is a compile-time
-// constant, so only the round function runs.
+// K[t] + W[t] of the constant padding block of a 64-byte message (0x80,
+// zeros, bit length 512): its message schedule is a compile-time constant.
+struct Pad64KW {
+  uint32_t v[64];
+  constexpr Pad64KW() : v() {
+    constexpr uint32_t K[64] = MLH_SHA_K;
+    uint32_t w[64] = {};
+    w[0] = 0x80000000u;
+    w[15] = 512u;
+    for (int t = 16; t < 64; ++t) {
+      const uint32_t a = w[t - 15], b = w[t - 2];
+      const uint32_t s0 = ((a >> 7) | (a << 25)) ^ ((a >> 18) | (a << 14)) ^ (a >> 3);
+      const uint32_t s1 = ((b >> 17) | (b << 15)) ^ ((b >> 19) | (b << 13)) ^ (b >> 10);
+      w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+    }
+    for (int t = 0; t < 64; ++t) v[t] = K[t] + w[t];
+  }
+};
+
+// Compression of that padding block: only the round function runs.
 __device__ __forceinline__ void sha256_compress_pad64(Sha256State& st) {
-  uint32_t w[16] = {0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512u};
-  sha256_compress(st, w);  // w is constant-folded after full unrolling
+  constexpr Pad64KW KW;
+  uint32_t a = st.h[0], b = st.h[1], c = st.h[2], d = st.h[3];
+  uint32_t e = st.h[4], f = st.h[5], g = st.h[6], h = st.h[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + KW.v[t];
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + S0 + maj;
+  }
+  st.h[0] += a;
+  st.h[1] += b;
+  st.h[2] += c;
+  st.h[3] += d;
+  st.h[4] += e;
+  st.h[5] += f;
+  st.h[6] += g;
+  st.h[7] += h;
 }
 
 // SHA256(32-byte message), words given big-endian-interpreted.

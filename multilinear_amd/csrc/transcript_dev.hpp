@@ -1,0 +1,80 @@
+// Device-side Fiat-Shamir transcript (one lane): the same SHA-256 state
+// machine as HostSha256 (src/transcript.rs semantics: absorb = update,
+// random = digest of a clone, next_challenge = F::from(u128_le(random[..16]))).
+// Lets the FRI / PCS commit loops derive each round's challenge on the GPU
+// from the root just written to HBM, so the loop never waits on the host; the
+// host transcript is brought to the same state afterwards by replaying the
+// same absorbs (it is a pure function of the absorbed bytes).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "field.hpp"
+#include "sha256.hpp"
+
+namespace mlh {
+
+// Byte-identical layout to HostSha256 {h[8], buf[64], len}.
+struct DevSha {
+  uint32_t h[8];
+  uint8_t buf[64];
+  uint64_t len;
+};
+
+__device__ inline void dsha_compress_buf(DevSha& s) {
+  uint32_t w[16];
+  for (int i = 0; i < 16; ++i)
+    w[i] = ((uint32_t)s.buf[4 * i] << 24) | ((uint32_t)s.buf[4 * i + 1] << 16) |
+           ((uint32_t)s.buf[4 * i + 2] << 8) | (uint32_t)s.buf[4 * i + 3];
+  Sha256State st;
+  for (int i = 0; i < 8; ++i) st.h[i] = s.h[i];
+  sha256_compress(st, w);
+  for (int i = 0; i < 8; ++i) s.h[i] = st.h[i];
+}
+
+__device__ inline void dsha_update(DevSha& s, const uint8_t* p, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    s.buf[s.len % 64] = p[i];
+    s.len += 1;
+    if (s.len % 64 == 0) dsha_compress_buf(s);
+  }
+}
+
+// digest of a clone (the state itself is unchanged)
+__device__ inline void dsha_digest(const DevSha& s0, uint8_t out[32]) {
+  DevSha c = s0;
+  const uint64_t bits = c.len * 8;
+  const uint8_t one = 0x80, z = 0;
+  dsha_update(c, &one, 1);
+  while (c.len % 64 != 56) dsha_update(c, &z, 1);
+  uint8_t lb[8];
+  for (int i = 0; i < 8; ++i) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
+  dsha_update(c, lb, 8);
+  for (int i = 0; i < 8; ++i) {
+    out[4 * i] = (uint8_t)(c.h[i] >> 24);
+    out[4 * i + 1] = (uint8_t)(c.h[i] >> 16);
+    out[4 * i + 2] = (uint8_t)(c.h[i] >> 8);
+    out[4 * i + 3] = (uint8_t)c.h[i];
+  }
+}
+
+// Field128::from(u128) (field.rs:138-142): one conditional subtraction of M.
+__device__ inline fe dsha_challenge(const DevSha& s) {
+  uint8_t d[32];
+  dsha_digest(s, d);
+  fe v;
+  for (int i = 0; i < 4; ++i)
+    v.w[i] = (uint32_t)d[4 * i] | ((uint32_t)d[4 * i + 1] << 8) | ((uint32_t)d[4 * i + 2] << 16) |
+             ((uint32_t)d[4 * i + 3] << 24);
+  return canon_with_carry(v, 0u);
+}
+
+// absorb n bytes from device memory, then (if r_out) write next_challenge()
+hipError_t launch_transcript_absorb(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out,
+                                    hipStream_t st);
+// final FRI layer (2 values): flag = (v0 != v1) ("not an RS code"),
+// absorb LE16(v0), copy v0 to last_out
+hipError_t launch_fri_last(const fe* vals, DevSha* t, uint32_t* flag, fe* last_out,
+                           hipStream_t st);
+
+}  // namespace mlh
