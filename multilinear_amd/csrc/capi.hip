@@ -680,32 +680,39 @@ mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
 // root_1, ..., last element) and ends in the identical state.
 static_assert(sizeof(DevSha) == sizeof(HostSha256), "transcript layouts differ");
 
-static mlh_status fri_fold_device(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
-                                  mlh_transcript* tr, mlh_fri_prover** out) {
-  if (!ctx || !dev_code || !tr || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
-  if (log_code < 2 || log_code > 40)
-    return fail(ctx, log_code < 2 ? MLH_ERR_INVALID : MLH_ERR_NOT_POW2,
-                "fold needs 4 <= code length <= 2^40");
-  std::unique_ptr<mlh_fri_prover> p(new mlh_fri_prover());
-  p->ctx = ctx;
-  p->log_code = log_code;
-  const fe *tlo, *thi;
-  MLH_TRY(fold_tables(ctx, log_code, &tlo, &thi));
-  const uint32_t steps = log_code - MLH_LOG_BLOWUP;
-  // device scratch: transcript state, one challenge per round, last pair, flag
-  PoolBuf scratch(ctx);
-  const size_t off_r = 128, off_last = off_r + 16 * (steps + 1), off_flag = off_last + 16;
-  MLH_TRY(scratch.alloc(off_flag + 16));
-  uint8_t* sb = scratch.as<uint8_t>();
-  DevSha* dt = reinterpret_cast<DevSha*>(sb);
-  fe* rbuf = reinterpret_cast<fe*>(sb + off_r);
-  memcpy(ctx->pinned, &tr->sha, sizeof(DevSha));
-  HIP_TRY(ctx, hipMemcpyAsync(dt, ctx->pinned, sizeof(DevSha), hipMemcpyHostToDevice, ctx->stream));
+// Device-side commit loop state: [transcript | r_0..r_steps | last (16) |
+// flag (16) | roots 32 x (steps + 1) | polys 32 x steps | prev (16)].
+struct FriDevLoop {
+  mlh_ctx* ctx;
+  mlh_fri_prover* p;
+  const fe *tlo = nullptr, *thi = nullptr;
+  PoolBuf scratch;
+  size_t off_r = 128, off_last = 0, off_flag = 0, off_roots = 0, off_polys = 0, off_prev = 0;
+  bool done = false;
+  explicit FriDevLoop(mlh_ctx* c, mlh_fri_prover* pr) : ctx(c), p(pr), scratch(c) {}
+  uint8_t* sb() const { return scratch.as<uint8_t>(); }
+  DevSha* dt() const { return reinterpret_cast<DevSha*>(sb()); }
+  fe* r(uint32_t k) const { return reinterpret_cast<fe*>(sb() + off_r) + k; }
+  uint8_t* root(uint32_t t) const { return sb() + off_roots + 32 * t; }
+  fe* poly(uint32_t k) const { return reinterpret_cast<fe*>(sb() + off_polys) + 2 * k; }
+  fe* prev() const { return reinterpret_cast<fe*>(sb() + off_prev); }
 
-  FriLayer l0;
-  l0.values = reinterpret_cast<const fe*>(dev_code);
-  l0.log_n = log_code;
-  {
+  mlh_status init(const void* dev_code, uint32_t log_code, const mlh_transcript* tr,
+                  bool challenge_after_root0) {
+    const uint32_t steps = log_code - MLH_LOG_BLOWUP;
+    off_last = off_r + 16 * (steps + 1);
+    off_flag = off_last + 16;
+    off_roots = off_flag + 16;
+    off_polys = off_roots + 32 * (steps + 1);
+    off_prev = off_polys + 32 * steps;
+    MLH_TRY(scratch.alloc(off_prev + 16));
+    MLH_TRY(fold_tables(ctx, log_code, &tlo, &thi));
+    memcpy(ctx->pinned, &tr->sha, sizeof(DevSha));
+    HIP_TRY(ctx, hipMemcpyAsync(dt(), ctx->pinned, sizeof(DevSha), hipMemcpyHostToDevice,
+                                ctx->stream));
+    FriLayer l0;
+    l0.values = reinterpret_cast<const fe*>(dev_code);
+    l0.log_n = log_code;
     const uint64_t L = 1ull << (log_code - 1);
     void* tree;
     MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
@@ -713,25 +720,31 @@ static mlh_status fri_fold_device(mlh_ctx* ctx, const void* dev_code, uint32_t l
     p->layers.push_back(l0);
     HIP_TRY(ctx, launch_leaf_pairs(l0.values, L, l0.tree, ctx->stream));
     HIP_TRY(ctx, launch_merkle_levels(l0.tree, L, ctx->stream));
-    HIP_TRY(ctx, launch_transcript_absorb(dt, l0.tree + (2 * L - 2) * 32, 32, rbuf, ctx->stream));
+    HIP_TRY(ctx, launch_transcript_absorb(dt(), l0.tree + (2 * L - 2) * 32, 32,
+                                          challenge_after_root0 ? r(0) : nullptr, ctx->stream,
+                                          root(0)));
+    return MLH_OK;
   }
-  bool done = false;
-  for (uint32_t k = 0; k < steps && !done; ++k) {
+
+  // fold_step k with the challenge at rp (device); absorbs the new root (or
+  // the last element); writes next_challenge() to r(k + 1) if challenge_next.
+  mlh_status step(uint32_t k, const fe* rp, bool challenge_next) {
+    if (done) return MLH_OK;
     const FriLayer cur = p->layers.back();
     const uint32_t log_n = cur.log_n;
+    if ((1ull << log_n) <= (1ull << MLH_LOG_BLOWUP)) return MLH_OK;
     const uint64_t half_n = 1ull << (log_n - 1);
     void* vals;
     MLH_TRY(pool_alloc(ctx, half_n * sizeof(fe), &vals));
     if (half_n == (1ull << MLH_LOG_BLOWUP)) {  // fri/mod.rs:116-126
       HIP_TRY(ctx, launch_fri_fold(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), fe{},
-                                   tlo, thi, k, 1ull << log_code, ctx->stream, ShardMap(),
-                                   rbuf + k));
-      HIP_TRY(ctx, launch_fri_last(reinterpret_cast<const fe*>(vals), dt,
-                                   reinterpret_cast<uint32_t*>(sb + off_flag),
-                                   reinterpret_cast<fe*>(sb + off_last), ctx->stream));
+                                   tlo, thi, k, 1ull << p->log_code, ctx->stream, ShardMap(), rp));
+      HIP_TRY(ctx, launch_fri_last(reinterpret_cast<const fe*>(vals), dt(),
+                                   reinterpret_cast<uint32_t*>(sb() + off_flag),
+                                   reinterpret_cast<fe*>(sb() + off_last), ctx->stream));
       pool_free(ctx, vals);
       done = true;
-      break;
+      return MLH_OK;
     }
     FriLayer nx;
     nx.log_n = log_n - 1;
@@ -743,30 +756,58 @@ static mlh_status fri_fold_device(mlh_ctx* ctx, const void* dev_code, uint32_t l
     nx.tree = reinterpret_cast<uint8_t*>(tree);
     p->layers.push_back(nx);
     HIP_TRY(ctx, launch_fri_fold_leaves(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
-                                        nx.tree, fe{}, tlo, thi, k, 1ull << log_code, ctx->stream,
-                                        ShardMap(), rbuf + k));
+                                        nx.tree, fe{}, tlo, thi, k, 1ull << p->log_code,
+                                        ctx->stream, ShardMap(), rp));
     HIP_TRY(ctx, launch_merkle_levels(nx.tree, L, ctx->stream));
-    HIP_TRY(ctx, launch_transcript_absorb(dt, nx.tree + (2 * L - 2) * 32, 32, rbuf + k + 1,
-                                          ctx->stream));
+    const uint32_t t = (uint32_t)p->layers.size() - 1;
+    HIP_TRY(ctx, launch_transcript_absorb(dt(), nx.tree + (2 * L - 2) * 32, 32,
+                                          challenge_next ? r(k + 1) : nullptr, ctx->stream,
+                                          root(t)));
+    return MLH_OK;
   }
-  if (!done) return fail(ctx, MLH_ERR_INVALID, "fold produced no last element");
-  // one sync: roots, last element, RS flag
-  const size_t nt = p->layers.size();
-  for (size_t t = 0; t < nt; ++t) {
-    const uint64_t L = 1ull << (p->layers[t].log_n - 1);
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 32 * t, p->layers[t].tree + (2 * L - 2) * 32, 32,
-                                hipMemcpyDeviceToHost, ctx->stream));
+
+  // one sync: last element, RS flag, roots (+ polys_bytes of sumcheck polys)
+  mlh_status finish(size_t polys_bytes) {
+    if (!done) return fail(ctx, MLH_ERR_INVALID, "fold produced no last element");
+    const size_t nt = p->layers.size();
+    const size_t bytes = off_polys - off_last + polys_bytes;
+    if (bytes > 3072) return fail(ctx, MLH_ERR_INVALID, "proof staging too large");
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, sb() + off_last, bytes, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint8_t* h = ctx->pinned;
+    for (size_t t = 0; t < nt; ++t)
+      memcpy(p->layers[t].root, h + (off_roots - off_last) + 32 * t, 32);
+    uint32_t flag;
+    memcpy(&flag, h + (off_flag - off_last), 4);
+    if (flag) return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
+    memcpy(p->last, h, 16);
+    p->has_last = true;
+    return MLH_OK;
   }
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 32 * nt, sb + off_last, 32, hipMemcpyDeviceToHost,
-                              ctx->stream));
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  for (size_t t = 0; t < nt; ++t) memcpy(p->layers[t].root, ctx->pinned + 32 * t, 32);
-  uint32_t flag;
-  memcpy(&flag, ctx->pinned + 32 * nt + 16, 4);
-  if (flag) return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
-  memcpy(p->last, ctx->pinned + 32 * nt, 16);
-  p->has_last = true;
-  for (size_t t = 0; t < nt; ++t) mlh_transcript_absorb(tr, p->layers[t].root, 32);
+  const uint8_t* host_polys() const { return ctx->pinned + (off_polys - off_last); }
+};
+
+// FriProverData::fold (fri/mod.rs:136-145) with the transcript on the device:
+// every round's challenge is derived on the GPU from the root just written,
+// so the whole commit phase is one stream of kernels with a single sync at
+// the end; the host transcript then replays the same absorbs (root_0,
+// root_1, ..., last element) and ends in the identical state.
+static mlh_status fri_fold_device(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                                  mlh_transcript* tr, mlh_fri_prover** out) {
+  if (!ctx || !dev_code || !tr || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_code < 2 || log_code > 40)
+    return fail(ctx, log_code < 2 ? MLH_ERR_INVALID : MLH_ERR_NOT_POW2,
+                "fold needs 4 <= code length <= 2^40");
+  std::unique_ptr<mlh_fri_prover> p(new mlh_fri_prover());
+  p->ctx = ctx;
+  p->log_code = log_code;
+  FriDevLoop lp(ctx, p.get());
+  MLH_TRY(lp.init(dev_code, log_code, tr, true));
+  const uint32_t steps = log_code - MLH_LOG_BLOWUP;
+  for (uint32_t k = 0; k < steps; ++k) MLH_TRY(lp.step(k, lp.r(k), true));
+  MLH_TRY(lp.finish(0));
+  for (size_t t = 0; t < p->layers.size(); ++t) mlh_transcript_absorb(tr, p->layers[t].root, 32);
   mlh_transcript_absorb(tr, p->last, 16);
   *out = p.release();
   return MLH_OK;
@@ -1139,27 +1180,6 @@ mlh_status mlh_sumcheck_fold_and_sums(mlh_ctx* ctx, void* dev_matrix, void* dev_
 
 }  // extern "C"
 
-// One sumcheck round on the host given the device sums: interpolation on
-// x = 0,1,2 (polynomials.rs:51-87, closed form), absorb c1, c2, challenge,
-// previous_sum = p(r)  (sumcheck.rs:188-199).
-static void sumcheck_round_host(const uint8_t sums[32], u128* prev, mlh_transcript* tr,
-                                uint8_t poly_out[32], u128* r_out) {
-  const u128 s1 = h_load(sums), s2 = h_load(sums + 16);
-  const u128 e0 = h_sub(*prev, s1);
-  const u128 inv2 = h_inv(2);
-  const u128 c2 = h_mul(h_add(h_sub(s2, h_add(s1, s1)), e0), inv2);
-  const u128 c1 = h_sub(h_sub(s1, e0), c2);
-  h_store(poly_out, c1);
-  h_store(poly_out + 16, c2);
-  mlh_transcript_absorb(tr, poly_out, 16);
-  mlh_transcript_absorb(tr, poly_out + 16, 16);
-  uint8_t rb[16];
-  mlh_transcript_next_challenge(tr, rb);
-  const u128 r = h_load(rb);
-  *prev = h_add(e0, h_mul(r, h_add(c1, h_mul(c2, r))));
-  *r_out = r;
-}
-
 extern "C" {
 
 mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, uint32_t log_height,
@@ -1167,25 +1187,38 @@ mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, u
                               uint8_t* rs_out) {
   if (!ctx || !dev_matrix || !dev_delta || !sum || !tr || log_height < 1 || log_height > 40)
     return fail(ctx, MLH_ERR_INVALID, "bad argument");
-  u128 prev = h_load(sum);
-  uint8_t sums[32];
-  MLH_TRY(mlh_sumcheck_partial_sums(ctx, dev_matrix, dev_delta, log_height, sums));
-  for (uint32_t k = 0; k < log_height; ++k) {
-    uint8_t poly[32];
-    u128 r;
-    sumcheck_round_host(sums, &prev, tr, poly, &r);
-    if (polys_out) memcpy(polys_out + 32 * k, poly, 32);
-    uint8_t rb[16];
-    h_store(rb, r);
-    if (rs_out) memcpy(rs_out + 16 * k, rb, 16);
-    const uint32_t lh = log_height - k;
-    if (lh >= 2) {
-      MLH_TRY(mlh_sumcheck_fold_and_sums(ctx, dev_matrix, dev_delta, lh, rb, sums));
-    } else {
-      MLH_TRY(mlh_sumcheck_fold(ctx, dev_matrix, dev_delta, lh, rb));
-    }
+  // transcript on the device (one sync): [DevSha | prev | polys 32 x L | rs 16 x L]
+  const uint32_t L = log_height;
+  PoolBuf sc(ctx);
+  MLH_TRY(sc.alloc(128 + 16 + 48ull * L));
+  uint8_t* sb = sc.as<uint8_t>();
+  DevSha* dt = reinterpret_cast<DevSha*>(sb);
+  fe* prev = reinterpret_cast<fe*>(sb + 128);
+  fe* polys = reinterpret_cast<fe*>(sb + 144);
+  fe* rs = reinterpret_cast<fe*>(sb + 144 + 32ull * L);
+  memcpy(ctx->pinned, &tr->sha, sizeof(DevSha));
+  memcpy(ctx->pinned + 128, sum, 16);
+  HIP_TRY(ctx, hipMemcpyAsync(sb, ctx->pinned, 144, hipMemcpyHostToDevice, ctx->stream));
+  fe* m = reinterpret_cast<fe*>(dev_matrix);
+  fe* d = reinterpret_cast<fe*>(dev_delta);
+  HIP_TRY(ctx, launch_sums(m, d, 1ull << (L - 1), ctx->partials, ctx->small, ctx->stream));
+  for (uint32_t k = 0; k < L; ++k) {
+    HIP_TRY(ctx, launch_sumcheck_round(ctx->small, prev, dt, polys + 2 * k, rs + k, ctx->stream));
+    const uint64_t S = 1ull << (L - k);
+    if (S >= 4)
+      HIP_TRY(ctx, launch_fold_sums(m, d, S, fe{}, ctx->partials, ctx->small, ctx->stream, rs + k));
+    else
+      HIP_TRY(ctx, launch_fold(m, d, S, fe{}, ctx->stream, rs + k));
   }
+  std::vector<uint8_t> host(48ull * L);
+  HIP_TRY(ctx, hipMemcpyAsync(host.data(), polys, 48ull * L, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (uint32_t k = 0; k < L; ++k) {  // host transcript replay (sumcheck.rs:188-199)
+    mlh_transcript_absorb(tr, host.data() + 32 * k, 16);
+    mlh_transcript_absorb(tr, host.data() + 32 * k + 16, 16);
+  }
+  if (polys_out) memcpy(polys_out, host.data(), 32ull * L);
+  if (rs_out) memcpy(rs_out, host.data() + 32ull * L, 16ull * L);
   return MLH_OK;
 }
 
@@ -1214,33 +1247,49 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   MLH_TRY(mlh_mle_to_coefficient(ctx, coeffs.p, n_vars));
   MLH_TRY(mlh_bit_reverse_permutation(ctx, coeffs.p, brev.p, n_vars));
   MLH_TRY(mlh_reed_solomon(ctx, brev.p, n_vars, genb, code.p));
-  // PCSProverData::init (:28-42): FRI init + sumcheck tables
-  mlh_fri_prover* fp = nullptr;
-  MLH_TRY(mlh_fri_prover_init(ctx, code.p, log_domain, tr, &fp));
-  std::unique_ptr<mlh_fri_prover, void (*)(mlh_fri_prover*)> guard(fp, mlh_fri_prover_destroy);
+  // PCSProverData::init (:28-42) + fold loop (:57-75), transcript on the
+  // device: per round the sumcheck round kernel absorbs (c1, c2) and derives
+  // r, which the sumcheck fold and the FRI fold_step read from HBM.
+  std::unique_ptr<mlh_fri_prover> fp(new mlh_fri_prover());
+  fp->ctx = ctx;
+  fp->log_code = log_domain;
+  FriDevLoop lp(ctx, fp.get());
+  MLH_TRY(lp.init(code.p, log_domain, tr, false));
   HIP_TRY(ctx, hipMemcpyAsync(matrix.p, dev_evals, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
   MLH_TRY(mlh_eq_table(ctx, host_inputs, n_vars, delta.p));
-  // PCSProverData::fold loop (:57-75)
-  u128 prev = h_load(output);
-  uint8_t sums[32];
-  MLH_TRY(mlh_sumcheck_partial_sums(ctx, matrix.p, delta.p, n_vars, sums));
+  memcpy(ctx->pinned + 3072, output, 16);
+  HIP_TRY(ctx, hipMemcpyAsync(lp.prev(), ctx->pinned + 3072, 16, hipMemcpyHostToDevice,
+                              ctx->stream));
+  fe* sums = ctx->small;
+  HIP_TRY(ctx, launch_sums(matrix.as<fe>(), delta.as<fe>(), n / 2, ctx->partials, sums,
+                           ctx->stream));
   for (uint32_t k = 0; k < n_vars; ++k) {
-    uint8_t poly[32];
-    u128 r;
-    sumcheck_round_host(sums, &prev, tr, poly, &r);
-    if (proof->sumcheck_polys) memcpy(proof->sumcheck_polys + 32 * k, poly, 32);
-    uint8_t rb[16];
-    h_store(rb, r);
-    const uint32_t lh = n_vars - k;
-    if (lh >= 2) {
-      MLH_TRY(mlh_sumcheck_fold_and_sums(ctx, matrix.p, delta.p, lh, rb, sums));
+    HIP_TRY(ctx, launch_sumcheck_round(sums, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
+                                       ctx->stream));
+    const uint64_t S = 1ull << (n_vars - k);
+    if (S >= 4) {
+      HIP_TRY(ctx, launch_fold_sums(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->partials, sums,
+                                    ctx->stream, lp.r(k)));
     } else {
-      MLH_TRY(mlh_sumcheck_fold(ctx, matrix.p, delta.p, lh, rb));
+      HIP_TRY(ctx, launch_fold(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->stream, lp.r(k)));
     }
-    MLH_TRY(mlh_fri_prover_fold_step(ctx, fp, k, rb, tr));
+    MLH_TRY(lp.step(k, lp.r(k), false));
   }
-  if (!fp->has_last) return fail(ctx, MLH_ERR_INVALID, "no last element");
-  MLH_TRY(fri_queries(ctx, fp, tr, &proof->fri));
+  MLH_TRY(lp.finish(32ull * n_vars));
+  // host transcript replay: root_0, then per round (c1, c2), root_{k+1} / last
+  const uint8_t* polys = lp.host_polys();
+  if (proof->sumcheck_polys) memcpy(proof->sumcheck_polys, polys, 32ull * n_vars);
+  mlh_transcript_absorb(tr, fp->layers[0].root, 32);
+  for (uint32_t k = 0; k < n_vars; ++k) {
+    mlh_transcript_absorb(tr, polys + 32 * k, 16);
+    mlh_transcript_absorb(tr, polys + 32 * k + 16, 16);
+    if (k + 1 < fp->layers.size())
+      mlh_transcript_absorb(tr, fp->layers[k + 1].root, 32);
+    else
+      mlh_transcript_absorb(tr, fp->last, 16);
+  }
+  mlh_fri_prover* fpp = fp.get();
+  MLH_TRY(fri_queries(ctx, fpp, tr, &proof->fri));
   return MLH_OK;
 }
 

@@ -94,27 +94,35 @@ hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t
 // ---- device transcript steps (transcript_dev.hpp) ---------------------------
 namespace mlh {
 
-__global__ void transcript_absorb_kernel(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out) {
+__global__ void transcript_absorb_kernel(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out,
+                                         uint8_t* copy_out) {
+  // the state lives in LDS while a single lane updates it (the byte buffer is
+  // indexed dynamically; in VGPRs it would spill to scratch)
+  __shared__ DevSha s;
   if (threadIdx.x != 0) return;
-  DevSha s = *t;
+  s = *t;
   dsha_update(s, src, n);
   *t = s;
+  if (copy_out)
+    for (uint32_t i = 0; i < n; ++i) copy_out[i] = src[i];
   if (r_out) fe_store(r_out, dsha_challenge(s));
 }
 
 hipError_t launch_transcript_absorb(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out,
-                                    hipStream_t st) {
-  hipLaunchKernelGGL(transcript_absorb_kernel, dim3(1), dim3(64), 0, st, t, src, n, r_out);
+                                    hipStream_t st, uint8_t* copy_out) {
+  hipLaunchKernelGGL(transcript_absorb_kernel, dim3(1), dim3(64), 0, st, t, src, n, r_out,
+                     copy_out);
   return hipGetLastError();
 }
 
 __global__ void fri_last_kernel(const fe* vals, DevSha* t, uint32_t* flag, fe* last_out) {
+  __shared__ DevSha s;
   if (threadIdx.x != 0) return;
   const fe a = fe_load(vals), b = fe_load(vals + 1);
   *flag = fe_eq(a, b) ? 0u : 1u;
   fe_store(last_out, a);
-  DevSha s = *t;
-  dsha_update(s, reinterpret_cast<const uint8_t*>(last_out), 16);
+  s = *t;
+  dsha_update(s, reinterpret_cast<const uint8_t*>(&a), 16);
   *t = s;
 }
 

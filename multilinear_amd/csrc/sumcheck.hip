@@ -22,6 +22,7 @@
 // round moves 2*S*16 B in and S*16 B out (the survey's 48 S bytes).
 #include "field.hpp"
 #include "sumcheck.hpp"
+#include "transcript_dev.hpp"
 
 namespace mlh {
 
@@ -83,7 +84,8 @@ __device__ __forceinline__ fe lerp(const fe& lo, const fe& hi, const fe& r) {
 // round's sums over the folded tables (h' = S/4).
 __global__ void __launch_bounds__(kRedThreads)
 fold_sums_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r,
-                 fe* __restrict__ partials) {
+                 fe* __restrict__ partials, const fe* __restrict__ rp) {
+  if (rp) r = fe_load(rp);
   const uint64_t h = S / 2, q = S / 4;
   fe s1 = fe_zero(), s2 = fe_zero();
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -109,7 +111,9 @@ fold_sums_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r,
 }
 
 __global__ void __launch_bounds__(256)
-fold_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r) {
+fold_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r,
+            const fe* __restrict__ rp) {
+  if (rp) r = fe_load(rp);
   const uint64_t h = S / 2;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= h) return;
@@ -235,16 +239,18 @@ hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* o
 }
 
 hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* out,
-                            hipStream_t st) {
+                            hipStream_t st, const fe* r_dev) {
   const unsigned nb = red_blocks(S / 4);
-  hipLaunchKernelGGL(fold_sums_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, d, S, r, partials);
+  hipLaunchKernelGGL(fold_sums_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, d, S, r, partials,
+                     r_dev);
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, out);
   return hipGetLastError();
 }
 
-hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st) {
+hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe* r_dev) {
   const uint64_t h = S / 2;
-  hipLaunchKernelGGL(fold_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, st, m, d, S, r);
+  hipLaunchKernelGGL(fold_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, st, m, d, S, r,
+                     r_dev);
   return hipGetLastError();
 }
 
@@ -298,6 +304,41 @@ hipError_t launch_bitrev(const fe* in, fe* out, uint32_t log_n, hipStream_t st) 
   const uint64_t N = 1ull << log_n;
   hipLaunchKernelGGL(bitrev_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, in, out,
                      log_n);
+  return hipGetLastError();
+}
+
+}  // namespace mlh
+
+// ---- one sumcheck round with the transcript on the device -------------------
+namespace mlh {
+
+// sums = (s1, s2) = p(1), p(2); prev = claimed sum = p(0) + p(1).  Closed-form
+// interpolation on x = 0,1,2 (polynomials.rs:51-87): e0 = prev - s1,
+// c2 = (s2 - 2 s1 + e0) / 2, c1 = s1 - e0 - c2; absorb LE16(c1), LE16(c2)
+// (sumcheck.rs:188-199), r = next_challenge(), prev = e0 + r (c1 + c2 r).
+__global__ void sumcheck_round_kernel(const fe* sums, fe* prev, DevSha* t, fe* poly_out,
+                                      fe* r_out) {
+  __shared__ DevSha s;
+  if (threadIdx.x != 0) return;
+  const fe s1 = fe_load(sums), s2 = fe_load(sums + 1), p = fe_load(prev);
+  const fe e0 = fe_sub(p, s1);
+  const fe c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
+  const fe c1 = fe_sub(fe_sub(s1, e0), c2);
+  fe_store(poly_out, c1);
+  fe_store(poly_out + 1, c2);
+  s = *t;
+  dsha_update(s, reinterpret_cast<const uint8_t*>(&c1), 16);
+  dsha_update(s, reinterpret_cast<const uint8_t*>(&c2), 16);
+  *t = s;
+  const fe r = dsha_challenge(s);
+  fe_store(r_out, r);
+  fe_store(prev, fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r)))));
+}
+
+hipError_t launch_sumcheck_round(const fe* sums, fe* prev, DevSha* t, fe* poly_out, fe* r_out,
+                                 hipStream_t st) {
+  hipLaunchKernelGGL(sumcheck_round_kernel, dim3(1), dim3(64), 0, st, sums, prev, t, poly_out,
+                     r_out);
   return hipGetLastError();
 }
 

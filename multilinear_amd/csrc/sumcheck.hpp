@@ -14,8 +14,12 @@ hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* o
                        hipStream_t st);
 // fold size-S tables with r, then sums of the folded (size S/2) tables.
 hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* out,
-                            hipStream_t st);
-hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st);
+                            hipStream_t st, const fe* r_dev = nullptr);
+hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe* r_dev = nullptr);
+struct DevSha;
+// one sumcheck round (interpolate, absorb, challenge, new claim) on the device
+hipError_t launch_sumcheck_round(const fe* sums, fe* prev, DevSha* t, fe* poly_out, fe* r_out,
+                                 hipStream_t st);
 hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
                       hipStream_t st);
 hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st);

@@ -40,9 +40,11 @@ __device__ inline void dsha_update(DevSha& s, const uint8_t* p, uint32_t n) {
   }
 }
 
-// digest of a clone (the state itself is unchanged)
+// digest of a clone (the state itself is unchanged); the clone is padded in
+// place in a word buffer (at most two compressions)
 __device__ inline void dsha_digest(const DevSha& s0, uint8_t out[32]) {
-  DevSha c = s0;
+  __shared__ DevSha c;
+  c = s0;
   const uint64_t bits = c.len * 8;
   const uint8_t one = 0x80, z = 0;
   dsha_update(c, &one, 1);
@@ -69,9 +71,10 @@ __device__ inline fe dsha_challenge(const DevSha& s) {
   return canon_with_carry(v, 0u);
 }
 
-// absorb n bytes from device memory, then (if r_out) write next_challenge()
+// absorb n bytes from device memory, then (if r_out) write next_challenge();
+// copy_out (optional) receives a copy of the absorbed bytes
 hipError_t launch_transcript_absorb(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out,
-                                    hipStream_t st);
+                                    hipStream_t st, uint8_t* copy_out = nullptr);
 // final FRI layer (2 values): flag = (v0 != v1) ("not an RS code"),
 // absorb LE16(v0), copy v0 to last_out
 hipError_t launch_fri_last(const fe* vals, DevSha* t, uint32_t* flag, fe* last_out,
