@@ -86,8 +86,10 @@ def load_pmc(kernel, log_n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--spinup-s", type=float, default=0.3,
+                    help="untimed setup: run the step this long first so clocks settle")
     ap.add_argument("--log-n", type=int, default=24)
     ap.add_argument("--extra-reps", type=int, default=3, help="reps of the secondary timings")
     ap.add_argument("--no-cpu", action="store_true")
@@ -140,6 +142,21 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    # setup (not a step): tables, allocator, clock ramp.  The iteration count
+    # is agreed over ranks so the sharded step's collectives stay matched.
+    ntt_once()
+    barrier()
+    t_one = time.perf_counter()
+    ntt_once()
+    torch.cuda.synchronize()
+    iters = int(args.spinup_s / max(time.perf_counter() - t_one, 1e-5)) + 1
+    if dist is not None:
+        t = torch.tensor([iters], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        iters = int(t.item())
+    for _ in range(min(iters, 5000)):
+        ntt_once()
+    barrier()
     for _ in range(args.warmup):
         ntt_once()
     barrier()
