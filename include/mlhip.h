@@ -76,6 +76,9 @@ mlh_status mlh_field_add(mlh_ctx* ctx, const void* dev_a, const void* dev_b, voi
 mlh_status mlh_field_sub(mlh_ctx* ctx, const void* dev_a, const void* dev_b, void* dev_out, uint64_t n);
 mlh_status mlh_field_mul(mlh_ctx* ctx, const void* dev_a, const void* dev_b, void* dev_out, uint64_t n);
 mlh_status mlh_field_neg(mlh_ctx* ctx, const void* dev_a, void* dev_out, uint64_t n);
+/* out[i] = a[i] * c (scalar Mul, field.rs:98-106); c canonical LE16. */
+mlh_status mlh_field_scale(mlh_ctx* ctx, const void* dev_a, const uint8_t c[16], void* dev_out,
+                           uint64_t n);
 
 /* ---- NTT (src/ntt/mod.rs) ------------------------------------------------ */
 /* Polynomial::ntt (ntt/mod.rs:69-110): evals[i] = sum_j coeffs[j] gen^(ij),

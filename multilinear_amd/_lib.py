@@ -74,6 +74,7 @@ SIGNATURES = {
     "mlh_field_sub": (_I, [_P, _P, _P, _P, _U64]),
     "mlh_field_mul": (_I, [_P, _P, _P, _P, _U64]),
     "mlh_field_neg": (_I, [_P, _P, _P, _U64]),
+    "mlh_field_scale": (_I, [_P, _P, _P, _P, _U64]),
     "mlh_ntt": (_I, [_P, _P, _P, _U32, _P]),
     "mlh_intt": (_I, [_P, _P, _P, _U32, _P]),
     "mlh_bit_reverse_permutation": (_I, [_P, _P, _P, _U32]),

@@ -465,6 +465,14 @@ mlh_status mlh_field_mul(mlh_ctx* ctx, const void* a, const void* b, void* out, 
 mlh_status mlh_field_neg(mlh_ctx* ctx, const void* a, void* out, uint64_t n) {
   return vec_op(ctx, 3, a, nullptr, out, n);
 }
+mlh_status mlh_field_scale(mlh_ctx* ctx, const void* a, const uint8_t c[16], void* out,
+                           uint64_t n) {
+  if (!ctx || !a || !out || !c) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (h_load(c) >= kModulus) return fail(ctx, MLH_ERR_INVALID, "scalar not canonical");
+  HIP_TRY(ctx, launch_vec_op(4, reinterpret_cast<const fe*>(a), nullptr, reinterpret_cast<fe*>(out),
+                             n, ctx->stream, to_fe(h_load(c))));
+  return MLH_OK;
+}
 
 mlh_status mlh_bit_reverse_permutation(mlh_ctx* ctx, const void* dev_in, void* dev_out,
                                        uint32_t log_n) {

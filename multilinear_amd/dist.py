@@ -199,6 +199,38 @@ class HipOps:
     def to_host(self, values):
         return values.cpu().contiguous().numpy().view(np.uint32).reshape(-1, 4)
 
+    # -- sumcheck (tables folded in place) --
+    def eq_table(self, points):
+        from .polynomials import eq_table
+
+        return eq_table(points, self.device)
+
+    def scale(self, x, c):
+        ctx = self._ctx()
+        out = self.empty(x.shape[0])
+        check(lib().mlh_field_scale(ctx, ptr(x), fe_bytes(c), ptr(out), x.shape[0]), ctx)
+        return out
+
+    def _pair(self, raw):
+        b = bytes(raw)
+        return int.from_bytes(b[:16], "little"), int.from_bytes(b[16:], "little")
+
+    def sc_sums(self, m, d):
+        ctx = self._ctx()
+        out = (ctypes.c_uint8 * 32)()
+        check(lib().mlh_sumcheck_partial_sums(ctx, ptr(m), ptr(d), _log2(m.shape[0]), out), ctx)
+        return self._pair(out)
+
+    def sc_fold_and_sums(self, m, d, log_h, r):
+        ctx = self._ctx()
+        out = (ctypes.c_uint8 * 32)()
+        check(lib().mlh_sumcheck_fold_and_sums(ctx, ptr(m), ptr(d), log_h, fe_bytes(r), out), ctx)
+        return self._pair(out)
+
+    def sc_fold(self, m, d, log_h, r):
+        ctx = self._ctx()
+        check(lib().mlh_sumcheck_fold(ctx, ptr(m), ptr(d), log_h, fe_bytes(r)), ctx)
+
     def sync(self):
         import torch
 
@@ -447,3 +479,90 @@ def _to_natural(values, log_n, log_p, log_s, tp, ops):
     S = 1 << log_s
     P = 1 << log_p
     return g.reshape(P, -1, S, 4).transpose(0, 1).reshape(-1, 4).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# sharded sumcheck ("shard by low index bits")
+# ---------------------------------------------------------------------------
+
+def eq_table(points, tp, ops):
+    """delta of build_tables_for_pcs (sumcheck.rs:128-145) in the cyclic
+    layout: rank r holds delta[l P + r] = eq(points[:n-p], l) * c_r, where
+    c_r = prod_{b<p} (bit_b(r) ? points[n-1-b] : 1 - points[n-1-b]) -- the low
+    index bits pair with the LAST points (big-endian order)."""
+    P, rank = tp.world, tp.rank
+    p = _log2(P)
+    n = len(points)
+    if n < p:
+        raise ValueError("fewer variables than log2(world)")
+    c = 1
+    for b in range(p):
+        pt = points[n - 1 - b]
+        c = c * (pt if (rank >> b) & 1 else (1 - pt) % M) % M
+    local = ops.eq_table(points[:n - p]) if n > p else None
+    if local is None:
+        local = ops.eq_table([])
+    return ops.scale(local, c) if c != 1 else local
+
+
+def _fold_pairs(parts):
+    s1 = s2 = 0
+    for raw in parts:
+        s1 = (s1 + int.from_bytes(raw[:16], "little")) % M
+        s2 = (s2 + int.from_bytes(raw[16:], "little")) % M
+    return s1, s2
+
+
+def _combine(sums, tp):
+    if tp.world == 1:
+        return sums
+    raw = sums[0].to_bytes(16, "little") + sums[1].to_bytes(16, "little")
+    return _fold_pairs(tp.gather_bytes(raw))
+
+
+def _round(s1, s2, prev, transcript):
+    """compute_sumcheck_polynomial (sumcheck.rs:174-202): p(0) = prev - p(1),
+    closed-form interpolation on x = 0, 1, 2, absorb c1, c2, r, p(r)."""
+    e0 = (prev - s1) % M
+    c2 = (s2 - 2 * s1 + e0) * pow(2, M - 2, M) % M
+    c1 = (s1 - e0 - c2) % M
+    transcript.absorb(c1.to_bytes(16, "little"))
+    transcript.absorb(c2.to_bytes(16, "little"))
+    r = transcript.next_challenge()
+    return c1, c2, r, (e0 + r * (c1 + c2 * r)) % M
+
+
+def sumcheck_prove(m, d, n, total_sum, transcript, tp, ops):
+    """SumcheckTables::compute_sumcheck_polynomials (sumcheck.rs:77-102) for
+    the PCS composition x[0], tables of 2^n entries in the cyclic layout
+    (``m``, ``d`` local, folded in place).  The MSB-first fold pairs (i, i+h)
+    share their low bits, so they stay on one rank while the local table has
+    >= 2 entries; round sums are all-gathered (2 x 16 B per rank) and added
+    mod M; the last p rounds run replicated on the gathered P-entry tables.
+    Returns ([(c1, c2)], [r]) -- identical to the single-GPU prover."""
+    P = tp.world
+    p = _log2(P)
+    sharded = P > 1
+    log_local = n - p
+    if sharded and log_local == 0:
+        m, d, sharded, log_local = tp.all_gather(m), tp.all_gather(d), False, n
+    s1, s2 = _combine(ops.sc_sums(m, d), tp) if sharded else ops.sc_sums(m, d)
+    prev = total_sum
+    polys, rs = [], []
+    for k in range(n):
+        c1, c2, r, prev = _round(s1, s2, prev, transcript)
+        polys.append((c1, c2))
+        rs.append(r)
+        if k + 1 == n:
+            ops.sc_fold(m, d, log_local, r)
+            break
+        if log_local >= 2:
+            sums = ops.sc_fold_and_sums(m, d, log_local, r)
+            log_local -= 1
+            s1, s2 = _combine(sums, tp) if sharded else sums
+        else:  # sharded, local 2 -> 1: gather the P-entry tables, go replicated
+            ops.sc_fold(m, d, log_local, r)
+            m, d = tp.all_gather(m[:1]), tp.all_gather(d[:1])
+            sharded, log_local = False, p
+            s1, s2 = ops.sc_sums(m, d)
+    return polys, rs

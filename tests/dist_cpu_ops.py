@@ -101,5 +101,36 @@ class CpuOps(D.HipOps):
     def to_host(self, values):
         return _limbs(values)
 
+    # -- sumcheck: oracle formulas, tables mutated in place ---------------------
+    def eq_table(self, points):
+        from oracle import sumcheck as OS
+
+        return _tensor(OS.eq_table(points))
+
+    def scale(self, x, c):
+        return _tensor([v * c % F.M for v in _ints(x)])
+
+    @staticmethod
+    def _sums(m, d):
+        h = len(m) // 2
+        s1 = sum(m[i + h] * d[i + h] for i in range(h)) % F.M
+        s2 = sum((2 * m[i + h] - m[i]) * (2 * d[i + h] - d[i]) for i in range(h)) % F.M
+        return s1, s2
+
+    def sc_sums(self, m, d):
+        return self._sums(_ints(m), _ints(d))
+
+    def sc_fold(self, m, d, log_h, r):
+        for t in (m, d):
+            v = _ints(t)
+            h = 1 << (log_h - 1)
+            folded = [(v[i] + r * (v[i + h] - v[i])) % F.M for i in range(h)]
+            t[:h] = _tensor(folded)
+
+    def sc_fold_and_sums(self, m, d, log_h, r):
+        self.sc_fold(m, d, log_h, r)
+        h = 1 << (log_h - 1)
+        return self._sums(_ints(m[:h]), _ints(d[:h]))
+
     def sync(self):
         pass

@@ -118,3 +118,71 @@ def test_sharded_rs_ntt_fri_match_single(world, log_c, gather_log):
         for value, path in q:
             raw += value + b"".join(s for s, _ in path)
     assert qraw == raw
+
+
+def _sc_worker(rank, world, port, n, q):
+    import torch
+    import torch.distributed as tdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from multilinear_amd import dist as D
+        from multilinear_amd.transcript import Transcript
+        from tests.dist_cpu_ops import CpuOps
+
+        tp, ops = D.Transport(), CpuOps()
+        rng = np.random.default_rng(3)
+        ev = rng.integers(0, 2**32, size=(1 << n, 4), dtype=np.uint64).astype(np.uint32)
+        ev[:, 3] = np.minimum(ev[:, 3], 0xFFFFFFFE)
+        pts = [int(x) for x in rng.integers(0, 2**62, size=n)]
+        m = torch.from_numpy(D.shard_cyclic(ev, world, rank).view(np.int32).copy())
+        d = D.eq_table(pts, tp, ops)
+        tr = Transcript()
+        tr.absorb(b"sumcheck")
+        polys, rs = D.sumcheck_prove(m, d, n, 12345, tr, tp, ops)
+        q.put((rank, polys, rs, tr.random()))
+    except Exception:
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc(), None))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 6), (4, 7), (4, 2), (2, 1), (8, 5)])
+def test_sharded_sumcheck_matches_oracle(world, n):
+    """dist.eq_table + dist.sumcheck_prove vs the oracle's
+    compute_sumcheck_polynomial loop (sumcheck.rs:77-102, 174-202)."""
+    from oracle import field as F
+    from oracle import sumcheck as OS
+    from oracle.transcript import Transcript as OT
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sc_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r[2]
+    rng = np.random.default_rng(3)
+    ev = rng.integers(0, 2**32, size=(1 << n, 4), dtype=np.uint64).astype(np.uint32)
+    ev[:, 3] = np.minimum(ev[:, 3], 0xFFFFFFFE)
+    pts = [int(x) for x in rng.integers(0, 2**62, size=n)]
+    tab = OS.SumcheckTables(F.from_limbs(ev), OS.eq_table(pts))
+    tr = OT()
+    tr.absorb(b"sumcheck")
+    prev, polys, rs = 12345, [], []
+    for _ in range(n):
+        nz, r, prev = tab.compute_sumcheck_polynomial(prev, tr)
+        polys.append(tuple(nz))
+        rs.append(r)
+    for r in res:
+        assert [tuple(p) for p in r[1]] == polys, "rank %d polys" % r[0]
+        assert r[2] == rs
+        assert r[3] == tr.random()

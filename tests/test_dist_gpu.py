@@ -162,3 +162,61 @@ def test_sharded_fri_prove_multiprocess(world, log_c, gather_log):
         assert res[r]["ok"], "rank %d proof rejected" % r
         for key in ("commit", "q", "idx", "last", "lr"):
             assert res[r][key] == ref[key], "rank %d: %s differs from single-GPU proof" % (r, key)
+
+
+def _sc_worker(rank, world, port, n, q):
+    import torch.distributed as tdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import random
+
+        from multilinear_amd import polynomials as MPL
+        from multilinear_amd import sumcheck as MS
+
+        torch.cuda.set_device(0)
+        tp, ops = D.Transport(host_staged=True), D.HipOps(0)
+        ev = DV.random_limbs(1 << n, seed=21)
+        rr = random.Random(4)
+        pts = [rr.randrange(M) for _ in range(n)]
+        m = DV.to_device(D.shard_cyclic(ev, world, rank))
+        d = D.eq_table(pts, tp, ops)
+        tr = Transcript()
+        polys, rs = D.sumcheck_prove(m, d, n, 777, tr, tp, ops)
+        res = {"polys": polys, "rs": rs, "lr": tr.random()}
+        if rank == 0:
+            x = DV.to_device(ev)
+            tab = MS.SumcheckTables(x.clone(), MPL.eq_table(pts))
+            t2 = Transcript()
+            rp, rr2 = tab.compute_sumcheck_polynomials(777, t2)
+            res["ref"] = {"polys": rp, "rs": rr2, "lr": t2.random()}
+        q.put((rank, res))
+    except Exception:
+        import traceback
+
+        q.put((rank, {"error": traceback.format_exc()}))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 18), (4, 20)])
+def test_sharded_sumcheck_multiprocess(world, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sc_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=300) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+    ref = res[0].pop("ref")
+    for r in range(world):
+        assert [tuple(p) for p in res[r]["polys"]] == [tuple(p) for p in ref["polys"]]
+        assert res[r]["rs"] == ref["rs"] and res[r]["lr"] == ref["lr"]
