@@ -157,6 +157,18 @@ uint64_t mlh_fri_query_bytes(uint32_t log_code);
 /* FriProof::prove (fri/mod.rs:261-285). */
 mlh_status mlh_fri_prove(mlh_ctx* ctx, const void* dev_code, uint32_t log_code, mlh_transcript* tr,
                          mlh_fri_proof* proof);
+/* Wire format: serde + bincode 2 standard / little-endian / fixed-int encoding
+ * of FriProof<Field128> (fri/mod.rs:239-249, 367-397; field.rs:40-64) -- the
+ * bytes the reference's bincode::serde::encode_to_vec produces.  encode needs
+ * query_indices (the Direction of every path level is bit i of the index);
+ * decode fills commitments, queries, last_elem, last_random and (if non-NULL)
+ * query_indices recovered from the directions; MLH_ERR_VERIFY if a path's
+ * directions disagree with its index (the reference verifier rejects those). */
+uint64_t mlh_fri_proof_encoded_size(const mlh_fri_proof* proof);
+mlh_status mlh_fri_proof_encode(const mlh_fri_proof* proof, uint8_t* out, uint64_t cap);
+mlh_status mlh_fri_proof_decode_header(const uint8_t* in, uint64_t len, uint32_t* log_code,
+                                       uint32_t* num_queries);
+mlh_status mlh_fri_proof_decode(const uint8_t* in, uint64_t len, mlh_fri_proof* proof);
 /* FriProof::verify (fri/mod.rs:287-340), host side; MLH_ERR_VERIFY if rejected. */
 mlh_status mlh_fri_verify(const mlh_fri_proof* proof);
 

@@ -97,6 +97,10 @@ SIGNATURES = {
     "mlh_fri_query_bytes": (_U64, [_U32]),
     "mlh_fri_prove": (_I, [_P, _P, _U32, _P, ctypes.POINTER(FriProofC)]),
     "mlh_fri_verify": (_I, [ctypes.POINTER(FriProofC)]),
+    "mlh_fri_proof_encoded_size": (_U64, [ctypes.POINTER(FriProofC)]),
+    "mlh_fri_proof_encode": (_I, [ctypes.POINTER(FriProofC), _P, _U64]),
+    "mlh_fri_proof_decode_header": (_I, [_P, _U64, ctypes.POINTER(_U32), ctypes.POINTER(_U32)]),
+    "mlh_fri_proof_decode": (_I, [_P, _U64, ctypes.POINTER(FriProofC)]),
     "mlh_shard_ntt_cross": (_I, [_P, _P, _P, _U32, _U32, _U32, _P, _I]),
     "mlh_shard_fri_fold": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _U32, _U32, _U32]),
     "mlh_shard_fri_fold_commit": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _P, _U32, _U32, _U32]),

@@ -149,3 +149,25 @@ class FriProof:
     def verify(self):
         """FriProof::verify (fri/mod.rs:287-309) in libmlhip (host)."""
         return lib().mlh_fri_verify(ctypes.byref(self.c)) == 0
+
+    def to_bytes(self):
+        """bincode 2 (standard, LE, fixed-int) serde encoding, as the reference's
+        encode_to_vec (fri/mod.rs:367-392)."""
+        n = lib().mlh_fri_proof_encoded_size(ctypes.byref(self.c))
+        buf = (ctypes.c_uint8 * n)()
+        check(lib().mlh_fri_proof_encode(ctypes.byref(self.c), buf, n))
+        return bytes(buf)
+
+    @staticmethod
+    def from_bytes(data: bytes):
+        """decode_from_slice (fri/mod.rs:394-397) into a host FriProof."""
+        src = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
+        lc, nq = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().mlh_fri_proof_decode_header(src, len(data), ctypes.byref(lc), ctypes.byref(nq)))
+        if nq.value != NUM_QUERIES:
+            raise _lib.MlhError(_lib.MLH_ERR_INVALID, "expected %d queries" % NUM_QUERIES)
+        p = FriProof(lc.value)
+        p.c.log_code = lc.value
+        p.c.num_queries = nq.value
+        check(lib().mlh_fri_proof_decode(src, len(data), ctypes.byref(p.c)))
+        return p

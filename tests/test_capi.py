@@ -136,3 +136,51 @@ def test_host_pcs_verifier_accepts_oracle_proof():
     pc.sumcheck_polys = ctypes.cast(polys, ctypes.c_void_p)
     assert lib.mlh_pcs_verify(ctypes.byref(pc), n, _points(pts), fe_bytes(out), Transcript().h) == 0
     assert lib.mlh_pcs_verify(ctypes.byref(pc), n, _points(pts), fe_bytes(out + 1), Transcript().h) == 7
+
+
+def test_fri_proof_wire_format_matches_oracle_encoding():
+    """mlh_fri_proof_{encode,decode} vs oracle/wire.py (bincode 2 fixed-int
+    serde layout of FriProof<Field128>, fri/mod.rs:239-249, 367-397)."""
+    from multilinear_amd.fri import FriProof
+    from oracle import wire as OW
+
+    ln = 7
+    vals = [F.from_i64(7 * i + 3) for i in range(1 << ln)]
+    gp = F.pow_2_generator_powers(ln + 1)
+    proof = OF.FriProof.prove(OF.reed_solomon(vals, gp[1]), gp, OT.Transcript())
+    want = OW.encode_fri_proof(proof)
+    L = ln + 1
+    per_query = 8 + sum(48 + 8 + 36 * (L - 1 - t) for t in range(L - 1))
+    assert len(want) == 8 + 32 * (L - 1) + 8 + 128 * per_query + 24 + 32
+    dec = FriProof.from_bytes(want)  # indices recovered from the directions
+    assert dec.verify()
+    assert dec.commitments == proof.commitments and dec.last_elem == proof.last_elem
+    tr = OT.Transcript()
+    for c in proof.commitments:
+        tr.absorb(c)
+    tr.absorb(F.to_bytes(proof.last_elem))
+    for q in range(128):
+        i = OF.query_index(tr, 1 << L)
+        tr.absorb(i.to_bytes(8, "little"))
+        assert dec.query_indices[q] == i
+    assert dec.to_bytes() == want
+    # malformed: truncated, trailing byte, wrong field length, bad / inconsistent direction
+    with pytest.raises(_lib.MlhError):
+        FriProof.from_bytes(want[:-1])
+    with pytest.raises(_lib.MlhError):
+        FriProof.from_bytes(want + b"\0")
+    off = 8 + 32 * (L - 1) + 8 + 8  # first query's first path: value field length
+    bad = bytearray(want)
+    bad[off] = 15
+    with pytest.raises(_lib.MlhError):
+        FriProof.from_bytes(bytes(bad))
+    # direction of tree 1, level 0 (inconsistent with tree 0's index bit)
+    d_off = off + 48 + 8 + 36 * (L - 1) + 48 + 8 + 32
+    bad = bytearray(want)
+    bad[d_off] ^= 1
+    with pytest.raises(_lib.MlhError) as e:
+        FriProof.from_bytes(bytes(bad))
+    assert e.value.status == 7
+    bad[d_off] = 2
+    with pytest.raises(_lib.MlhError):
+        FriProof.from_bytes(bytes(bad))

@@ -530,3 +530,20 @@ def test_field_mul_random_bulk():
     for i in range(0, n, 997):
         assert D.limbs_to_ints(got[i:i + 1])[0] == coracle.mul(D.limbs_to_ints(x[i:i + 1])[0],
                                                                  D.limbs_to_ints(y[i:i + 1])[0])
+
+
+@pytest.mark.parametrize("log_n", [5, 9])
+def test_fri_proof_wire_bytes_match_oracle(log_n):
+    """GPU proof -> bincode bytes (mlh_fri_proof_encode) == the oracle's
+    encoding of its own proof of the same code; decode round-trips."""
+    from oracle import wire as OW
+
+    vals = [F.from_i64(7 * i + 3) for i in range(1 << log_n)]
+    gp = F.pow_2_generator_powers(log_n + 1)
+    code = OF.reed_solomon(vals, gp[1])
+    want = OW.encode_fri_proof(OF.FriProof.prove(code, gp, OT.Transcript()))
+    p = MF.FriProof.prove(dev(code), Transcript())
+    got = p.to_bytes()
+    assert got == want
+    q = MF.FriProof.from_bytes(got)
+    assert q.verify() and q.to_bytes() == got and q.query_indices == p.query_indices
