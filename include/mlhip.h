@@ -212,6 +212,45 @@ mlh_status mlh_merkle_open_pairs(mlh_ctx* ctx, const void* dev_values, uint32_t 
                                  const void* dev_tree, uint32_t levels, const uint64_t* idx,
                                  uint32_t nq, uint8_t* out);
 
+/* ---- batched FRI / batched PCS (src/fri/batched_fri.rs, batched_pcs.rs) ----
+ * m codes (or MLEs) stored back to back on the device: item j at j * size.
+ * fingerprint(r, c_0..c_{m-1}) = Horner = sum_j c_j r^(m-1-j) (batched_fri.rs:30-38). */
+typedef struct mlh_batched_fri_proof {
+  uint32_t log_code;    /* L = log2(code length)                            */
+  uint32_t num_codes;   /* m                                               */
+  uint32_t num_trees;   /* inner FRI commitments: L - 2                    */
+  uint32_t num_queries; /* MLH_NUM_QUERIES                                 */
+  uint8_t batch_commitment[32];
+  uint8_t* commitments; /* [num_trees][32]                                 */
+  uint8_t last_elem[16];
+  uint8_t last_random[32];
+  uint64_t* query_indices; /* [num_queries] (optional)                     */
+  uint8_t* queries;        /* [num_queries][mlh_batched_fri_query_bytes]   */
+} mlh_batched_fri_proof;
+/* Query record: the opened batch column (m x 32 B RS pairs, code order) and
+ * its L-1 batch-tree siblings, then the inner QueryProof: for inner tree
+ * t = 0..L-3 the pair (32 B) and its L-2-t siblings (directions = index bits). */
+uint64_t mlh_batched_fri_query_bytes(uint32_t log_code, uint32_t num_codes);
+/* BatchedFriProof::prove (batched_fri.rs:280-311). */
+mlh_status mlh_batched_fri_prove(mlh_ctx* ctx, const void* dev_codes, uint32_t num_codes,
+                                 uint32_t log_code, mlh_transcript* tr,
+                                 mlh_batched_fri_proof* proof);
+/* BatchedFriProof::verify (batched_fri.rs:313-388), host side. */
+mlh_status mlh_batched_fri_verify(const mlh_batched_fri_proof* proof);
+typedef struct mlh_batched_pcs_proof {
+  mlh_batched_fri_proof fri;
+  uint8_t* sumcheck_polys; /* [n_vars][2][16] */
+} mlh_batched_pcs_proof;
+/* BatchedPCSProof::prove (batched_pcs.rs:127-180): dev_evals = num_polys MLEs
+ * of 2^n_vars evals; claim = (inputs[n_vars], outputs[num_polys]) LE16 each. */
+mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t num_polys,
+                                 uint32_t n_vars, const uint8_t* inputs, const uint8_t* outputs,
+                                 mlh_transcript* tr, mlh_batched_pcs_proof* proof);
+/* BatchedPCSProof::verify (batched_pcs.rs:182-250), host side. */
+mlh_status mlh_batched_pcs_verify(const mlh_batched_pcs_proof* proof, uint32_t n_vars,
+                                  const uint8_t* inputs, const uint8_t* outputs,
+                                  mlh_transcript* tr);
+
 /* ---- transcript (src/transcript.rs), host side --------------------------- */
 mlh_status mlh_transcript_create(mlh_transcript** out);
 mlh_status mlh_transcript_clone(const mlh_transcript* t, mlh_transcript** out);

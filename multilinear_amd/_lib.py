@@ -49,6 +49,25 @@ class PcsProofC(ctypes.Structure):
     _fields_ = [("fri", FriProofC), ("sumcheck_polys", ctypes.c_void_p)]
 
 
+class BatchedFriProofC(ctypes.Structure):
+    _fields_ = [
+        ("log_code", ctypes.c_uint32),
+        ("num_codes", ctypes.c_uint32),
+        ("num_trees", ctypes.c_uint32),
+        ("num_queries", ctypes.c_uint32),
+        ("batch_commitment", ctypes.c_uint8 * 32),
+        ("commitments", ctypes.c_void_p),
+        ("last_elem", ctypes.c_uint8 * 16),
+        ("last_random", ctypes.c_uint8 * 32),
+        ("query_indices", ctypes.c_void_p),
+        ("queries", ctypes.c_void_p),
+    ]
+
+
+class BatchedPcsProofC(ctypes.Structure):
+    _fields_ = [("fri", BatchedFriProofC), ("sumcheck_polys", ctypes.c_void_p)]
+
+
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
 _U64 = ctypes.c_uint64
@@ -105,6 +124,12 @@ SIGNATURES = {
     "mlh_shard_fri_fold": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _U32, _U32, _U32]),
     "mlh_shard_fri_fold_commit": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _P, _U32, _U32, _U32]),
     "mlh_merkle_open_pairs": (_I, [_P, _P, _U32, _P, _U32, _P, _U32, _P]),
+    "mlh_batched_fri_query_bytes": (_U64, [_U32, _U32]),
+    "mlh_batched_fri_prove": (_I, [_P, _P, _U32, _U32, _P, ctypes.POINTER(BatchedFriProofC)]),
+    "mlh_batched_fri_verify": (_I, [ctypes.POINTER(BatchedFriProofC)]),
+    "mlh_batched_pcs_prove": (_I, [_P, _P, _U32, _U32, _P, _P, _P,
+                                   ctypes.POINTER(BatchedPcsProofC)]),
+    "mlh_batched_pcs_verify": (_I, [ctypes.POINTER(BatchedPcsProofC), _U32, _P, _P, _P]),
     "mlh_transcript_create": (_I, [ctypes.POINTER(_P)]),
     "mlh_transcript_clone": (_I, [_P, ctypes.POINTER(_P)]),
     "mlh_transcript_destroy": (None, [_P]),

@@ -23,6 +23,7 @@
 
 #include "../../include/mlhip.h"
 #include "field.hpp"
+#include "batched.hpp"
 #include "dist.hpp"
 #include "fieldops.hpp"
 #include "host_field.hpp"
@@ -689,35 +690,105 @@ mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
 static_assert(sizeof(DevSha) == sizeof(HostSha256), "transcript layouts differ");
 
 // Device-side commit loop state: [transcript | r_0..r_steps | last (16) |
-// flag (16) | roots 32 x (steps + 1) | polys 32 x steps | prev (16)].
+// flag (16) | batch root (32) | fingerprint r (16) | roots 32 x (steps + 1) |
+// polys 32 x steps | prev (16) | extra (16 x n_extra)].
 struct FriDevLoop {
   mlh_ctx* ctx;
   mlh_fri_prover* p;
   const fe *tlo = nullptr, *thi = nullptr;
   PoolBuf scratch;
-  size_t off_r = 128, off_last = 0, off_flag = 0, off_roots = 0, off_polys = 0, off_prev = 0;
+  size_t off_r = 128, off_last = 0, off_flag = 0, off_broot = 0, off_fr = 0, off_roots = 0,
+         off_polys = 0, off_prev = 0, off_extra = 0;
   bool done = false;
-  explicit FriDevLoop(mlh_ctx* c, mlh_fri_prover* pr) : ctx(c), p(pr), scratch(c) {}
+  // batched mode: the m codes ([m][N]) and the batch-layer tree
+  const fe* codes = nullptr;
+  uint32_t m = 0;
+  PoolBuf btree;
+  explicit FriDevLoop(mlh_ctx* c, mlh_fri_prover* pr) : ctx(c), p(pr), scratch(c), btree(c) {}
   uint8_t* sb() const { return scratch.as<uint8_t>(); }
   DevSha* dt() const { return reinterpret_cast<DevSha*>(sb()); }
   fe* r(uint32_t k) const { return reinterpret_cast<fe*>(sb() + off_r) + k; }
   uint8_t* root(uint32_t t) const { return sb() + off_roots + 32 * t; }
   fe* poly(uint32_t k) const { return reinterpret_cast<fe*>(sb() + off_polys) + 2 * k; }
   fe* prev() const { return reinterpret_cast<fe*>(sb() + off_prev); }
+  fe* fr() const { return reinterpret_cast<fe*>(sb() + off_fr); }
+  fe* extra() const { return reinterpret_cast<fe*>(sb() + off_extra); }
 
-  mlh_status init(const void* dev_code, uint32_t log_code, const mlh_transcript* tr,
-                  bool challenge_after_root0) {
+  mlh_status layout(uint32_t log_code, const mlh_transcript* tr, size_t n_extra = 0) {
     const uint32_t steps = log_code - MLH_LOG_BLOWUP;
     off_last = off_r + 16 * (steps + 1);
     off_flag = off_last + 16;
-    off_roots = off_flag + 16;
+    off_broot = off_flag + 16;
+    off_fr = off_broot + 32;
+    off_roots = off_fr + 16;
     off_polys = off_roots + 32 * (steps + 1);
     off_prev = off_polys + 32 * steps;
-    MLH_TRY(scratch.alloc(off_prev + 16));
+    off_extra = off_prev + 16;
+    MLH_TRY(scratch.alloc(off_extra + 16 * (n_extra ? n_extra : 1)));
     MLH_TRY(fold_tables(ctx, log_code, &tlo, &thi));
     memcpy(ctx->pinned, &tr->sha, sizeof(DevSha));
     HIP_TRY(ctx, hipMemcpyAsync(dt(), ctx->pinned, sizeof(DevSha), hipMemcpyHostToDevice,
                                 ctx->stream));
+    return MLH_OK;
+  }
+
+  // BatchedFriProverData::init (batched_fri.rs:41-98): batch layer over the
+  // m codes' RS pairs, absorb its root, fingerprint_r = next_challenge(),
+  // absorb LE16(fingerprint_r); r_0 = next_challenge() if challenge_r0.
+  mlh_status init_batched(const fe* dev_codes, uint32_t num_codes, uint32_t log_code,
+                          const mlh_transcript* tr, bool challenge_r0, size_t n_extra = 0) {
+    MLH_TRY(layout(log_code, tr, n_extra));
+    codes = dev_codes;
+    m = num_codes;
+    const uint64_t N = 1ull << log_code, L = N / 2;
+    MLH_TRY(btree.alloc(mlh_merkle_layers_bytes(L)));
+    uint8_t* bt = btree.as<uint8_t>();
+    HIP_TRY(ctx, launch_batch_pairs_leaves(codes, m, N, bt, ctx->stream));
+    HIP_TRY(ctx, launch_merkle_levels(bt, L, ctx->stream));
+    HIP_TRY(ctx, launch_transcript_absorb(dt(), bt + (2 * L - 2) * 32, 32, fr(), ctx->stream,
+                                          sb() + off_broot));
+    HIP_TRY(ctx, launch_transcript_absorb(dt(), reinterpret_cast<const uint8_t*>(fr()), 16,
+                                          challenge_r0 ? r(0) : nullptr, ctx->stream));
+    return MLH_OK;
+  }
+
+  // batched_fold_step (batched_fri.rs:100-176): fold the fingerprinted pairs
+  // with r at rp into the inner prover's first layer (or the last element).
+  mlh_status step_batched(const fe* rp, bool challenge_next) {
+    const uint32_t L = p->log_code;
+    const uint64_t N = 1ull << L, half_n = N / 2;
+    void* vals;
+    MLH_TRY(pool_alloc(ctx, half_n * sizeof(fe), &vals));
+    if (half_n == (1ull << MLH_LOG_BLOWUP)) {
+      HIP_TRY(ctx, launch_batched_fold_leaves(codes, m, N, fr(), rp, tlo, thi,
+                                              reinterpret_cast<fe*>(vals), nullptr, ctx->stream));
+      HIP_TRY(ctx, launch_fri_last(reinterpret_cast<const fe*>(vals), dt(),
+                                   reinterpret_cast<uint32_t*>(sb() + off_flag),
+                                   reinterpret_cast<fe*>(sb() + off_last), ctx->stream));
+      pool_free(ctx, vals);
+      done = true;
+      return MLH_OK;
+    }
+    FriLayer nx;
+    nx.log_n = L - 1;
+    nx.owned_values = vals;
+    nx.values = reinterpret_cast<const fe*>(vals);
+    const uint64_t leaves = half_n / 2;
+    void* tree;
+    MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(leaves), &tree));
+    nx.tree = reinterpret_cast<uint8_t*>(tree);
+    p->layers.push_back(nx);
+    HIP_TRY(ctx, launch_batched_fold_leaves(codes, m, N, fr(), rp, tlo, thi,
+                                            reinterpret_cast<fe*>(vals), nx.tree, ctx->stream));
+    HIP_TRY(ctx, launch_merkle_levels(nx.tree, leaves, ctx->stream));
+    HIP_TRY(ctx, launch_transcript_absorb(dt(), nx.tree + (2 * leaves - 2) * 32, 32,
+                                          challenge_next ? r(1) : nullptr, ctx->stream, root(0)));
+    return MLH_OK;
+  }
+
+  mlh_status init(const void* dev_code, uint32_t log_code, const mlh_transcript* tr,
+                  bool challenge_after_root0) {
+    MLH_TRY(layout(log_code, tr));
     FriLayer l0;
     l0.values = reinterpret_cast<const fe*>(dev_code);
     l0.log_n = log_code;
@@ -794,6 +865,8 @@ struct FriDevLoop {
     return MLH_OK;
   }
   const uint8_t* host_polys() const { return ctx->pinned + (off_polys - off_last); }
+  const uint8_t* host_broot() const { return ctx->pinned + (off_broot - off_last); }
+  const uint8_t* host_fr() const { return ctx->pinned + (off_fr - off_last); }
 };
 
 // FriProverData::fold (fri/mod.rs:136-145) with the transcript on the device:
@@ -864,11 +937,11 @@ struct QueryTree {
 
 __global__ void gather_queries_kernel(const QueryTree* __restrict__ trees, uint32_t ntrees,
                                       const uint64_t* __restrict__ indices, uint32_t nq,
-                                      uint64_t qbytes, uint8_t* __restrict__ out) {
+                                      uint64_t qbytes, uint64_t base, uint8_t* __restrict__ out) {
   const uint32_t q = blockIdx.x;
   if (q >= nq) return;
   // record offsets per tree
-  uint64_t off = 0;
+  uint64_t off = base;
   for (uint32_t t = 0; t < ntrees; ++t) {
     const QueryTree T = trees[t];
     const uint64_t half = 1ull << (T.log_n - 1);  // leaves
@@ -893,24 +966,34 @@ __global__ void gather_queries_kernel(const QueryTree* __restrict__ trees, uint3
   }
 }
 
-static mlh_status gather_queries(mlh_ctx* ctx, const mlh_fri_prover* p, const uint64_t* idx,
-                                 uint32_t nq, uint8_t* host_out) {
+// Launch the per-tree gathers of p's layers into device records (qbytes
+// each, this part starting at byte `base` of a record).
+static mlh_status gather_queries_dev(mlh_ctx* ctx, const mlh_fri_prover* p, const uint64_t* d_idx,
+                                     uint32_t nq, uint64_t qbytes, uint64_t base, uint8_t* d_out,
+                                     PoolBuf& dtrees) {
   const uint32_t nt = (uint32_t)p->layers.size();
-  const uint64_t qbytes = mlh_fri_query_bytes(p->log_code);
+  if (nt == 0 || nq == 0) return MLH_OK;
   std::vector<QueryTree> qt(nt);
-  for (uint32_t t = 0; t < nt; ++t) qt[t] = QueryTree{p->layers[t].values, p->layers[t].tree, p->layers[t].log_n};
-  PoolBuf dtrees(ctx), didx(ctx), dout(ctx);
+  for (uint32_t t = 0; t < nt; ++t)
+    qt[t] = QueryTree{p->layers[t].values, p->layers[t].tree, p->layers[t].log_n};
   MLH_TRY(dtrees.alloc(nt * sizeof(QueryTree)));
-  MLH_TRY(didx.alloc(nq * sizeof(uint64_t)));
-  MLH_TRY(dout.alloc(nq * qbytes));
   HIP_TRY(ctx, hipMemcpyAsync(dtrees.p, qt.data(), nt * sizeof(QueryTree), hipMemcpyHostToDevice,
                               ctx->stream));
+  hipLaunchKernelGGL(gather_queries_kernel, dim3(nq), dim3(64), 0, ctx->stream,
+                     dtrees.as<QueryTree>(), nt, d_idx, nq, qbytes, base, d_out);
+  HIP_TRY(ctx, hipGetLastError());
+  return MLH_OK;
+}
+
+static mlh_status gather_queries(mlh_ctx* ctx, const mlh_fri_prover* p, const uint64_t* idx,
+                                 uint32_t nq, uint8_t* host_out) {
+  const uint64_t qbytes = mlh_fri_query_bytes(p->log_code);
+  PoolBuf dtrees(ctx), didx(ctx), dout(ctx);
+  MLH_TRY(didx.alloc(nq * sizeof(uint64_t)));
+  MLH_TRY(dout.alloc(nq * qbytes));
   HIP_TRY(ctx, hipMemcpyAsync(didx.p, idx, nq * sizeof(uint64_t), hipMemcpyHostToDevice,
                               ctx->stream));
-  hipLaunchKernelGGL(gather_queries_kernel, dim3(nq), dim3(64), 0, ctx->stream,
-                     dtrees.as<QueryTree>(), nt, didx.as<uint64_t>(), nq, qbytes,
-                     dout.as<uint8_t>());
-  HIP_TRY(ctx, hipGetLastError());
+  MLH_TRY(gather_queries_dev(ctx, p, didx.as<uint64_t>(), nq, qbytes, 0, dout.as<uint8_t>(), dtrees));
   HIP_TRY(ctx, hipMemcpyAsync(host_out, dout.p, nq * qbytes, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   return MLH_OK;
@@ -1314,11 +1397,11 @@ static void sha_pair(const uint8_t* a, const uint8_t* b, uint8_t out[32]) {
 }
 
 // MerkleInclusionPath::verify (merkle_tree/mod.rs:216-253); directions from index bits.
-static bool verify_path(const uint8_t* value32, const uint8_t* sibs, uint32_t depth,
-                        const uint8_t root[32], uint64_t index) {
+static bool verify_path_len(const uint8_t* value, uint64_t len, const uint8_t* sibs,
+                            uint32_t depth, const uint8_t root[32], uint64_t index) {
   uint8_t h[32];
   HostSha256 s;
-  s.update(value32, 32);
+  s.update(value, len);
   s.digest(h);
   for (uint32_t l = 0; l < depth; ++l) {
     uint8_t nh[32];
@@ -1331,50 +1414,108 @@ static bool verify_path(const uint8_t* value32, const uint8_t* sibs, uint32_t de
   return memcmp(h, root, 32) == 0;
 }
 
+static bool verify_path(const uint8_t* value32, const uint8_t* sibs, uint32_t depth,
+                        const uint8_t root[32], uint64_t index) {
+  return verify_path_len(value32, 32, sibs, depth, root, index);
+}
+
+// QueryProof::verify (fri/mod.rs:184-236) over flat records: ntrees paths,
+// tree t has leaves n/2^t (depth log2(n) - t), gen of order 2n.
+static bool query_chain(const uint8_t* rec, const uint8_t* commitments, uint32_t ntrees,
+                        uint64_t n, uint64_t index, u128 gen, const u128* rs, u128 last) {
+  const u128 inv2 = h_inv(2);
+  uint64_t cur_n = n, cur_idx = index, off = 0;
+  u128 cur_gen = gen;
+  const uint32_t depth0 = 63 - __builtin_clzll(n);
+  for (uint32_t t = 0; t < ntrees; ++t) {
+    const uint32_t depth = depth0 - t;
+    const uint8_t* val = rec + off;
+    if (!verify_path(val, val + 32, depth, commitments + 32 * t, cur_idx)) return false;
+    const u128 v = h_load(val), mv = h_load(val + 16);
+    const u128 gp = h_pow(cur_gen, cur_idx);
+    const u128 even = h_mul(h_add(v, mv), inv2);
+    const u128 odd = h_mul(h_sub(v, mv), h_inv(h_mul(2, gp)));
+    const u128 folded = h_add(even, h_mul(rs[t], odd));
+    if (t + 1 == ntrees) return folded == last;
+    const uint64_t nidx = cur_idx % (cur_n / 2);
+    const uint8_t* nval = rec + off + 32ull * (1 + depth);
+    const u128 nv = nidx == cur_idx ? h_load(nval) : h_load(nval + 16);
+    if (nv != folded) return false;
+    cur_gen = h_mul(cur_gen, cur_gen);
+    cur_n /= 2;
+    cur_idx = nidx;
+    off += 32ull * (1 + depth);
+  }
+  return true;
+}
+
+static uint64_t transcript_query_index(mlh_transcript* tr, uint64_t half) {
+  uint8_t rnd[32];
+  mlh_transcript_random(tr, rnd);
+  uint64_t u;
+  memcpy(&u, rnd, 8);
+  return u % half;
+}
+
 static mlh_status fri_verify_queries(const mlh_fri_proof* pf, mlh_transcript* tr,
                                      const std::vector<u128>& rs) {
   const uint32_t L = pf->log_code;
   const uint64_t domain = 1ull << L;
   const u128 gen = h_pow2_generator(L);
   const uint64_t qbytes = mlh_fri_query_bytes(L);
-  const u128 inv2 = h_inv(2);
   const u128 last = h_load(pf->last_elem);
   for (uint32_t q = 0; q < pf->num_queries; ++q) {
-    uint8_t rnd[32];
-    mlh_transcript_random(tr, rnd);
-    uint64_t u;
-    memcpy(&u, rnd, 8);
-    const uint64_t index = u % (domain / 2);
+    const uint64_t index = transcript_query_index(tr, domain / 2);
     uint8_t le[8];
     memcpy(le, &index, 8);
     mlh_transcript_absorb(tr, le, 8);
     if (pf->query_indices && pf->query_indices[q] != index) return MLH_ERR_VERIFY;
+    if (!query_chain(pf->queries + q * qbytes, pf->commitments, pf->num_trees, domain / 2, index,
+                     gen, rs.data(), last))
+      return MLH_ERR_VERIFY;
+  }
+  uint8_t lr[32];
+  mlh_transcript_random(tr, lr);
+  return memcmp(lr, pf->last_random, 32) == 0 ? MLH_OK : MLH_ERR_VERIFY;
+}
+
+// BatchedFriProof::verify_queries (batched_fri.rs:226-278, 345-388).
+static mlh_status batched_verify_queries(const mlh_batched_fri_proof* pf, mlh_transcript* tr,
+                                         const std::vector<u128>& rs, u128 fr) {
+  const uint32_t L = pf->log_code, m = pf->num_codes;
+  const uint64_t domain = 1ull << L, n = domain / 2;
+  const u128 gen = h_pow2_generator(L);
+  const uint64_t qbytes = mlh_batched_fri_query_bytes(L, m);
+  const u128 inv2 = h_inv(2), last = h_load(pf->last_elem);
+  for (uint32_t q = 0; q < pf->num_queries; ++q) {
+    const uint64_t index = transcript_query_index(tr, n);
+    if (pf->query_indices && pf->query_indices[q] != index) return MLH_ERR_VERIFY;
     const uint8_t* rec = pf->queries + q * qbytes;
-    uint64_t cur_n = domain / 2, cur_idx = index;
-    u128 cur_gen = gen;
-    uint64_t off = 0;
-    for (uint32_t t = 0; t < pf->num_trees; ++t) {
-      const uint32_t depth = L - 1 - t;
-      const uint8_t* val = rec + off;
-      if (!verify_path(val, val + 32, depth, pf->commitments + 32 * t, cur_idx)) return MLH_ERR_VERIFY;
-      const u128 v = h_load(val), mv = h_load(val + 16);
-      const u128 gp = h_pow(cur_gen, cur_idx);
-      const u128 even = h_mul(h_add(v, mv), inv2);
-      const u128 odd = h_mul(h_sub(v, mv), h_inv(h_mul(2, gp)));
-      const u128 folded = h_add(even, h_mul(rs[t], odd));
-      if (t + 1 == pf->num_trees) {
-        if (folded != last) return MLH_ERR_VERIFY;
-        break;
-      }
-      const uint64_t nidx = cur_idx % (cur_n / 2);
-      const uint8_t* nval = rec + off + 32ull * (1 + depth);
-      const u128 nv = nidx == cur_idx ? h_load(nval) : h_load(nval + 16);
-      if (nv != folded) return MLH_ERR_VERIFY;
-      cur_gen = h_mul(cur_gen, cur_gen);
-      cur_n /= 2;
-      cur_idx = nidx;
-      off += 32ull * (1 + depth);
+    if (!verify_path_len(rec, 32ull * m, rec + 32ull * m, L - 1, pf->batch_commitment, index))
+      return MLH_ERR_VERIFY;
+    u128 v = 0, mv = 0;  // fingerprints (Horner over the codes)
+    for (uint32_t j = 0; j < m; ++j) {
+      v = h_add(h_mul(v, fr), h_load(rec + 32ull * j));
+      mv = h_add(h_mul(mv, fr), h_load(rec + 32ull * j + 16));
     }
+    const u128 gp = h_pow(gen, index);
+    const u128 even = h_mul(h_add(v, mv), inv2);
+    const u128 odd = h_mul(h_sub(v, mv), h_inv(h_mul(2, gp)));
+    const u128 folded = h_add(even, h_mul(rs[0], odd));
+    const uint8_t* inner = rec + 32ull * m + 32ull * (L - 1);
+    if (pf->num_trees == 0) {
+      if (folded != last) return MLH_ERR_VERIFY;
+    } else {
+      const uint64_t nidx = index % (n / 2);
+      const u128 nv = nidx == index ? h_load(inner) : h_load(inner + 16);
+      if (nv != folded) return MLH_ERR_VERIFY;
+      if (!query_chain(inner, pf->commitments, pf->num_trees, n / 2, nidx, h_mul(gen, gen),
+                       rs.data() + 1, last))
+        return MLH_ERR_VERIFY;
+    }
+    uint8_t le[8];
+    memcpy(le, &index, 8);
+    mlh_transcript_absorb(tr, le, 8);
   }
   uint8_t lr[32];
   mlh_transcript_random(tr, lr);
@@ -1486,6 +1627,238 @@ mlh_status mlh_bench_ntt(mlh_ctx* ctx, void* dev_buf, uint32_t log_n, uint32_t i
   (void)hipEventDestroy(b);
   *ms_out = ms / iters;
   return MLH_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// batched FRI / batched PCS (src/fri/batched_fri.rs, batched_pcs.rs)
+// ---------------------------------------------------------------------------
+// Queries of a batched proof (batched_fri.rs:287-300): the transcript draws
+// the indices, the batch column + batch siblings and the inner paths are
+// gathered into one device buffer, one D2H.
+static mlh_status batched_queries(mlh_ctx* ctx, FriDevLoop& lp, mlh_transcript* tr,
+                                  mlh_batched_fri_proof* pf) {
+  const uint32_t L = lp.p->log_code, m = lp.m;
+  const uint64_t N = 1ull << L;
+  std::vector<uint64_t> idx(MLH_NUM_QUERIES);
+  for (int q = 0; q < MLH_NUM_QUERIES; ++q) {
+    idx[q] = transcript_query_index(tr, N / 2);
+    uint8_t le[8];
+    memcpy(le, &idx[q], 8);
+    mlh_transcript_absorb(tr, le, 8);
+  }
+  pf->log_code = L;
+  pf->num_codes = m;
+  pf->num_trees = (uint32_t)lp.p->layers.size();
+  pf->num_queries = MLH_NUM_QUERIES;
+  if (pf->query_indices) memcpy(pf->query_indices, idx.data(), idx.size() * 8);
+  memcpy(pf->last_elem, lp.p->last, 16);
+  mlh_transcript_random(tr, pf->last_random);
+  if (pf->commitments) mlh_fri_prover_roots(lp.p, pf->commitments);
+  if (!pf->queries) return MLH_OK;
+  const uint64_t qbytes = mlh_batched_fri_query_bytes(L, m);
+  PoolBuf didx(ctx), dout(ctx), dtrees(ctx);
+  MLH_TRY(didx.alloc(MLH_NUM_QUERIES * sizeof(uint64_t)));
+  MLH_TRY(dout.alloc(MLH_NUM_QUERIES * qbytes));
+  HIP_TRY(ctx, hipMemcpyAsync(didx.p, idx.data(), MLH_NUM_QUERIES * 8, hipMemcpyHostToDevice,
+                              ctx->stream));
+  HIP_TRY(ctx, launch_batch_queries(lp.codes, m, N, lp.btree.as<uint8_t>(), didx.as<uint64_t>(),
+                                    MLH_NUM_QUERIES, qbytes, dout.as<uint8_t>(), ctx->stream));
+  MLH_TRY(gather_queries_dev(ctx, lp.p, didx.as<uint64_t>(), MLH_NUM_QUERIES, qbytes,
+                             32ull * m + 32ull * (L - 1), dout.as<uint8_t>(), dtrees));
+  HIP_TRY(ctx, hipMemcpyAsync(pf->queries, dout.p, MLH_NUM_QUERIES * qbytes,
+                              hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+
+extern "C" {
+
+uint64_t mlh_batched_fri_query_bytes(uint32_t log_code, uint32_t num_codes) {
+  if (log_code < 2 || num_codes == 0) return 0;
+  uint64_t b = 32ull * num_codes + 32ull * (log_code - 1);
+  for (uint32_t t = 0; t + 2 < log_code; ++t) b += 32ull * (1 + (log_code - 2 - t));
+  return b;
+}
+
+mlh_status mlh_batched_fri_prove(mlh_ctx* ctx, const void* dev_codes, uint32_t num_codes,
+                                 uint32_t log_code, mlh_transcript* tr,
+                                 mlh_batched_fri_proof* proof) {
+  if (!ctx || !dev_codes || !tr || !proof) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (num_codes == 0) return fail(ctx, MLH_ERR_INVALID, "Codes must not be empty");
+  if (log_code < 2 || log_code > 40)
+    return fail(ctx, MLH_ERR_NOT_POW2, "Code size must be a power of two (>= 4)");
+  std::unique_ptr<mlh_fri_prover> p(new mlh_fri_prover());
+  p->ctx = ctx;
+  p->log_code = log_code;
+  FriDevLoop lp(ctx, p.get());
+  MLH_TRY(lp.init_batched(reinterpret_cast<const fe*>(dev_codes), num_codes, log_code, tr, true));
+  // fold (batched_fri.rs:178-205): the batched step, then ordinary steps
+  MLH_TRY(lp.step_batched(lp.r(0), true));
+  const uint32_t steps = log_code - MLH_LOG_BLOWUP;
+  for (uint32_t k = 1; k < steps; ++k) MLH_TRY(lp.step(k, lp.r(k), true));
+  MLH_TRY(lp.finish(0));
+  // host transcript replay: batch root, fingerprint_r, inner roots, last
+  mlh_transcript_absorb(tr, lp.host_broot(), 32);
+  mlh_transcript_absorb(tr, lp.host_fr(), 16);
+  for (size_t t = 0; t < p->layers.size(); ++t) mlh_transcript_absorb(tr, p->layers[t].root, 32);
+  mlh_transcript_absorb(tr, p->last, 16);
+  memcpy(proof->batch_commitment, lp.host_broot(), 32);
+  return batched_queries(ctx, lp, tr, proof);
+}
+
+mlh_status mlh_batched_fri_verify(const mlh_batched_fri_proof* pf) {
+  if (!pf || !pf->queries || (pf->num_trees && !pf->commitments) || pf->num_codes == 0)
+    return MLH_ERR_INVALID;
+  if (pf->num_queries != MLH_NUM_QUERIES) return MLH_ERR_VERIFY;
+  if (pf->num_trees + 1 + MLH_LOG_BLOWUP != pf->log_code) return MLH_ERR_VERIFY;
+  mlh_transcript tr;
+  mlh_transcript_absorb(&tr, pf->batch_commitment, 32);
+  uint8_t frb[16];
+  mlh_transcript_next_challenge(&tr, frb);
+  mlh_transcript_absorb(&tr, frb, 16);
+  std::vector<u128> rs;
+  uint8_t r[16];
+  mlh_transcript_next_challenge(&tr, r);
+  rs.push_back(h_load(r));
+  for (uint32_t t = 0; t < pf->num_trees; ++t) {
+    mlh_transcript_absorb(&tr, pf->commitments + 32 * t, 32);
+    mlh_transcript_next_challenge(&tr, r);
+    rs.push_back(h_load(r));
+  }
+  mlh_transcript_absorb(&tr, pf->last_elem, 16);
+  return batched_verify_queries(pf, &tr, rs, h_load(frb));
+}
+
+mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t num_polys,
+                                 uint32_t n_vars, const uint8_t* inputs, const uint8_t* outputs,
+                                 mlh_transcript* tr, mlh_batched_pcs_proof* proof) {
+  if (!ctx || !dev_evals || !inputs || !outputs || !tr || !proof)
+    return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (num_polys == 0) return fail(ctx, MLH_ERR_INVALID, "no polynomials");
+  if (n_vars < 1 || n_vars > 36) return fail(ctx, MLH_ERR_INVALID, "n_vars out of range");
+  const uint32_t log_domain = n_vars + MLH_LOG_BLOWUP;
+  const uint64_t n = 1ull << n_vars, N = 2 * n;
+  uint8_t genb[16];
+  h_store(genb, h_pow2_generator(log_domain));
+  // codes: to_coefficient, bit reverse, RS per polynomial (batched_pcs.rs:137-146)
+  PoolBuf coeffs(ctx), brev(ctx), codes(ctx), matrix(ctx), delta(ctx), outs(ctx);
+  MLH_TRY(coeffs.alloc(n * 16));
+  MLH_TRY(brev.alloc(n * 16));
+  MLH_TRY(codes.alloc((uint64_t)num_polys * N * 16));
+  MLH_TRY(matrix.alloc(n * 16));
+  MLH_TRY(delta.alloc(n * 16));
+  MLH_TRY(outs.alloc(16ull * num_polys));
+  const uint8_t* ev = reinterpret_cast<const uint8_t*>(dev_evals);
+  for (uint32_t j = 0; j < num_polys; ++j) {
+    HIP_TRY(ctx, hipMemcpyAsync(coeffs.p, ev + (uint64_t)j * n * 16, n * 16,
+                                hipMemcpyDeviceToDevice, ctx->stream));
+    MLH_TRY(mlh_mle_to_coefficient(ctx, coeffs.p, n_vars));
+    MLH_TRY(mlh_bit_reverse_permutation(ctx, coeffs.p, brev.p, n_vars));
+    MLH_TRY(mlh_reed_solomon(ctx, brev.p, n_vars, genb,
+                             codes.as<uint8_t>() + (uint64_t)j * N * 16));
+  }
+  // init (batched_pcs.rs:36-78): absorb the claim, batched FRI init
+  for (uint32_t i = 0; i < n_vars; ++i) mlh_transcript_absorb(tr, inputs + 16 * i, 16);
+  for (uint32_t j = 0; j < num_polys; ++j) mlh_transcript_absorb(tr, outputs + 16 * j, 16);
+  std::unique_ptr<mlh_fri_prover> fp(new mlh_fri_prover());
+  fp->ctx = ctx;
+  fp->log_code = log_domain;
+  FriDevLoop lp(ctx, fp.get());
+  MLH_TRY(lp.init_batched(codes.as<fe>(), num_polys, log_domain, tr, false));
+  // fingerprinted MLE + eq table; previous_sum = fingerprint(fr, outputs)
+  HIP_TRY(ctx, launch_fingerprint(reinterpret_cast<const fe*>(dev_evals), num_polys, n, lp.fr(),
+                                  matrix.as<fe>(), ctx->stream));
+  MLH_TRY(mlh_eq_table(ctx, inputs, n_vars, delta.p));
+  {
+    std::vector<uint8_t> ob(outputs, outputs + 16ull * num_polys);
+    HIP_TRY(ctx, hipMemcpyAsync(outs.p, ob.data(), ob.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // ob is pageable and goes out of scope
+  }
+  HIP_TRY(ctx, launch_fingerprint_scalar(outs.as<fe>(), num_polys, lp.fr(), lp.prev(), ctx->stream));
+  fe* sums = ctx->small;
+  HIP_TRY(ctx, launch_sums(matrix.as<fe>(), delta.as<fe>(), n / 2, ctx->partials, sums,
+                           ctx->stream));
+  for (uint32_t k = 0; k < n_vars; ++k) {  // fold (batched_pcs.rs:80-125)
+    HIP_TRY(ctx, launch_sumcheck_round(sums, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
+                                       ctx->stream));
+    const uint64_t S = 1ull << (n_vars - k);
+    if (S >= 4)
+      HIP_TRY(ctx, launch_fold_sums(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->partials, sums,
+                                    ctx->stream, lp.r(k)));
+    else
+      HIP_TRY(ctx, launch_fold(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->stream, lp.r(k)));
+    if (k == 0)
+      MLH_TRY(lp.step_batched(lp.r(0), false));
+    else
+      MLH_TRY(lp.step(k, lp.r(k), false));
+  }
+  MLH_TRY(lp.finish(32ull * n_vars));
+  // host transcript replay
+  const uint8_t* polys = lp.host_polys();
+  if (proof->sumcheck_polys) memcpy(proof->sumcheck_polys, polys, 32ull * n_vars);
+  mlh_transcript_absorb(tr, lp.host_broot(), 32);
+  mlh_transcript_absorb(tr, lp.host_fr(), 16);
+  for (uint32_t k = 0; k < n_vars; ++k) {
+    mlh_transcript_absorb(tr, polys + 32 * k, 16);
+    mlh_transcript_absorb(tr, polys + 32 * k + 16, 16);
+    if (k < fp->layers.size())
+      mlh_transcript_absorb(tr, fp->layers[k].root, 32);
+    else
+      mlh_transcript_absorb(tr, fp->last, 16);
+  }
+  memcpy(proof->fri.batch_commitment, lp.host_broot(), 32);
+  return batched_queries(ctx, lp, tr, &proof->fri);
+}
+
+mlh_status mlh_batched_pcs_verify(const mlh_batched_pcs_proof* pf, uint32_t n_vars,
+                                  const uint8_t* inputs, const uint8_t* outputs,
+                                  mlh_transcript* tr) {
+  if (!pf || !tr || !inputs || !outputs || !pf->sumcheck_polys) return MLH_ERR_INVALID;
+  const mlh_batched_fri_proof* fp = &pf->fri;
+  if (fp->num_queries != MLH_NUM_QUERIES) return MLH_ERR_VERIFY;
+  if (fp->num_trees + 1 != n_vars || fp->num_codes == 0) return MLH_ERR_VERIFY;
+  const uint32_t m = fp->num_codes;
+  for (uint32_t i = 0; i < n_vars; ++i) mlh_transcript_absorb(tr, inputs + 16 * i, 16);
+  for (uint32_t j = 0; j < m; ++j) mlh_transcript_absorb(tr, outputs + 16 * j, 16);
+  std::vector<u128> rs;
+  u128 fr = 0;
+  for (uint32_t i = 0; i < n_vars; ++i) {
+    if (i == 0) {
+      mlh_transcript_absorb(tr, fp->batch_commitment, 32);
+      uint8_t b[16];
+      mlh_transcript_next_challenge(tr, b);
+      fr = h_load(b);
+      mlh_transcript_absorb(tr, b, 16);
+    } else {
+      mlh_transcript_absorb(tr, fp->commitments + 32 * (i - 1), 32);
+    }
+    mlh_transcript_absorb(tr, pf->sumcheck_polys + 32 * i, 32);
+    uint8_t r[16];
+    mlh_transcript_next_challenge(tr, r);
+    rs.push_back(h_load(r));
+  }
+  mlh_transcript_absorb(tr, fp->last_elem, 16);
+  // sumcheck chain from fingerprint(fr, outputs) (batched_pcs.rs:221-240)
+  u128 sum = 0;
+  for (uint32_t j = 0; j < m; ++j) sum = h_add(h_mul(sum, fr), h_load(outputs + 16 * j));
+  const u128 inv2 = h_inv(2);
+  u128 cur = sum, val = 0;
+  for (uint32_t k = 0; k < n_vars; ++k) {
+    const u128 c1 = h_load(pf->sumcheck_polys + 32 * k), c2 = h_load(pf->sumcheck_polys + 32 * k + 16);
+    const u128 c0 = h_mul(h_sub(cur, h_add(c1, c2)), inv2);
+    val = h_add(c0, h_mul(rs[k], h_add(c1, h_mul(c2, rs[k]))));
+    cur = val;
+  }
+  // Delta::evaluate(inputs, rs) (evaluation.rs:75-91)
+  u128 delta = 1;
+  for (uint32_t i = 0; i < n_vars; ++i) {
+    const u128 a = h_load(inputs + 16 * i), b = rs[i];
+    delta = h_mul(delta, h_add(h_mul(a, b), h_mul(h_sub(1, a), h_sub(1, b))));
+  }
+  if (h_mul(delta, h_load(fp->last_elem)) != val) return MLH_ERR_VERIFY;
+  return batched_verify_queries(fp, tr, rs, fr);
 }
 
 }  // extern "C"

@@ -184,3 +184,69 @@ def test_fri_proof_wire_format_matches_oracle_encoding():
     bad[d_off] = 2
     with pytest.raises(_lib.MlhError):
         FriProof.from_bytes(bytes(bad))
+
+
+def _fill_batched(proof, log_code, m):
+    """oracle BatchedFriProof -> C layout (mlh_batched_fri_proof)."""
+    from multilinear_amd.batched import BatchedFriProof
+
+    p = BatchedFriProof(log_code, m)
+    raw = b""
+    for (col, bpath), inner in proof.queries:
+        raw += b"".join(col) + b"".join(s for s, _ in bpath)
+        for value, path in inner:
+            raw += value + b"".join(s for s, _ in path)
+    assert len(raw) == p.qbytes * 128
+    ctypes.memmove(p._q, raw, len(raw))
+    if proof.commitments:
+        ctypes.memmove(p._commit, b"".join(proof.commitments), 32 * len(proof.commitments))
+    p.c.num_trees = len(proof.commitments)
+    p.c.num_queries = 128
+    p.c.query_indices = None
+    p.c.batch_commitment[:] = list(proof.batch_commitment)
+    p.c.last_elem[:] = list(F.to_bytes(proof.last_elem))
+    p.c.last_random[:] = list(proof.last_random)
+    return p
+
+
+@pytest.mark.parametrize("m,log_n", [(1, 4), (3, 5), (2, 1)])
+def test_host_batched_fri_verifier_accepts_oracle_proof(m, log_n):
+    """mlh_batched_fri_verify (batched_fri.rs:313-388) on oracle proofs."""
+    from oracle import batched as OB
+
+    gp = F.pow_2_generator_powers(log_n + 1)
+    codes = [OF.reed_solomon([F.from_i64(7 * i + 3 + 100 * j) for i in range(1 << log_n)], gp[1])
+             for j in range(m)]
+    proof = OB.BatchedFriProof.prove(codes, gp, OT.Transcript())
+    assert proof.verify()
+    p = _fill_batched(proof, log_n + 1, m)
+    assert p.verify()
+    p.c.batch_commitment[3] ^= 1
+    assert not p.verify()
+    p.c.batch_commitment[3] ^= 1
+    p._q[5] ^= 1  # an opened batch value
+    assert not p.verify()
+
+
+def test_host_batched_pcs_verifier_accepts_oracle_proof():
+    """mlh_batched_pcs_verify (batched_pcs.rs:182-250) on an oracle proof."""
+    from multilinear_amd.batched import BatchedPCSProof
+    from oracle import batched as OB
+
+    n, m = 5, 3
+    pts = [F.from_i64(i) for i in range(n)]
+    polys = [[F.from_i64((j * 3 + i * 5) % 100) for j in range(1 << n)] for i in range(m)]
+    outs = [OPL.mle_evaluate(p, pts) for p in polys]
+    pr = OB.BatchedPCSProof.prove(pts, outs, polys, OT.Transcript())
+    assert pr.verify(OT.Transcript())
+    bp = BatchedPCSProof(n, m)
+    fp = _fill_batched(pr.fri_proof, n + 1, m)
+    bp.fri_proof = fp
+    raw = b"".join(F.to_bytes(a) + F.to_bytes(b) for a, b in pr.sumcheck_polynomials)
+    ctypes.memmove(bp._polys, raw, len(raw))
+    bp.inputs, bp.outputs = pts, outs
+    from multilinear_amd.transcript import Transcript
+
+    assert bp.verify(Transcript())
+    bp.outputs = [outs[0] + 1] + outs[1:]
+    assert not bp.verify(Transcript())

@@ -547,3 +547,65 @@ def test_fri_proof_wire_bytes_match_oracle(log_n):
     assert got == want
     q = MF.FriProof.from_bytes(got)
     assert q.verify() and q.to_bytes() == got and q.query_indices == p.query_indices
+
+
+# ---- batched FRI / batched PCS (src/fri/batched_fri.rs, batched_pcs.rs) ------
+
+def _flat_batched_queries(proof):
+    raw = b""
+    for (col, bpath), inner in proof.queries:
+        raw += b"".join(col) + b"".join(s for s, _ in bpath)
+        for value, path in inner:
+            raw += value + b"".join(s for s, _ in path)
+    return raw
+
+
+@pytest.mark.parametrize("m,log_n", [(1, 4), (4, 6), (3, 9), (2, 1), (5, 2)])
+def test_batched_fri_prove_matches_oracle(m, log_n):
+    from multilinear_amd.batched import BatchedFriProof
+    from oracle import batched as OB
+
+    gp = F.pow_2_generator_powers(log_n + 1)
+    codes = [OF.reed_solomon([F.from_i64(7 * i + 3 + 100 * j) for i in range(1 << log_n)], gp[1])
+             for j in range(m)]
+    want = OB.BatchedFriProof.prove(codes, gp, OT.Transcript())
+    got = BatchedFriProof.prove(dev([v for c in codes for v in c]), m, Transcript())
+    assert got.batch_commitment == want.batch_commitment
+    assert got.commitments == want.commitments
+    assert got.last_elem == want.last_elem and got.last_random == want.last_random
+    assert bytes(got._q) == _flat_batched_queries(want)
+    assert got.verify()
+
+
+def test_batched_fri_large_verifies():
+    from multilinear_amd.batched import BatchedFriProof
+
+    m, log_n = 4, 18
+    g = F.pow_2_generator(log_n + 1)
+    codes = [MF.reed_solomon(D.random_device(1 << log_n, 40 + j), g) for j in range(m)]
+    import torch
+
+    p = BatchedFriProof.prove(torch.cat(codes, 0), m, Transcript())
+    assert p.verify()
+
+
+@pytest.mark.parametrize("m,n", [(3, 5), (1, 4), (2, 1), (10, 7)])
+def test_batched_pcs_prove_matches_oracle(m, n):
+    from multilinear_amd.batched import BatchedPCSProof
+    from oracle import batched as OB
+
+    pts = [F.from_i64(i) for i in range(n)]
+    polys = [[F.from_i64((j * 3 + i * 5) % 100) for j in range(1 << n)] for i in range(m)]
+    outs = [OPL.mle_evaluate(p, pts) for p in polys]
+    want = OB.BatchedPCSProof.prove(pts, outs, polys, OT.Transcript())
+    got = BatchedPCSProof.prove(pts, outs, dev([v for p in polys for v in p]), Transcript())
+    assert [tuple(x) for x in got.sumcheck_polynomials] == [tuple(x) for x in want.sumcheck_polynomials]
+    fp = got.fri_proof
+    assert fp.batch_commitment == want.fri_proof.batch_commitment
+    assert fp.commitments == want.fri_proof.commitments
+    assert fp.last_elem == want.fri_proof.last_elem
+    assert fp.last_random == want.fri_proof.last_random
+    assert bytes(fp._q) == _flat_batched_queries(want.fri_proof)
+    assert got.verify(Transcript())
+    got.outputs = [outs[0] + 1] + outs[1:]
+    assert not got.verify(Transcript())
