@@ -213,21 +213,19 @@ __device__ __forceinline__ fe reduce_wide(const uint32_t r[8]) {
   a[3] = subb(a[3], r[7], b, &b);
   a[4] = subb(a[4], 0u, b, &b);
   a[5] = a[5] - b;
-  // Second fold: Th = a[4] + a[5]*2^32 (< 2^47).  Th*C = Th*0x2D00*2^32 - Th.
+  // Second fold: Th = a[4] + a[5]*2^32 (< 2^47).  X = Th*C = Th*0x2D00*2^32 - Th
+  // (>= 0, < 2^93: three limbs); value = a[0..3] + X < 2^128 + 2^93 < 2M.
   const uint64_t th = (uint64_t)a[4] | ((uint64_t)a[5] << 32);
   const uint64_t v = th * (uint64_t)kCmul;  // < 2^61
+  const uint32_t x0 = subb(0u, (uint32_t)th, 0u, &b);
+  const uint32_t x1 = subb((uint32_t)v, (uint32_t)(th >> 32), b, &b);
+  const uint32_t x2 = (uint32_t)(v >> 32) - b;
   fe s;
-  s.w[0] = a[0];
-  s.w[1] = addc(a[1], (uint32_t)v, 0u, &k);
-  s.w[2] = addc(a[2], (uint32_t)(v >> 32), k, &k);
+  s.w[0] = addc(a[0], x0, 0u, &k);
+  s.w[1] = addc(a[1], x1, k, &k);
+  s.w[2] = addc(a[2], x2, k, &k);
   s.w[3] = addc(a[3], 0u, k, &k);
-  uint32_t hi = k;
-  s.w[0] = subb(s.w[0], (uint32_t)th, 0u, &b);
-  s.w[1] = subb(s.w[1], (uint32_t)(th >> 32), b, &b);
-  s.w[2] = subb(s.w[2], 0u, b, &b);
-  s.w[3] = subb(s.w[3], 0u, b, &b);
-  hi -= b;  // value = s + hi*2^128, hi in {0,1}
-  return canon_with_carry(s, hi);
+  return canon_with_carry(s, k);
 }
 
 __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
@@ -273,22 +271,19 @@ __device__ __forceinline__ fe fe_mul_pre_r(const fe& a, const fe& B0, const fe& 
   mac_carry(acc, a.w[3], B3.w[3], c2);
   r3 = (uint32_t)acc;
   const uint32_t t_lo = (uint32_t)(acc >> 32), t_hi = c2;  // T = t_lo + t_hi 2^32 < 2^34
-  // value = r + T*0x2D00*2^32 - T  (>= 0, < 2^128 + 2^80)
+  // X = T*C = T*0x2D00*2^32 - T (>= 0, < 2^80: three limbs), value = r + X < 2^128 + 2^80
   const uint64_t v = (uint64_t)t_lo * kCmul;
   const uint32_t vh = (uint32_t)(v >> 32) + __umul24(t_hi, kCmul);
-  uint32_t k, b;
+  uint32_t b, k;
+  const uint32_t x0 = subb(0u, t_lo, 0u, &b);
+  const uint32_t x1 = subb((uint32_t)v, t_hi, b, &b);
+  const uint32_t x2 = vh - b;
   fe s;
-  s.w[0] = r0;
-  s.w[1] = addc(r1, (uint32_t)v, 0u, &k);
-  s.w[2] = addc(r2, vh, k, &k);
+  s.w[0] = addc(r0, x0, 0u, &k);
+  s.w[1] = addc(r1, x1, k, &k);
+  s.w[2] = addc(r2, x2, k, &k);
   s.w[3] = addc(r3, 0u, k, &k);
-  uint32_t hi = k;
-  s.w[0] = subb(s.w[0], t_lo, 0u, &b);
-  s.w[1] = subb(s.w[1], t_hi, b, &b);
-  s.w[2] = subb(s.w[2], 0u, b, &b);
-  s.w[3] = subb(s.w[3], 0u, b, &b);
-  hi -= b;  // value = s + hi*2^128, hi in {0,1}
-  return canon_with_carry(s, hi);
+  return canon_with_carry(s, k);
 }
 
 __device__ __forceinline__ fe fe_mul_pre(const fe& a, const fe* B) {
