@@ -69,6 +69,30 @@ def cpu_baseline(log_n):
     }
 
 
+def cpu_baseline_all_cores(log_n):
+    """OpenMP variant of the same C restatement on the host cores the box
+    grants (OMP_NUM_THREADS, else os.cpu_count()); SURVEY.md 8(d)."""
+    from multilinear_amd import device as D
+    from oracle import coracle
+    from oracle import field as F
+
+    threads = int(os.environ.get("OMP_NUM_THREADS") or (os.cpu_count() or 1))
+    x = D.random_limbs(1 << log_n, 1)
+    g = F.pow_2_generator(log_n)
+    coracle.ntt_omp(x[: 1 << 12], 12, F.pow_2_generator(12), threads)  # thread pool warm-up
+    t0 = time.perf_counter()
+    coracle.ntt_omp(x, log_n, g, threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": (1 << log_n) / dt,
+        "unit": "field-elems/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": "one 2^%d-point forward NTT, OpenMP restatement (stages split over %d threads), "
+                  "%.3f s" % (log_n, threads, dt),
+    }
+
+
 def load_pmc(kernel, log_n):
     """HBM traffic per launch from the committed rocprofv3 PMC summary, if it
     matches this kernel/size (tools/pmc_summary.py writes it)."""
@@ -302,6 +326,10 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(log_n)
+        try:
+            result["cpu_baseline_all_cores"] = cpu_baseline_all_cores(log_n)
+        except Exception as e:  # the 1-core baseline stays the reported one
+            result["cpu_baseline_all_cores"] = {"error": str(e)}
         result["vs_cpu_1core"] = value / result["cpu_baseline"]["value"]
 
     if dist is not None:

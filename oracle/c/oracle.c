@@ -240,6 +240,63 @@ int orc_ntt(const uint8_t* in, uint8_t* out, uint32_t log_n, const uint8_t gen[1
   return 0;
 }
 
+
+/* OpenMP variant of orc_ntt (same loops, butterflies of a stage split over
+ * `threads` cores; twiddle table of each stage built in per-thread chunks).
+ * The cpu_baseline "all host cores" figure; not a checker. */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+int orc_ntt_omp(const uint8_t* in, uint8_t* out, uint32_t log_n, const uint8_t gen[16], int threads) {
+  uint64_t n = 1ull << log_n;
+  if (log_n < 1) return 2;
+  u128* v = (u128*)malloc(n * sizeof(u128));
+  u128* pows = (u128*)malloc(sizeof(u128) * (n / 2));
+  if (!v || !pows) return 5;
+  memcpy(v, in, n * 16);
+  int bits = (int)log_n;
+  long long N = (long long)n;
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (long long i = 0; i < N; i++) {
+    uint64_t j = rev_bits((uint64_t)i, bits);
+    if ((uint64_t)i < j) {
+      u128 t = v[i];
+      v[i] = v[j];
+      v[j] = t;
+    }
+  }
+  u128 g = ld(gen);
+  for (uint64_t len = 2; len <= n; len *= 2) {
+    const u128 cur = fpow(g, n / len);
+    const long long half = (long long)(len / 2);
+#pragma omp parallel num_threads(threads)
+    {
+#ifdef _OPENMP
+      const int t = omp_get_thread_num(), T = omp_get_num_threads();
+#else
+      const int t = 0, T = 1;
+#endif
+      const long long lo = half * t / T, hi = half * (t + 1) / T;
+      u128 acc = fpow(cur, (u128)lo);
+      for (long long j = lo; j < hi; j++) {
+        pows[j] = acc;
+        acc = fmul(acc, cur);
+      }
+    }
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (long long b = 0; b < N / 2; b++) {
+      const uint64_t i = ((uint64_t)b / half) * len, j = (uint64_t)b % half;
+      u128 w = fmul(v[i + j + half], pows[j]), u = v[i + j];
+      v[i + j] = fadd(u, w);
+      v[i + j + half] = fsub(u, w);
+    }
+  }
+  memcpy(out, v, n * 16);
+  free(v);
+  free(pows);
+  return 0;
+}
+
 void orc_pow_2_generator(uint32_t log_size, uint8_t out[16]) {
   st(out, fpow(3, (MOD - 1) >> log_size));
 }

@@ -27,6 +27,7 @@ def lib():
         L.orc_fold.argtypes = [P, P, U, P]
         L.orc_sha256.argtypes = [P, ctypes.c_uint64, P]
         L.orc_mul.argtypes = [P, P, P]
+        L.orc_ntt_omp.argtypes = [P, P, U, P, ctypes.c_int]
         L.orc_pow_2_generator.argtypes = [U, P]
         L.orc_pow_2_generator_powers.argtypes = [U, P]
         _lib = L
@@ -47,6 +48,15 @@ def ntt(limbs, log_n, gen, inverse=False):
     out = np.empty_like(a)
     g = _fe(gen)
     rc = lib().orc_ntt(_p(a), _p(out), log_n, _p(g), 1 if inverse else 0)
+    assert rc == 0
+    return out
+
+
+def ntt_omp(limbs, log_n, gen, threads):
+    """OpenMP variant of ntt (cpu_baseline on all host cores)."""
+    a = np.ascontiguousarray(limbs, dtype=np.uint32)
+    out = np.empty_like(a)
+    rc = lib().orc_ntt_omp(_p(a), _p(out), log_n, _p(_fe(gen)), threads)
     assert rc == 0
     return out
 
