@@ -323,6 +323,11 @@ def main():
             result.update(config5(args, lib, ctx, local, world, rank, barrier))
         except Exception as e:  # keep the headline line; report the failure
             result["config5_error"] = "%s: %s" % (type(e).__name__, e)
+        if world > 1:
+            try:
+                result.update(config4_sharded(args, local, world, rank, barrier))
+            except Exception as e:
+                result["config4_sharded_error"] = "%s: %s" % (type(e).__name__, e)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(log_n)
@@ -337,6 +342,44 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def config4_sharded(args, local, world, rank, barrier):
+    """Config 4 over the N ranks (strong scaling): 2^24-entry MLE in the cyclic
+    layout, sharded eq table + 24 sumcheck rounds (multilinear_amd/dist.py)."""
+    import random
+
+    import torch
+
+    from multilinear_amd import device as D
+    from multilinear_amd import dist as DS
+    from multilinear_amd.transcript import Transcript
+
+    n = args.log_n
+    tp, ops = DS.Transport(), DS.HipOps(local)
+    rr = random.Random(5)
+    pts = [rr.randrange(D.M) for _ in range(n)]
+    base = D.random_device(1 << (n - tp.world.bit_length() + 1), 500 + rank, local)
+
+    def run():
+        m = base.clone()
+        d = DS.eq_table(pts, tp, ops)
+        return DS.sumcheck_prove(m, d, n, 0, Transcript(), tp, ops)
+
+    run()
+    barrier()
+    reps = max(1, min(args.extra_reps, 3))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    import torch.distributed as tdist
+
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return {"config4_sharded_eq_sumcheck_ms": float(t.item()) * 1e3,
+            "config4_layout": "sharded x%d (cyclic by low index bits)" % world}
 
 
 def config5(args, lib, ctx, local, world, rank, barrier):
