@@ -32,8 +32,22 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# RCCL in production; MLH_BENCH_BACKEND=gloo rehearses the multi-rank logic with
+# host-staged exchanges (e.g. 2 ranks sharing one GPU).  Never used for a result.
+BACKEND = os.environ.get("MLH_BENCH_BACKEND", "nccl")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK = 7.864e13   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz full-rate lane-ops/s
+
+
+def _allreduce_max(x):
+    """max over ranks of a host float (device tensor for RCCL, host for gloo)."""
+    import torch
+    import torch.distributed as tdist
+
+    dev = "cuda" if BACKEND == "nccl" else "cpu"
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def cpu_model():
@@ -126,12 +140,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if BACKEND != "nccl":  # rehearsal: ranks may share the box's GPU(s)
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:  # rehearsal of the N > 1 path with several ranks on one GPU
+            dist.init_process_group(BACKEND)
 
     from multilinear_amd import device as D
     from multilinear_amd import fri as MF
@@ -154,7 +173,7 @@ def main():
     else:
         from multilinear_amd import dist as DS
 
-        tp, ops = DS.Transport(), DS.HipOps(local)
+        tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
         g_total = int.from_bytes(bytes(_gen(lib, log_n + log_p)), "little")
 
         def ntt_once():  # x: this rank's cyclic shard of the N * 2^24 vector
@@ -175,9 +194,7 @@ def main():
     torch.cuda.synchronize()
     iters = int(args.spinup_s / max(time.perf_counter() - t_one, 1e-5)) + 1
     if dist is not None:
-        t = torch.tensor([iters], dtype=torch.int64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        iters = int(t.item())
+        iters = int(_allreduce_max(iters))
     for _ in range(min(iters, 5000)):
         ntt_once()
     barrier()
@@ -194,9 +211,7 @@ def main():
     lib.mlh_profile_enable(ctx, 0)
     elapsed = t1 - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = _allreduce_max(elapsed)
     barrier()
 
     # dominant kernel timing (HIP events on the launch stream, timed region)
@@ -356,7 +371,7 @@ def config4_sharded(args, local, world, rank, barrier):
     from multilinear_amd.transcript import Transcript
 
     n = args.log_n
-    tp, ops = DS.Transport(), DS.HipOps(local)
+    tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
     rr = random.Random(5)
     pts = [rr.randrange(D.M) for _ in range(n)]
     base = D.random_device(1 << (n - tp.world.bit_length() + 1), 500 + rank, local)
@@ -376,9 +391,7 @@ def config4_sharded(args, local, world, rank, barrier):
     dt = (time.perf_counter() - t0) / reps
     import torch.distributed as tdist
 
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-    return {"config4_sharded_eq_sumcheck_ms": float(t.item()) * 1e3,
+    return {"config4_sharded_eq_sumcheck_ms": _allreduce_max(dt) * 1e3,
             "config4_layout": "sharded x%d (cyclic by low index bits)" % world}
 
 
@@ -403,7 +416,7 @@ def config5(args, lib, ctx, local, world, rank, barrier):
     else:
         from multilinear_amd import dist as DS
 
-        tp, ops = DS.Transport(), DS.HipOps(local)
+        tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
         coeffs = D.random_device(1 << (L - 1 - tp.world.bit_length() + 1), 77 + rank, local)
 
         def run():
@@ -420,9 +433,7 @@ def config5(args, lib, ctx, local, world, rank, barrier):
     import torch.distributed as tdist
 
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = _allreduce_max(dt)
     return {"config5_log_code": L, "config5_rs_fri_prove_ms": dt * 1e3,
             "config5_verified": bool(p.verify()),
             "config5_layout": "single GPU" if world == 1 else "sharded x%d" % world}
