@@ -1214,8 +1214,9 @@ mlh_status mlh_eq_table(mlh_ctx* ctx, const uint8_t* host_points, uint32_t n, vo
   if (n) HIP_TRY(ctx, hipMemcpyAsync(pts.p, host_points, n * 16ull, hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, launch_eq_table(pts.as<fe>(), n, scratch.as<fe>(), reinterpret_cast<fe*>(dev_out),
                                ctx->stream));
-  // pts/scratch return to the pool: keep them alive until the kernels ran
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  // pts/scratch go back to the pool now: a later user of those blocks is
+  // ordered after these kernels on the same stream (and the pageable H2D
+  // above has consumed host_points before returning)
   return MLH_OK;
 }
 
@@ -1292,18 +1293,22 @@ mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, u
   HIP_TRY(ctx, hipMemcpyAsync(sb, ctx->pinned, 144, hipMemcpyHostToDevice, ctx->stream));
   fe* m = reinterpret_cast<fe*>(dev_matrix);
   fe* d = reinterpret_cast<fe*>(dev_delta);
-  HIP_TRY(ctx, launch_sums(m, d, 1ull << (L - 1), ctx->partials, ctx->small, ctx->stream));
+  uint32_t np = 0;
+  HIP_TRY(ctx, launch_sums(m, d, 1ull << (L - 1), ctx->partials, ctx->small, ctx->stream, &np));
   for (uint32_t k = 0; k < L; ++k) {
-    HIP_TRY(ctx, launch_sumcheck_round(ctx->small, prev, dt, polys + 2 * k, rs + k, ctx->stream));
+    HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, prev, dt, polys + 2 * k, rs + k,
+                                       ctx->stream));
     const uint64_t S = 1ull << (L - k);
     if (S >= 4)
-      HIP_TRY(ctx, launch_fold_sums(m, d, S, fe{}, ctx->partials, ctx->small, ctx->stream, rs + k));
+      HIP_TRY(ctx, launch_fold_sums(m, d, S, fe{}, ctx->partials, ctx->small, ctx->stream, rs + k,
+                                    &np));
     else
       HIP_TRY(ctx, launch_fold(m, d, S, fe{}, ctx->stream, rs + k));
   }
   std::vector<uint8_t> host(48ull * L);
-  HIP_TRY(ctx, hipMemcpyAsync(host.data(), polys, 48ull * L, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(host.data(), ctx->pinned, 48ull * L);
   for (uint32_t k = 0; k < L; ++k) {  // host transcript replay (sumcheck.rs:188-199)
     mlh_transcript_absorb(tr, host.data() + 32 * k, 16);
     mlh_transcript_absorb(tr, host.data() + 32 * k + 16, 16);
@@ -1352,15 +1357,16 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   HIP_TRY(ctx, hipMemcpyAsync(lp.prev(), ctx->pinned + 3072, 16, hipMemcpyHostToDevice,
                               ctx->stream));
   fe* sums = ctx->small;
+  uint32_t np = 0;
   HIP_TRY(ctx, launch_sums(matrix.as<fe>(), delta.as<fe>(), n / 2, ctx->partials, sums,
-                           ctx->stream));
+                           ctx->stream, &np));
   for (uint32_t k = 0; k < n_vars; ++k) {
-    HIP_TRY(ctx, launch_sumcheck_round(sums, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
+    HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
                                        ctx->stream));
     const uint64_t S = 1ull << (n_vars - k);
     if (S >= 4) {
       HIP_TRY(ctx, launch_fold_sums(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->partials, sums,
-                                    ctx->stream, lp.r(k)));
+                                    ctx->stream, lp.r(k), &np));
     } else {
       HIP_TRY(ctx, launch_fold(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->stream, lp.r(k)));
     }
@@ -1778,15 +1784,16 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   }
   HIP_TRY(ctx, launch_fingerprint_scalar(outs.as<fe>(), num_polys, lp.fr(), lp.prev(), ctx->stream));
   fe* sums = ctx->small;
+  uint32_t np = 0;
   HIP_TRY(ctx, launch_sums(matrix.as<fe>(), delta.as<fe>(), n / 2, ctx->partials, sums,
-                           ctx->stream));
+                           ctx->stream, &np));
   for (uint32_t k = 0; k < n_vars; ++k) {  // fold (batched_pcs.rs:80-125)
-    HIP_TRY(ctx, launch_sumcheck_round(sums, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
+    HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
                                        ctx->stream));
     const uint64_t S = 1ull << (n_vars - k);
     if (S >= 4)
       HIP_TRY(ctx, launch_fold_sums(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->partials, sums,
-                                    ctx->stream, lp.r(k)));
+                                    ctx->stream, lp.r(k), &np));
     else
       HIP_TRY(ctx, launch_fold(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->stream, lp.r(k)));
     if (k == 0)

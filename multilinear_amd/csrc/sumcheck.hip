@@ -231,19 +231,27 @@ static inline unsigned red_blocks(uint64_t work) {
 }
 
 hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* out,
-                       hipStream_t st) {
+                       hipStream_t st, uint32_t* nparts) {
   const unsigned nb = red_blocks(h);
   hipLaunchKernelGGL(sums_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, d, h, partials);
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, out);
+  if (nparts)
+    *nparts = nb;  // the caller reduces (sumcheck_round_kernel)
+  else
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb,
+                       out);
   return hipGetLastError();
 }
 
 hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* out,
-                            hipStream_t st, const fe* r_dev) {
+                            hipStream_t st, const fe* r_dev, uint32_t* nparts) {
   const unsigned nb = red_blocks(S / 4);
   hipLaunchKernelGGL(fold_sums_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, d, S, r, partials,
                      r_dev);
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, out);
+  if (nparts)
+    *nparts = nb;
+  else
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb,
+                       out);
   return hipGetLastError();
 }
 
@@ -316,29 +324,38 @@ namespace mlh {
 // interpolation on x = 0,1,2 (polynomials.rs:51-87): e0 = prev - s1,
 // c2 = (s2 - 2 s1 + e0) / 2, c1 = s1 - e0 - c2; absorb LE16(c1), LE16(c2)
 // (sumcheck.rs:188-199), r = next_challenge(), prev = e0 + r (c1 + c2 r).
-__global__ void sumcheck_round_kernel(const fe* sums, fe* prev, DevSha* t, fe* poly_out,
-                                      fe* r_out) {
+__global__ void __launch_bounds__(kRedThreads)
+sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev, DevSha* t,
+                      fe* poly_out, fe* r_out) {
   __shared__ DevSha s;
+  // the round sums: reduce the per-workgroup partials (loads unrolled so a
+  // lane's few loads are in flight together), then one lane runs the round
+  fe s1 = fe_zero(), s2 = fe_zero();
+#pragma unroll 4
+  for (uint32_t i = threadIdx.x; i < nparts; i += kRedThreads) {
+    s1 = fe_add(s1, fe_load(partials + 2 * i));
+    s2 = fe_add(s2, fe_load(partials + 2 * i + 1));
+  }
+  block_reduce2(s1, s2);
   if (threadIdx.x != 0) return;
-  const fe s1 = fe_load(sums), s2 = fe_load(sums + 1), p = fe_load(prev);
+  const fe p = fe_load(prev);
   const fe e0 = fe_sub(p, s1);
   const fe c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
   const fe c1 = fe_sub(fe_sub(s1, e0), c2);
   fe_store(poly_out, c1);
   fe_store(poly_out + 1, c2);
   s = *t;
-  dsha_update(s, reinterpret_cast<const uint8_t*>(&c1), 16);
-  dsha_update(s, reinterpret_cast<const uint8_t*>(&c2), 16);
+  dsha_update(s, reinterpret_cast<const uint8_t*>(poly_out), 32);
   *t = s;
   const fe r = dsha_challenge(s);
   fe_store(r_out, r);
   fe_store(prev, fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r)))));
 }
 
-hipError_t launch_sumcheck_round(const fe* sums, fe* prev, DevSha* t, fe* poly_out, fe* r_out,
-                                 hipStream_t st) {
-  hipLaunchKernelGGL(sumcheck_round_kernel, dim3(1), dim3(64), 0, st, sums, prev, t, poly_out,
-                     r_out);
+hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, DevSha* t,
+                                 fe* poly_out, fe* r_out, hipStream_t st) {
+  hipLaunchKernelGGL(sumcheck_round_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nparts,
+                     prev, t, poly_out, r_out);
   return hipGetLastError();
 }
 

@@ -11,15 +11,17 @@ constexpr uint32_t kMaxRedBlocks = 2048;  // partials buffer: 2 * kMaxRedBlocks 
 
 // out[0] = s1, out[1] = s2 over tables of size 2h (device).
 hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* out,
-                       hipStream_t st);
+                       hipStream_t st, uint32_t* nparts = nullptr);
 // fold size-S tables with r, then sums of the folded (size S/2) tables.
+// nparts != null: skip the partials reduction and report the partial count
 hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* out,
-                            hipStream_t st, const fe* r_dev = nullptr);
+                            hipStream_t st, const fe* r_dev = nullptr, uint32_t* nparts = nullptr);
 hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe* r_dev = nullptr);
 struct DevSha;
-// one sumcheck round (interpolate, absorb, challenge, new claim) on the device
-hipError_t launch_sumcheck_round(const fe* sums, fe* prev, DevSha* t, fe* poly_out, fe* r_out,
-                                 hipStream_t st);
+// one sumcheck round on the device: reduce the nparts partial sum pairs,
+// interpolate, absorb, challenge, new claim
+hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, DevSha* t,
+                                 fe* poly_out, fe* r_out, hipStream_t st);
 hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
                       hipStream_t st);
 hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st);

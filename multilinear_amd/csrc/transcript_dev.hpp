@@ -23,16 +23,28 @@ struct DevSha {
 
 __device__ inline void dsha_compress_buf(DevSha& s) {
   uint32_t w[16];
-  for (int i = 0; i < 16; ++i)
-    w[i] = ((uint32_t)s.buf[4 * i] << 24) | ((uint32_t)s.buf[4 * i + 1] << 16) |
-           ((uint32_t)s.buf[4 * i + 2] << 8) | (uint32_t)s.buf[4 * i + 3];
+  const uint32_t* bw = reinterpret_cast<const uint32_t*>(s.buf);
+  for (int i = 0; i < 16; ++i) w[i] = bswap32(bw[i]);  // big-endian words
   Sha256State st;
   for (int i = 0; i < 8; ++i) st.h[i] = s.h[i];
   sha256_compress(st, w);
   for (int i = 0; i < 8; ++i) s.h[i] = st.h[i];
 }
 
+// Word path when the fill and the length are multiples of 4 and p is
+// 4-byte aligned (every device absorb: roots, field elements); bytes
+// otherwise.  buf keeps memory byte order, exactly as HostSha256.
 __device__ inline void dsha_update(DevSha& s, const uint8_t* p, uint32_t n) {
+  if (((s.len | n | reinterpret_cast<uintptr_t>(p)) & 3) == 0) {
+    uint32_t* bw = reinterpret_cast<uint32_t*>(s.buf);
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(p);
+    for (uint32_t i = 0; i < n / 4; ++i) {
+      bw[(s.len % 64) / 4] = pw[i];
+      s.len += 4;
+      if (s.len % 64 == 0) dsha_compress_buf(s);
+    }
+    return;
+  }
   for (uint32_t i = 0; i < n; ++i) {
     s.buf[s.len % 64] = p[i];
     s.len += 1;
@@ -41,17 +53,32 @@ __device__ inline void dsha_update(DevSha& s, const uint8_t* p, uint32_t n) {
 }
 
 // digest of a clone (the state itself is unchanged); the clone is padded in
-// place in a word buffer (at most two compressions)
+// place (at most two compressions)
 __device__ inline void dsha_digest(const DevSha& s0, uint8_t out[32]) {
   __shared__ DevSha c;
   c = s0;
   const uint64_t bits = c.len * 8;
-  const uint8_t one = 0x80, z = 0;
-  dsha_update(c, &one, 1);
-  while (c.len % 64 != 56) dsha_update(c, &z, 1);
-  uint8_t lb[8];
-  for (int i = 0; i < 8; ++i) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
-  dsha_update(c, lb, 8);
+  if ((c.len & 3) == 0) {
+    uint32_t* bw = reinterpret_cast<uint32_t*>(c.buf);
+    uint32_t pos = (uint32_t)(c.len % 64) / 4;
+    bw[pos++] = 0x80u;  // byte 0x80 then zeros, memory order
+    if (pos > 14) {
+      for (; pos < 16; ++pos) bw[pos] = 0;
+      dsha_compress_buf(c);
+      pos = 0;
+    }
+    for (; pos < 14; ++pos) bw[pos] = 0;
+    bw[14] = bswap32((uint32_t)(bits >> 32));
+    bw[15] = bswap32((uint32_t)bits);
+    dsha_compress_buf(c);
+  } else {
+    const uint8_t one = 0x80, z = 0;
+    dsha_update(c, &one, 1);
+    while (c.len % 64 != 56) dsha_update(c, &z, 1);
+    uint8_t lb[8];
+    for (int i = 0; i < 8; ++i) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
+    dsha_update(c, lb, 8);
+  }
   for (int i = 0; i < 8; ++i) {
     out[4 * i] = (uint8_t)(c.h[i] >> 24);
     out[4 * i + 1] = (uint8_t)(c.h[i] >> 16);
