@@ -287,6 +287,58 @@ def ntt(x_local, log_n, gen, tp, ops):
     return ops.cross(recv, log_n, _log2(P), tp.rank, gen, False)
 
 
+class NttPipeline:
+    """Sharded forward NTTs of a stream of independent vectors with the
+    all-to-all of vector i overlapping the local transform of vector i+1:
+    local NTTs and the cross-shard kernels run on the current (compute)
+    stream, the exchanges on a second stream, ordered by events.
+
+        pipe = NttPipeline(log_n, gen, tp, ops)
+        for x in xs: pipe.submit(x)        # returns finished outputs, in order
+        outs += pipe.drain()
+    """
+
+    def __init__(self, log_n, gen, tp, ops):
+        import torch
+
+        self.log_n, self.gen, self.tp, self.ops = log_n, gen, tp, ops
+        self.P = tp.world
+        self.comm = torch.cuda.Stream()
+        self.pending = None
+
+    def _finish(self):
+        import torch
+
+        recv, ev = self.pending
+        self.pending = None
+        comp = torch.cuda.current_stream()
+        comp.wait_event(ev)
+        recv.record_stream(comp)
+        return self.ops.cross(recv, self.log_n, _log2(self.P), self.tp.rank, self.gen, False)
+
+    def submit(self, x):
+        import torch
+
+        if self.P == 1:
+            return [self.ops.ntt(x, self.gen)]
+        comp = torch.cuda.current_stream()
+        z = self.ops.ntt(x, pow(self.gen, self.P, M))
+        ready = torch.cuda.Event()
+        ready.record(comp)
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(ready)
+            z.record_stream(self.comm)
+            recv = self.tp.all_to_all(z)
+            done = torch.cuda.Event()
+            done.record(self.comm)
+        out = [self._finish()] if self.pending is not None else []
+        self.pending = (recv, done)
+        return out
+
+    def drain(self):
+        return [self._finish()] if self.pending is not None else []
+
+
 def intt(X_local, log_n, gen, tp, ops):
     """LagrangePolynomial::intt (ntt/mod.rs:132-173): block-(n/P^2) layout in,
     cyclic layout out."""

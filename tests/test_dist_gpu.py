@@ -220,3 +220,49 @@ def test_sharded_sumcheck_multiprocess(world, n):
     for r in range(world):
         assert [tuple(p) for p in res[r]["polys"]] == [tuple(p) for p in ref["polys"]]
         assert res[r]["rs"] == ref["rs"] and res[r]["lr"] == ref["lr"]
+
+
+def _pipe_worker(rank, world, port, log_n, q):
+    import torch.distributed as tdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        tp, ops = D.Transport(host_staged=True), D.HipOps(0)
+        gen = MN.pow_2_generator(log_n)
+        xs = [DV.to_device(D.shard_cyclic(DV.random_limbs(1 << log_n, seed=s), world, rank))
+              for s in range(4)]
+        pipe = D.NttPipeline(log_n, gen, tp, ops)
+        outs = []
+        for x in xs:
+            outs += pipe.submit(x)
+        outs += pipe.drain()
+        ref = [D.ntt(x, log_n, gen, tp, ops) for x in xs]
+        torch.cuda.synchronize()
+        q.put((rank, {"ok": all(torch.equal(a, b) for a, b in zip(outs, ref)) and len(outs) == 4}))
+    except Exception:
+        import traceback
+
+        q.put((rank, {"error": traceback.format_exc()}))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_ntt_pipeline_matches_sharded_ntt():
+    world, log_n = 2, 16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, log_n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=300) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+        assert res[r]["ok"]
