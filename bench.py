@@ -40,6 +40,10 @@ sys.path.insert(0, ROOT)
 BACKEND = os.environ.get("MLH_BENCH_BACKEND", "nccl")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK = 7.864e13   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz full-rate lane-ops/s
+# practical issue rate of the butterfly instruction mix (fe_mul_pre + add + sub,
+# register resident, no memory): tools/bfly_peak.hip measured 5.3e11
+# butterflies/s x 301 VALU per 4 butterflies = 4.0e13 lane-instr/s
+VALU_PRACTICAL = 4.0e13
 
 
 def _allreduce_max(x):
@@ -108,6 +112,24 @@ def cpu_baseline_all_cores(log_n):
         "sample": "one 2^%d-point forward NTT, OpenMP restatement (stages split over %d threads), "
                   "%.3f s" % (log_n, threads, dt),
     }
+
+
+def load_valu(kernel):
+    """SQ_INSTS_VALU per launch of `kernel` from the committed VALU summary
+    (tools/valu_summary.py), or None."""
+    import glob
+
+    r, tw, z = kernel[len("ntt_pass<"):-1].split(",")
+    name = "void mlh::ntt_pass_kernel<%s, %s, %s>" % (r, tw, "true" if z == "1" else "false")
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(name)
+        if k and d.get("log_n", 24) == 24:
+            return k["SQ_INSTS_VALU"], os.path.basename(path)
+    return None
 
 
 def load_pmc(kernel, log_n):
@@ -284,6 +306,15 @@ def main():
         },
         "kernels": kernels,
     }
+    valu = load_valu(dom_name) if log_n == 24 else None
+    if valu:
+        rate = valu[0] * 64 / (dom_stat["avg_ms"] * 1e-3)
+        result["valu_roofline"] = {
+            "kernel": dom_name, "achieved": rate, "unit": "lane-instr/s",
+            "peak_practical": VALU_PRACTICAL, "frac_practical": rate / VALU_PRACTICAL,
+            "peak_nominal": VALU_PEAK, "frac_nominal": rate / VALU_PEAK,
+            "source": "SQ_INSTS_VALU per launch (%s) x 64 lanes / live avg launch time" % valu[1],
+        }
 
     if not args.no_extras and world == 1:
         reps = args.extra_reps

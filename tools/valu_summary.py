@@ -29,7 +29,7 @@ def main():
     dur = {}
     for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))):
         dur[int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-    out = {"round": tag, "nominal_lane_instr_per_s": NOMINAL, "kernels": {}}
+    out = {"round": tag, "log_n": 24, "nominal_lane_instr_per_s": NOMINAL, "kernels": {}}
     for name, cs in ctr.items():
         if not any(w in name for w in want):
             continue
