@@ -3,12 +3,16 @@
 Metric: "NTT 2^24 field-elems/sec + FRI commit ms; % HBM roofline".
   * N = 1: step = one forward 2^24-point NTT (config 2, src/ntt/mod.rs:69-110)
             over a device-resident synthetic vector (seeded uniform elements);
-  * N > 1: step = one SHARDED forward NTT of N * 2^24 points (weak scaling:
-            2^24 elements per GPU): local 2^24 NTT, one RCCL all-to-all over
-            xGMI, cross-shard DFT kernel (multilinear_amd/dist.py); the K steps
-            are independent transforms streamed through dist.NttPipeline, so
-            the exchange of step i overlaps the local NTT of step i+1 (all K
-            exchanges and cross kernels complete inside the timed region);
+  * N > 1 (default --mode replicas): every rank transforms its own 2^24-point
+            polynomial per step -- independent objects, no data-path
+            collective, weak scaling;
+  * N > 1, extra "sharded_ntt" (and the headline with --mode sharded): one
+            forward NTT of N * 2^24 points per step, 2^24 per GPU: local NTT,
+            one RCCL all-to-all over xGMI, cross-shard DFT kernel
+            (multilinear_amd/dist.py); the K steps stream through
+            dist.NttPipeline so the exchange of step i overlaps the local NTT
+            of step i+1 (every exchange and cross kernel completes inside the
+            timed region);
   * value = 2^24 * N * steps / max-over-ranks(time of the K steps);
   * extras in the same JSON line: inverse NTT, FRI commit (config 3: 2^24
     coeffs -> RS LDE 2^25 -> Merkle root), full FRI prove, the 24-round
@@ -158,6 +162,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--fri-log", type=int, default=28, help="config 5 codeword size (log2)")
+    ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas",
+                    help="N > 1 headline step: each GPU transforms its own 2^24 polynomial "
+                         "(replicas) or one N*2^24 transform is sharded with an all-to-all")
     args = ap.parse_args()
 
     import torch
@@ -192,23 +199,26 @@ def main():
     if world & (world - 1):
         raise SystemExit("world size must be a power of two")
     log_p = world.bit_length() - 1
-    if world == 1:
-        def ntt_once():
-            D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(out), log_n, gen), ctx)
+    sharded = world > 1 and args.mode == "sharded"
 
-        def ntt_drain():
-            pass
-    else:
+    def ntt_local():
+        D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(out), log_n, gen), ctx)
+
+    pipe = None
+    if world > 1:
         from multilinear_amd import dist as DS
 
         tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
         g_total = int.from_bytes(bytes(_gen(lib, log_n + log_p)), "little")
         pipe = DS.NttPipeline(log_n + log_p, g_total, tp, ops)
 
-        def ntt_once():  # x: this rank's cyclic shard of the N * 2^24 vector; the
-            pipe.submit(x)  # exchange of step i overlaps the local NTT of step i+1
+    def ntt_sharded():  # x: this rank's cyclic shard of the N * 2^24 vector; the
+        pipe.submit(x)  # exchange of step i overlaps the local NTT of step i+1
 
-        def ntt_drain():
+    ntt_once = ntt_sharded if sharded else ntt_local
+
+    def ntt_drain():
+        if sharded:
             pipe.drain()
 
     def barrier():
@@ -284,13 +294,15 @@ def main():
         "dtype": "u128 mod M (F_M, M = 2^128 - 45*2^40 + 1)",
         "data": "synthetic: seeded uniform field elements generated on device",
         "config": {
-            "workload": ("config 2: forward 2^%d-point NTT per step, natural order in/out, "
-                         "device resident" % log_n) if world == 1 else
+            "workload": ("config 2: forward 2^%d-point NTT per step per GPU, natural order "
+                         "in/out, device resident" % log_n) if not sharded else
                         ("sharded forward 2^%d-point NTT per step (2^%d per GPU): cyclic shards "
                          "in, block-cyclic out, one RCCL all-to-all" % (log_n + log_p, log_n)),
-            "log_n": log_n + log_p,
+            "log_n": log_n + (log_p if sharded else 0),
             "parallelism": "single GPU" if world == 1 else
-                           "sharded x%d (four-step NTT, all-to-all over xGMI)" % world,
+                           ("replicas x%d (independent 2^%d polynomial per GPU)" % (world, log_n)
+                            if not sharded else
+                            "sharded x%d (four-step NTT, all-to-all over xGMI)" % world),
         },
         "ntt_hbm_frac": (32.0 * N / (ms_per_step * 1e-3) / 1e9) / HBM_PEAK_GBS,
         "roofline": {
@@ -384,6 +396,12 @@ def main():
             result.update(config5(args, lib, ctx, local, world, rank, barrier))
         except Exception as e:  # keep the headline line; report the failure
             result["config5_error"] = "%s: %s" % (type(e).__name__, e)
+        if world > 1 and not sharded:
+            try:
+                result["sharded_ntt"] = sharded_ntt_extra(args, pipe, x, world, barrier, log_n,
+                                                          log_p, lib, ctx)
+            except Exception as e:
+                result["sharded_ntt_error"] = "%s: %s" % (type(e).__name__, e)
         if world > 1:
             try:
                 result.update(config4_sharded(args, local, world, rank, barrier))
@@ -403,6 +421,34 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def sharded_ntt_extra(args, pipe, x, world, barrier, log_n, log_p, lib, ctx):
+    """The all-to-all sharded NTT (north star: "the NTT shards across the GPUs
+    via an RCCL all-to-all transpose"): N*2^24 points per step, 2^24 per GPU,
+    steps streamed through dist.NttPipeline; same K / W as the headline."""
+    import torch
+
+    for _ in range(max(1, args.warmup)):
+        pipe.submit(x)
+    pipe.drain()
+    barrier()
+    lib.mlh_profile_reset(ctx)
+    lib.mlh_profile_enable(ctx, 1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.submit(x)
+    pipe.drain()
+    torch.cuda.synchronize()
+    dt = _allreduce_max(time.perf_counter() - t0)
+    lib.mlh_profile_enable(ctx, 0)
+    c, t = ctypes.c_uint64(), ctypes.c_double()
+    lib.mlh_profile_get(ctx, ("shard_dft<%d,0>" % log_p).encode(), ctypes.byref(c), ctypes.byref(t))
+    return {"metric": "sharded NTT field-elems/s", "value": (1 << (log_n + log_p)) * args.steps / dt,
+            "ms_per_step": dt / args.steps * 1e3, "log_n": log_n + log_p,
+            "scaling": "weak (2^%d per GPU)" % log_n,
+            "shard_dft_avg_ms": (t.value / c.value) if c.value else None,
+            "layout": "cyclic shards in, block-cyclic (2^%d) out" % (log_n - log_p)}
 
 
 def config4_sharded(args, local, world, rank, barrier):
