@@ -212,6 +212,32 @@ mlh_status mlh_merkle_open_pairs(mlh_ctx* ctx, const void* dev_values, uint32_t 
                                  const void* dev_tree, uint32_t levels, const uint64_t* idx,
                                  uint32_t nq, uint8_t* out);
 
+/* Device-resident Fiat-Shamir for sharded loops: the transcript state lives
+ * in a mlh_device_transcript_bytes() device buffer (same bytes as the host
+ * SHA-256 state); absorb reads from HBM and optionally writes
+ * next_challenge() (16 B) to HBM, where the *_dr steps read it. */
+uint64_t mlh_device_transcript_bytes(void);
+mlh_status mlh_transcript_to_device(mlh_ctx* ctx, const mlh_transcript* tr, void* dev_state);
+mlh_status mlh_transcript_from_device(mlh_ctx* ctx, const void* dev_state, mlh_transcript* tr);
+mlh_status mlh_device_transcript_absorb(mlh_ctx* ctx, void* dev_state, const void* dev_src,
+                                        uint32_t n, void* dev_challenge);
+/* final fold's two values: flag (u32) = not an RS code, absorb LE16(v0), last = v0 */
+mlh_status mlh_device_fri_last(mlh_ctx* ctx, const void* dev_vals2, void* dev_state,
+                               void* dev_flag, void* dev_last);
+/* mlh_shard_fri_fold(_commit) with the challenge read from HBM (dev_r, 16 B). */
+mlh_status mlh_shard_fri_fold_dr(mlh_ctx* ctx, const void* dev_layer, uint32_t log_local,
+                                 uint32_t k, uint32_t log_domain, const void* dev_r,
+                                 void* dev_next, uint32_t log_s, uint32_t log_p, uint32_t rank);
+mlh_status mlh_shard_fri_fold_commit_dr(mlh_ctx* ctx, const void* dev_layer, uint32_t log_local,
+                                        uint32_t k, uint32_t log_domain, const void* dev_r,
+                                        void* dev_next, void* dev_tree, uint32_t log_s,
+                                        uint32_t log_p, uint32_t rank);
+/* Cross-rank top of a sharded tree: dev_gathered = [P][per_rank] subtree roots
+ * (all-gathered); dev_levels receives the tree over the P*per_rank nodes in
+ * global order (t*P + h), level 0 first, root last: (2*P*per_rank - 1) x 32 B. */
+mlh_status mlh_merkle_top(mlh_ctx* ctx, const void* dev_gathered, uint32_t P, uint64_t per_rank,
+                          void* dev_levels);
+
 /* ---- batched FRI / batched PCS (src/fri/batched_fri.rs, batched_pcs.rs) ----
  * m codes (or MLEs) stored back to back on the device: item j at j * size.
  * fingerprint(r, c_0..c_{m-1}) = Horner = sum_j c_j r^(m-1-j) (batched_fri.rs:30-38). */

@@ -130,6 +130,14 @@ SIGNATURES = {
     "mlh_batched_pcs_prove": (_I, [_P, _P, _U32, _U32, _P, _P, _P,
                                    ctypes.POINTER(BatchedPcsProofC)]),
     "mlh_batched_pcs_verify": (_I, [ctypes.POINTER(BatchedPcsProofC), _U32, _P, _P, _P]),
+    "mlh_device_transcript_bytes": (_U64, []),
+    "mlh_transcript_to_device": (_I, [_P, _P, _P]),
+    "mlh_transcript_from_device": (_I, [_P, _P, _P]),
+    "mlh_device_transcript_absorb": (_I, [_P, _P, _P, _U32, _P]),
+    "mlh_device_fri_last": (_I, [_P, _P, _P, _P, _P]),
+    "mlh_shard_fri_fold_dr": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _U32, _U32, _U32]),
+    "mlh_shard_fri_fold_commit_dr": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _P, _U32, _U32, _U32]),
+    "mlh_merkle_top": (_I, [_P, _P, _U32, _U64, _P]),
     "mlh_transcript_create": (_I, [ctypes.POINTER(_P)]),
     "mlh_transcript_clone": (_I, [_P, ctypes.POINTER(_P)]),
     "mlh_transcript_destroy": (None, [_P]),

@@ -1869,3 +1869,103 @@ mlh_status mlh_batched_pcs_verify(const mlh_batched_pcs_proof* pf, uint32_t n_va
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// device-resident transcript + sharded steps that read the challenge from HBM
+// (multilinear_amd/dist.py fri_prove: no host round trip inside the fold loop)
+// ---------------------------------------------------------------------------
+extern "C" {
+
+uint64_t mlh_device_transcript_bytes(void) { return 128; }
+
+mlh_status mlh_transcript_to_device(mlh_ctx* ctx, const mlh_transcript* tr, void* dev_state) {
+  if (!ctx || !tr || !dev_state) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  std::vector<uint8_t> b(sizeof(DevSha));
+  memcpy(b.data(), &tr->sha, sizeof(DevSha));
+  HIP_TRY(ctx, hipMemcpyAsync(dev_state, b.data(), sizeof(DevSha), hipMemcpyHostToDevice,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_transcript_from_device(mlh_ctx* ctx, const void* dev_state, mlh_transcript* tr) {
+  if (!ctx || !tr || !dev_state) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, dev_state, sizeof(DevSha), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(&tr->sha, ctx->pinned, sizeof(DevSha));
+  return MLH_OK;
+}
+
+mlh_status mlh_device_transcript_absorb(mlh_ctx* ctx, void* dev_state, const void* dev_src,
+                                        uint32_t n, void* dev_challenge) {
+  if (!ctx || !dev_state || (n && !dev_src)) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  HIP_TRY(ctx, launch_transcript_absorb(reinterpret_cast<DevSha*>(dev_state),
+                                        reinterpret_cast<const uint8_t*>(dev_src), n,
+                                        reinterpret_cast<fe*>(dev_challenge), ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_device_fri_last(mlh_ctx* ctx, const void* dev_vals2, void* dev_state,
+                               void* dev_flag, void* dev_last) {
+  if (!ctx || !dev_vals2 || !dev_state || !dev_flag || !dev_last)
+    return fail(ctx, MLH_ERR_INVALID, "null argument");
+  HIP_TRY(ctx, launch_fri_last(reinterpret_cast<const fe*>(dev_vals2),
+                               reinterpret_cast<DevSha*>(dev_state),
+                               reinterpret_cast<uint32_t*>(dev_flag),
+                               reinterpret_cast<fe*>(dev_last), ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_shard_fri_fold_dr(mlh_ctx* ctx, const void* dev_layer, uint32_t log_local,
+                                 uint32_t k, uint32_t log_domain, const void* dev_r,
+                                 void* dev_next, uint32_t log_s, uint32_t log_p, uint32_t rank) {
+  ShardMap m;
+  const uint8_t dummy[16] = {0};
+  MLH_TRY(shard_fold_args(ctx, dev_layer, dev_next, dummy, log_local, k, log_domain, log_s, log_p,
+                          rank, &m));
+  if (!dev_r) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  const fe *tlo, *thi;
+  MLH_TRY(fold_tables(ctx, log_domain, &tlo, &thi));
+  HIP_TRY(ctx, launch_fri_fold(reinterpret_cast<const fe*>(dev_layer), 1ull << log_local,
+                               reinterpret_cast<fe*>(dev_next), fe{}, tlo, thi, k,
+                               1ull << log_domain, ctx->stream, m,
+                               reinterpret_cast<const fe*>(dev_r)));
+  return MLH_OK;
+}
+
+mlh_status mlh_shard_fri_fold_commit_dr(mlh_ctx* ctx, const void* dev_layer, uint32_t log_local,
+                                        uint32_t k, uint32_t log_domain, const void* dev_r,
+                                        void* dev_next, void* dev_tree, uint32_t log_s,
+                                        uint32_t log_p, uint32_t rank) {
+  ShardMap m;
+  const uint8_t dummy[16] = {0};
+  MLH_TRY(shard_fold_args(ctx, dev_layer, dev_next, dummy, log_local, k, log_domain, log_s, log_p,
+                          rank, &m));
+  if (!dev_tree || !dev_r) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_local < 2 || (log_p && log_s + 2 > log_local))
+    return fail(ctx, MLH_ERR_INVALID, "folded layer's pairs are not local");
+  const fe *tlo, *thi;
+  MLH_TRY(fold_tables(ctx, log_domain, &tlo, &thi));
+  uint8_t* tree = reinterpret_cast<uint8_t*>(dev_tree);
+  HIP_TRY(ctx, launch_fri_fold_leaves(reinterpret_cast<const fe*>(dev_layer), 1ull << log_local,
+                                      reinterpret_cast<fe*>(dev_next), tree, fe{}, tlo, thi, k,
+                                      1ull << log_domain, ctx->stream, m,
+                                      reinterpret_cast<const fe*>(dev_r)));
+  HIP_TRY(ctx, launch_merkle_levels(tree, 1ull << (log_local - 2), ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_merkle_top(mlh_ctx* ctx, const void* dev_gathered, uint32_t P, uint64_t per_rank,
+                          void* dev_levels) {
+  if (!ctx || !dev_gathered || !dev_levels) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  const uint64_t n = (uint64_t)P * per_rank;
+  if (!is_pow2(n)) return fail(ctx, MLH_ERR_NOT_POW2, "top tree size must be a power of two");
+  uint8_t* lv = reinterpret_cast<uint8_t*>(dev_levels);
+  HIP_TRY(ctx, launch_top_reorder(reinterpret_cast<const uint8_t*>(dev_gathered), P, per_rank, lv,
+                                  ctx->stream));
+  HIP_TRY(ctx, launch_merkle_levels(lv, n, ctx->stream));
+  return MLH_OK;
+}
+
+}  // extern "C"

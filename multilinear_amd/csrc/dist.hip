@@ -131,3 +131,28 @@ hipError_t launch_open_pairs(const fe* values, uint64_t half, const uint8_t* tre
 }
 
 }  // namespace mlh
+
+namespace mlh {
+
+// level-0 of the cross-rank top tree: gathered[h][t] (P ranks x per-rank
+// subtree roots) -> out[t * P + h], the global order of the level-log_s nodes.
+__global__ void top_reorder_kernel(const uint8_t* __restrict__ gathered, uint32_t P,
+                                   uint64_t per_rank, uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P * per_rank) return;
+  const uint64_t t = i / P, h = i % P;
+  const uint4* src = reinterpret_cast<const uint4*>(gathered + (h * per_rank + t) * 32);
+  uint4* dst = reinterpret_cast<uint4*>(out + i * 32);
+  dst[0] = src[0];
+  dst[1] = src[1];
+}
+
+hipError_t launch_top_reorder(const uint8_t* gathered, uint32_t P, uint64_t per_rank,
+                              uint8_t* out, hipStream_t st) {
+  const uint64_t n = P * per_rank;
+  hipLaunchKernelGGL(top_reorder_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     gathered, P, per_rank, out);
+  return hipGetLastError();
+}
+
+}  // namespace mlh

@@ -21,4 +21,8 @@ hipError_t launch_open_pairs(const fe* values, uint64_t half, const uint8_t* tre
                              uint32_t levels, const uint64_t* idx, uint32_t nq, uint8_t* out,
                              hipStream_t st);
 
+// gathered [P][per_rank] digests -> out [per_rank][P] (global node order)
+hipError_t launch_top_reorder(const uint8_t* gathered, uint32_t P, uint64_t per_rank,
+                              uint8_t* out, hipStream_t st);
+
 }  // namespace mlh

@@ -179,6 +179,66 @@ class HipOps:
                                               rank), c)
         return out, tree
 
+    # -- device-resident transcript and roots --
+    def dev_transcript(self, transcript):
+        import torch
+
+        st = torch.empty(int(lib().mlh_device_transcript_bytes()), dtype=torch.uint8,
+                         device="cuda:%d" % self.device)
+        c = self._ctx()
+        check(lib().mlh_transcript_to_device(c, transcript.h, ptr(st)), c)
+        return st
+
+    def absorb(self, state, src, challenge_out=None):
+        """absorb the bytes of device tensor ``src``; next_challenge() -> challenge_out."""
+        c = self._ctx()
+        check(lib().mlh_device_transcript_absorb(
+            c, ptr(state), ptr(src), src.numel() * src.element_size(),
+            ptr(challenge_out) if challenge_out is not None else None), c)
+
+    def fri_last(self, vals2, state, flag_out, last_out):
+        c = self._ctx()
+        check(lib().mlh_device_fri_last(c, ptr(vals2), ptr(state), ptr(flag_out), ptr(last_out)), c)
+
+    def fold_dr(self, values, k, log_domain, r_dev, log_s, log_p, rank):
+        c = self._ctx()
+        n = values.shape[0]
+        out = self.empty(n // 2)
+        check(lib().mlh_shard_fri_fold_dr(c, ptr(values), _log2(n), k, log_domain, ptr(r_dev),
+                                          ptr(out), log_s, log_p, rank), c)
+        return out
+
+    def fold_commit_dr(self, values, k, log_domain, r_dev, log_s, log_p, rank):
+        c = self._ctx()
+        n = values.shape[0]
+        out = self.empty(n // 2)
+        tree = self.empty_tree(n // 4)
+        check(lib().mlh_shard_fri_fold_commit_dr(c, ptr(values), _log2(n), k, log_domain,
+                                                 ptr(r_dev), ptr(out), ptr(tree), log_s, log_p,
+                                                 rank), c)
+        return out, tree
+
+    def merkle_top(self, gathered, P, per_rank):
+        c = self._ctx()
+        levels = self.empty_tree(P * per_rank)
+        check(lib().mlh_merkle_top(c, ptr(gathered), P, per_rank, ptr(levels)), c)
+        return levels
+
+    @staticmethod
+    def tree_root(tree):
+        return tree[-32:]
+
+    @staticmethod
+    def tree_level_dev(tree, leaves, level):
+        off = sum(leaves >> i for i in range(level))
+        return tree[32 * off:32 * (off + (leaves >> level))]
+
+    @staticmethod
+    def concat_bytes(parts):
+        import torch
+
+        return torch.cat(parts).cpu().numpy().tobytes()
+
     def tree_level(self, tree, leaves, level):
         """Digests of one level of a flattened tree (leaves first) -> bytes."""
         off = sum(leaves >> i for i in range(level))
@@ -377,30 +437,46 @@ class _Layer:
         self.log_n, self.log_p, self.log_s, self.rank = log_n, log_p, log_s, rank
         # tree levels held locally (siblings below this come from HBM)
         self.sub_levels = log_s if log_p else log_n - 1
-        self.top = []  # host levels sub_levels .. root (lists of digests)
+        self.top_dev = None  # device tree over the all-gathered level-log_s nodes
+        self.root_dev = None  # 32-byte device view of the root
+        self.top = []  # host copy of top_dev's levels (query phase)
 
     @property
     def local_leaves(self):
         return 1 << (self.log_n - 1 - self.log_p)
 
-    def root(self):
-        return self.top[-1][0]
-
 
 def _commit_top(layer, tp, ops):
-    """Combine the level-log_s subtree roots of all ranks; hash to the root."""
-    nodes_local = ops.tree_level(layer.tree, layer.local_leaves, layer.sub_levels)
+    """Root of the layer's tree, on the device: a replicated layer's own root;
+    a sharded layer all-gathers its level-log_s subtree roots (T/2 per rank)
+    and hashes the top levels (mlh_merkle_top).  No host round trip."""
     if layer.log_p == 0:
-        layer.top = [[nodes_local[i:i + 32] for i in range(0, len(nodes_local), 32)]]
+        layer.root_dev = ops.tree_root(layer.tree)
         return
-    per_rank = tp.gather_bytes(nodes_local)
-    P, half_t = tp.world, len(nodes_local) // 32
-    level = [per_rank[h][32 * t:32 * t + 32] for t in range(half_t) for h in range(P)]
-    top = [level]
-    while len(top[-1]) > 1:
-        cur = top[-1]
-        top.append([_hash_node(cur[2 * i], cur[2 * i + 1]) for i in range(len(cur) // 2)])
-    layer.top = top
+    half_t = layer.local_leaves >> layer.sub_levels
+    nodes = ops.tree_level_dev(layer.tree, layer.local_leaves, layer.sub_levels)
+    gathered = tp.all_gather(nodes)
+    layer.top_dev = ops.merkle_top(gathered, tp.world, half_t)
+    layer.root_dev = ops.tree_root(layer.top_dev)
+
+
+def _host_top(layer):
+    """Host levels of a sharded layer's top tree (for the query phase)."""
+    if layer.top_dev is None:
+        return
+    raw = ops_bytes(layer.top_dev)
+    n = len(raw) // 32
+    leaves = (n + 1) // 2
+    levels, off = [], 0
+    while leaves >= 1:
+        levels.append([raw[32 * (off + i):32 * (off + i + 1)] for i in range(leaves)])
+        off += leaves
+        leaves //= 2
+    layer.top = levels
+
+
+def ops_bytes(t):
+    return t.cpu().contiguous().numpy().tobytes()
 
 
 def _open(layer, idx, tp, ops):
@@ -436,6 +512,12 @@ def fri_prove(code_local, log_code, transcript, tp, ops, gather_log=16):
     """FriProof::prove (fri/mod.rs:261-285) of a 2^log_code codeword held in
     the block-(2^log_code / P^2) layout (``reed_solomon``'s output).
 
+    The commit loop is device resident on every rank: the transcript state is
+    replicated in HBM (mlh_transcript_to_device), each layer's root is built
+    on the device (local subtrees, an all-gather of the subtree roots, the
+    top levels) and absorbed by a device kernel that writes the next
+    challenge to HBM, where the next fold reads it.  The host waits once,
+    replays the absorbs into ``transcript`` and runs the query phase.
     Every rank returns the same proof; it equals the single-GPU proof of the
     natural-order codeword byte for byte."""
     from .fri import FriProof
@@ -448,6 +530,10 @@ def fri_prove(code_local, log_code, transcript, tp, ops, gather_log=16):
         raise ValueError("codeword too small for the world size")
     gather_log = max(gather_log, 2 * log_p + 2)
     n0 = log_code
+    steps = log_code - LOG_BLOWUP
+    state = ops.dev_transcript(transcript)
+    rbuf = ops.empty(steps + 1)
+    lastbuf, flagbuf = ops.empty(1), ops.empty(1)
     if log_p and log_code > gather_log:
         lay = _Layer(code_local, None, log_code, log_p, cross_log_s(log_code, log_p), rank)
     else:
@@ -458,30 +544,27 @@ def fri_prove(code_local, log_code, transcript, tp, ops, gather_log=16):
     lay.tree = ops.commit_pairs(lay.values)
     _commit_top(lay, tp, ops)
     layers = [lay]
-    transcript.absorb(lay.root())
-    last = None
-    for k in range(log_code - LOG_BLOWUP):
+    ops.absorb(state, lay.root_dev, rbuf[0])
+    done = False
+    for k in range(steps):
         cur = layers[-1]
         if (1 << cur.log_n) <= (1 << LOG_BLOWUP):
             break
-        r = transcript.next_challenge()
+        r = rbuf[k]
         log_next = cur.log_n - 1
         if (1 << log_next) == (1 << LOG_BLOWUP):  # fri/mod.rs:116-126
-            nx = ops.fold(cur.values, k, n0, r, 40, 0, 0)
-            vals = ops.to_host(nx)
-            if not (vals[0] == vals[1]).all():
-                raise _lib.MlhError(_lib.MLH_ERR_NOT_RS_CODE, "not an RS code")
-            last = vals[0].tobytes()
-            transcript.absorb(last)
+            nx = ops.fold_dr(cur.values, k, n0, r, 40, 0, 0)
+            ops.fri_last(nx, state, flagbuf, lastbuf)
+            done = True
             break
         if cur.log_p == 0:
-            nv, tree = ops.fold_commit(cur.values, k, n0, r, 40, 0, 0)
+            nv, tree = ops.fold_commit_dr(cur.values, k, n0, r, 40, 0, 0)
             lay = _Layer(nv, tree, log_next, 0, 0, rank)
         elif log_next - cur.log_p - cur.log_s >= 1:  # >= 2 local blocks: pairs local
-            nv, tree = ops.fold_commit(cur.values, k, n0, r, cur.log_s, cur.log_p, rank)
+            nv, tree = ops.fold_commit_dr(cur.values, k, n0, r, cur.log_s, cur.log_p, rank)
             lay = _Layer(nv, tree, log_next, cur.log_p, cur.log_s, rank)
         else:  # folded layer is in natural block order: re-deal or gather
-            nv = ops.fold(cur.values, k, n0, r, cur.log_s, cur.log_p, rank)
+            nv = ops.fold_dr(cur.values, k, n0, r, cur.log_s, cur.log_p, rank)
             if log_next > gather_log:
                 nv = tp.all_to_all(nv)
                 lay = _Layer(nv, None, log_next, log_p, cross_log_s(log_next, log_p), rank)
@@ -491,9 +574,20 @@ def fri_prove(code_local, log_code, transcript, tp, ops, gather_log=16):
             lay.tree = ops.commit_pairs(lay.values)
         _commit_top(lay, tp, ops)
         layers.append(lay)
-        transcript.absorb(lay.root())
-    if last is None:
+        ops.absorb(state, lay.root_dev, rbuf[k + 1])
+    if not done:
         raise _lib.MlhError(_lib.MLH_ERR_INVALID, "fold produced no last element")
+
+    # one wait: roots, last element, RS flag; the host transcript replays them
+    roots = ops.concat_bytes([l.root_dev for l in layers])
+    last = ops_bytes(lastbuf)[:16]
+    if int.from_bytes(ops_bytes(flagbuf)[:4], "little"):
+        raise _lib.MlhError(_lib.MLH_ERR_NOT_RS_CODE, "not an RS code")
+    for t in range(len(layers)):
+        transcript.absorb(roots[32 * t:32 * t + 32])
+    transcript.absorb(last)
+    for l in layers:
+        _host_top(l)
 
     idx = []
     for _ in range(NUM_QUERIES):  # fri/mod.rs:266-277
@@ -516,7 +610,7 @@ def fri_prove(code_local, log_code, transcript, tp, ops, gather_log=16):
     proof.c.log_code = log_code
     proof.c.num_trees = len(layers)
     proof.c.num_queries = NUM_QUERIES
-    ctypes.memmove(proof._commit, b"".join(l.root() for l in layers), 32 * len(layers))
+    ctypes.memmove(proof._commit, roots, 32 * len(layers))
     ctypes.memmove(proof._q, qraw, len(qraw))
     for q, i in enumerate(idx):
         proof._idx[q] = i

@@ -101,6 +101,44 @@ class CpuOps(D.HipOps):
     def to_host(self, values):
         return _limbs(values)
 
+    # -- device-resident transcript stand-ins (state = a host Transcript) ------
+    def dev_transcript(self, transcript):
+        return transcript.clone()
+
+    def absorb(self, state, src, challenge_out=None):
+        state.absorb(src.contiguous().numpy().tobytes())
+        if challenge_out is not None:
+            challenge_out[:] = _tensor([state.next_challenge()])[0]
+
+    def fri_last(self, vals2, state, flag_out, last_out):
+        v = _limbs(vals2)
+        flag_out[:] = 0
+        flag_out[0, 0] = 0 if (v[0] == v[1]).all() else 1
+        last_out[:] = vals2[0]
+        state.absorb(v[0].tobytes())
+
+    @staticmethod
+    def _r(r_dev):
+        return _ints(r_dev.reshape(1, 4))[0]
+
+    def fold_dr(self, values, k, log_domain, r_dev, log_s, log_p, rank):
+        return self.fold(values, k, log_domain, self._r(r_dev), log_s, log_p, rank)
+
+    def fold_commit_dr(self, values, k, log_domain, r_dev, log_s, log_p, rank):
+        return self.fold_commit(values, k, log_domain, self._r(r_dev), log_s, log_p, rank)
+
+    def merkle_top(self, gathered, P, per_rank):
+        import hashlib
+
+        g = gathered.numpy().tobytes()
+        lvl = [g[32 * (h * per_rank + t):32 * (h * per_rank + t + 1)]
+               for t in range(per_rank) for h in range(P)]
+        out = list(lvl)
+        while len(lvl) > 1:
+            lvl = [hashlib.sha256(lvl[2 * i] + lvl[2 * i + 1]).digest() for i in range(len(lvl) // 2)]
+            out += lvl
+        return torch.frombuffer(bytearray(b"".join(out)), dtype=torch.uint8)
+
     # -- sumcheck: oracle formulas, tables mutated in place ---------------------
     def eq_table(self, points):
         from oracle import sumcheck as OS
