@@ -238,6 +238,20 @@ mlh_status mlh_shard_fri_fold_commit_dr(mlh_ctx* ctx, const void* dev_layer, uin
 mlh_status mlh_merkle_top(mlh_ctx* ctx, const void* dev_gathered, uint32_t P, uint64_t per_rank,
                           void* dev_levels);
 
+/* Device-resident sumcheck steps: round sums written to HBM (2 x 16 B), the
+ * challenge read from HBM; mlh_device_sumcheck_round adds npairs (s1, s2)
+ * pairs (e.g. one per rank, all-gathered), interpolates, absorbs (c1, c2)
+ * into the device transcript, writes c1 c2 and r, and updates the claim. */
+mlh_status mlh_sumcheck_sums_dev(mlh_ctx* ctx, const void* dev_matrix, const void* dev_delta,
+                                 uint32_t log_height, void* dev_sums);
+mlh_status mlh_sumcheck_fold_sums_dr(mlh_ctx* ctx, void* dev_matrix, void* dev_delta,
+                                     uint32_t log_height, const void* dev_r, void* dev_sums);
+mlh_status mlh_sumcheck_fold_dr(mlh_ctx* ctx, void* dev_matrix, void* dev_delta,
+                                uint32_t log_height, const void* dev_r);
+mlh_status mlh_device_sumcheck_round(mlh_ctx* ctx, const void* dev_sum_pairs, uint32_t npairs,
+                                     void* dev_prev, void* dev_state, void* dev_poly_out,
+                                     void* dev_r_out);
+
 /* ---- batched FRI / batched PCS (src/fri/batched_fri.rs, batched_pcs.rs) ----
  * m codes (or MLEs) stored back to back on the device: item j at j * size.
  * fingerprint(r, c_0..c_{m-1}) = Horner = sum_j c_j r^(m-1-j) (batched_fri.rs:30-38). */

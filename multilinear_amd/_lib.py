@@ -138,6 +138,10 @@ SIGNATURES = {
     "mlh_shard_fri_fold_dr": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _U32, _U32, _U32]),
     "mlh_shard_fri_fold_commit_dr": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _P, _U32, _U32, _U32]),
     "mlh_merkle_top": (_I, [_P, _P, _U32, _U64, _P]),
+    "mlh_sumcheck_sums_dev": (_I, [_P, _P, _P, _U32, _P]),
+    "mlh_sumcheck_fold_sums_dr": (_I, [_P, _P, _P, _U32, _P, _P]),
+    "mlh_sumcheck_fold_dr": (_I, [_P, _P, _P, _U32, _P]),
+    "mlh_device_sumcheck_round": (_I, [_P, _P, _U32, _P, _P, _P, _P]),
     "mlh_transcript_create": (_I, [ctypes.POINTER(_P)]),
     "mlh_transcript_clone": (_I, [_P, ctypes.POINTER(_P)]),
     "mlh_transcript_destroy": (None, [_P]),

@@ -1969,3 +1969,56 @@ mlh_status mlh_merkle_top(mlh_ctx* ctx, const void* dev_gathered, uint32_t P, ui
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// device-resident sumcheck steps (sharded sumcheck in multilinear_amd/dist.py)
+// ---------------------------------------------------------------------------
+extern "C" {
+
+mlh_status mlh_sumcheck_sums_dev(mlh_ctx* ctx, const void* dev_matrix, const void* dev_delta,
+                                 uint32_t log_height, void* dev_sums) {
+  if (!ctx || !dev_matrix || !dev_delta || !dev_sums || log_height < 1 || log_height > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  HIP_TRY(ctx, launch_sums(reinterpret_cast<const fe*>(dev_matrix),
+                           reinterpret_cast<const fe*>(dev_delta), 1ull << (log_height - 1),
+                           ctx->partials, reinterpret_cast<fe*>(dev_sums), ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_sumcheck_fold_sums_dr(mlh_ctx* ctx, void* dev_matrix, void* dev_delta,
+                                     uint32_t log_height, const void* dev_r, void* dev_sums) {
+  if (!ctx || !dev_matrix || !dev_delta || !dev_r || !dev_sums || log_height < 2 ||
+      log_height > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  HIP_TRY(ctx, launch_fold_sums(reinterpret_cast<fe*>(dev_matrix), reinterpret_cast<fe*>(dev_delta),
+                                1ull << log_height, fe{}, ctx->partials,
+                                reinterpret_cast<fe*>(dev_sums), ctx->stream,
+                                reinterpret_cast<const fe*>(dev_r)));
+  return MLH_OK;
+}
+
+mlh_status mlh_sumcheck_fold_dr(mlh_ctx* ctx, void* dev_matrix, void* dev_delta,
+                                uint32_t log_height, const void* dev_r) {
+  if (!ctx || !dev_matrix || !dev_delta || !dev_r || log_height < 1 || log_height > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  HIP_TRY(ctx, launch_fold(reinterpret_cast<fe*>(dev_matrix), reinterpret_cast<fe*>(dev_delta),
+                           1ull << log_height, fe{}, ctx->stream,
+                           reinterpret_cast<const fe*>(dev_r)));
+  return MLH_OK;
+}
+
+mlh_status mlh_device_sumcheck_round(mlh_ctx* ctx, const void* dev_sum_pairs, uint32_t npairs,
+                                     void* dev_prev, void* dev_state, void* dev_poly_out,
+                                     void* dev_r_out) {
+  if (!ctx || !dev_sum_pairs || !dev_prev || !dev_state || !dev_poly_out || !dev_r_out ||
+      npairs == 0)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  HIP_TRY(ctx, launch_sumcheck_round(reinterpret_cast<const fe*>(dev_sum_pairs), npairs,
+                                     reinterpret_cast<fe*>(dev_prev),
+                                     reinterpret_cast<DevSha*>(dev_state),
+                                     reinterpret_cast<fe*>(dev_poly_out),
+                                     reinterpret_cast<fe*>(dev_r_out), ctx->stream));
+  return MLH_OK;
+}
+
+}  // extern "C"

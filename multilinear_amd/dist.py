@@ -275,6 +275,28 @@ class HipOps:
         b = bytes(raw)
         return int.from_bytes(b[:16], "little"), int.from_bytes(b[16:], "little")
 
+    def const(self, v):
+        from .device import ints_to_limbs, to_device
+
+        return to_device(ints_to_limbs([v]), self.device)
+
+    def sc_sums_dev(self, m, d, log_h, out):
+        c = self._ctx()
+        check(lib().mlh_sumcheck_sums_dev(c, ptr(m), ptr(d), log_h, ptr(out)), c)
+
+    def sc_fold_sums_dr(self, m, d, log_h, r_dev, out):
+        c = self._ctx()
+        check(lib().mlh_sumcheck_fold_sums_dr(c, ptr(m), ptr(d), log_h, ptr(r_dev), ptr(out)), c)
+
+    def sc_fold_dr(self, m, d, log_h, r_dev):
+        c = self._ctx()
+        check(lib().mlh_sumcheck_fold_dr(c, ptr(m), ptr(d), log_h, ptr(r_dev)), c)
+
+    def sc_round(self, pairs, npairs, prev, state, poly_out, r_out):
+        c = self._ctx()
+        check(lib().mlh_device_sumcheck_round(c, ptr(pairs), npairs, ptr(prev), ptr(state),
+                                              ptr(poly_out), ptr(r_out)), c)
+
     def sc_sums(self, m, d):
         ctx = self._ctx()
         out = (ctypes.c_uint8 * 32)()
@@ -651,64 +673,49 @@ def eq_table(points, tp, ops):
     return ops.scale(local, c) if c != 1 else local
 
 
-def _fold_pairs(parts):
-    s1 = s2 = 0
-    for raw in parts:
-        s1 = (s1 + int.from_bytes(raw[:16], "little")) % M
-        s2 = (s2 + int.from_bytes(raw[16:], "little")) % M
-    return s1, s2
-
-
-def _combine(sums, tp):
-    if tp.world == 1:
-        return sums
-    raw = sums[0].to_bytes(16, "little") + sums[1].to_bytes(16, "little")
-    return _fold_pairs(tp.gather_bytes(raw))
-
-
-def _round(s1, s2, prev, transcript):
-    """compute_sumcheck_polynomial (sumcheck.rs:174-202): p(0) = prev - p(1),
-    closed-form interpolation on x = 0, 1, 2, absorb c1, c2, r, p(r)."""
-    e0 = (prev - s1) % M
-    c2 = (s2 - 2 * s1 + e0) * pow(2, M - 2, M) % M
-    c1 = (s1 - e0 - c2) % M
-    transcript.absorb(c1.to_bytes(16, "little"))
-    transcript.absorb(c2.to_bytes(16, "little"))
-    r = transcript.next_challenge()
-    return c1, c2, r, (e0 + r * (c1 + c2 * r)) % M
-
-
 def sumcheck_prove(m, d, n, total_sum, transcript, tp, ops):
     """SumcheckTables::compute_sumcheck_polynomials (sumcheck.rs:77-102) for
     the PCS composition x[0], tables of 2^n entries in the cyclic layout
     (``m``, ``d`` local, folded in place).  The MSB-first fold pairs (i, i+h)
     share their low bits, so they stay on one rank while the local table has
-    >= 2 entries; round sums are all-gathered (2 x 16 B per rank) and added
-    mod M; the last p rounds run replicated on the gathered P-entry tables.
+    >= 2 entries; each round all-gathers the ranks' (s1, s2) sums straight
+    from HBM and a device kernel adds them, interpolates, absorbs (c1, c2)
+    into the replicated device transcript and writes r to HBM for the folds;
+    the last p rounds run replicated on the gathered P-entry tables.  The host
+    waits once and replays the absorbs into ``transcript``.
     Returns ([(c1, c2)], [r]) -- identical to the single-GPU prover."""
     P = tp.world
     p = _log2(P)
     sharded = P > 1
     log_local = n - p
+    state = ops.dev_transcript(transcript)
+    prev = ops.const(total_sum % M)
+    polys = ops.empty(2 * n)
+    rs = ops.empty(n)
+    sums = ops.empty(2)
     if sharded and log_local == 0:
         m, d, sharded, log_local = tp.all_gather(m), tp.all_gather(d), False, n
-    s1, s2 = _combine(ops.sc_sums(m, d), tp) if sharded else ops.sc_sums(m, d)
-    prev = total_sum
-    polys, rs = [], []
+    ops.sc_sums_dev(m, d, log_local, sums)
     for k in range(n):
-        c1, c2, r, prev = _round(s1, s2, prev, transcript)
-        polys.append((c1, c2))
-        rs.append(r)
+        pairs = tp.all_gather(sums) if sharded else sums
+        ops.sc_round(pairs, P if sharded else 1, prev, state, polys[2 * k:2 * k + 2], rs[k])
         if k + 1 == n:
-            ops.sc_fold(m, d, log_local, r)
+            ops.sc_fold_dr(m, d, log_local, rs[k])
             break
         if log_local >= 2:
-            sums = ops.sc_fold_and_sums(m, d, log_local, r)
+            ops.sc_fold_sums_dr(m, d, log_local, rs[k], sums)
             log_local -= 1
-            s1, s2 = _combine(sums, tp) if sharded else sums
         else:  # sharded, local 2 -> 1: gather the P-entry tables, go replicated
-            ops.sc_fold(m, d, log_local, r)
+            ops.sc_fold_dr(m, d, log_local, rs[k])
             m, d = tp.all_gather(m[:1]), tp.all_gather(d[:1])
             sharded, log_local = False, p
-            s1, s2 = ops.sc_sums(m, d)
-    return polys, rs
+            ops.sc_sums_dev(m, d, log_local, sums)
+    raw_p, raw_r = ops_bytes(polys), ops_bytes(rs)
+    out_p, out_r = [], []
+    for k in range(n):
+        c1, c2 = raw_p[32 * k:32 * k + 16], raw_p[32 * k + 16:32 * k + 32]
+        transcript.absorb(c1)
+        transcript.absorb(c2)
+        out_p.append((int.from_bytes(c1, "little"), int.from_bytes(c2, "little")))
+        out_r.append(int.from_bytes(raw_r[16 * k:16 * k + 16], "little"))
+    return out_p, out_r

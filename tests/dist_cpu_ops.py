@@ -165,6 +165,32 @@ class CpuOps(D.HipOps):
             folded = [(v[i] + r * (v[i + h] - v[i])) % F.M for i in range(h)]
             t[:h] = _tensor(folded)
 
+    def const(self, v):
+        return _tensor([v])
+
+    def sc_sums_dev(self, m, d, log_h, out):
+        out[:] = _tensor(list(self._sums(_ints(m[:1 << log_h]), _ints(d[:1 << log_h]))))
+
+    def sc_fold_sums_dr(self, m, d, log_h, r_dev, out):
+        out[:] = _tensor(list(self.sc_fold_and_sums(m, d, log_h, self._r(r_dev))))
+
+    def sc_fold_dr(self, m, d, log_h, r_dev):
+        self.sc_fold(m, d, log_h, self._r(r_dev))
+
+    def sc_round(self, pairs, npairs, prev, state, poly_out, r_out):
+        v = _ints(pairs)
+        s1 = sum(v[0::2]) % F.M
+        s2 = sum(v[1::2]) % F.M
+        e0 = (_ints(prev)[0] - s1) % F.M
+        c2 = (s2 - 2 * s1 + e0) * INV2 % F.M
+        c1 = (s1 - e0 - c2) % F.M
+        poly_out[:] = _tensor([c1, c2])
+        state.absorb(F.to_bytes(c1))
+        state.absorb(F.to_bytes(c2))
+        r = state.next_challenge()
+        r_out[:] = _tensor([r])[0]
+        prev[:] = _tensor([(e0 + r * (c1 + c2 * r)) % F.M])
+
     def sc_fold_and_sums(self, m, d, log_h, r):
         self.sc_fold(m, d, log_h, r)
         h = 1 << (log_h - 1)
