@@ -473,6 +473,22 @@ def config4_sharded(args, local, world, rank, barrier):
         d = DS.eq_table(pts, tp, ops)
         return DS.sumcheck_prove(m, d, n, 0, Transcript(), tp, ops)
 
+    # config 3 sharded: RS LDE of 2^n coefficients + Merkle root over the ranks
+    coeffs = D.random_device(1 << (n - tp.world.bit_length() + 1), 700 + rank, local)
+    g2 = int.from_bytes(bytes(_gen(D.lib(), n + 1)), "little")
+
+    def commit():
+        code = DS.reed_solomon(coeffs, n, g2, tp, ops)
+        return DS.commit_rs_code(code, n + 1, tp, ops)
+
+    commit()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(max(1, min(args.extra_reps, 3))):
+        commit()
+    torch.cuda.synchronize()
+    commit_ms = _allreduce_max((time.perf_counter() - t0) / max(1, min(args.extra_reps, 3))) * 1e3
+
     run()
     barrier()
     reps = max(1, min(args.extra_reps, 3))
@@ -484,6 +500,7 @@ def config4_sharded(args, local, world, rank, barrier):
     import torch.distributed as tdist
 
     return {"config4_sharded_eq_sumcheck_ms": _allreduce_max(dt) * 1e3,
+            "config3_sharded_fri_commit_ms": commit_ms,
             "config4_layout": "sharded x%d (cyclic by low index bits)" % world}
 
 

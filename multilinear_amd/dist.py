@@ -530,6 +530,22 @@ def _open(layer, idx, tp, ops):
     return [o if o is not None else bytes(rec_len) for o in out]
 
 
+def commit_rs_code(code_local, log_code, tp, ops):
+    """commit_rs_code + Merkle::commit (fri/mod.rs:45-55, merkle_tree/mod.rs:
+    65-85) of a 2^log_code codeword in the block-(2^log_code / P^2) layout:
+    local leaves and subtrees, one all-gather of the subtree roots, the top
+    levels on the device.  Returns the root (32 bytes, host)."""
+    P = tp.world
+    log_p = _log2(P)
+    if log_p:
+        lay = _Layer(code_local, None, log_code, log_p, cross_log_s(log_code, log_p), tp.rank)
+    else:
+        lay = _Layer(code_local, None, log_code, 0, 0, tp.rank)
+    lay.tree = ops.commit_pairs(lay.values)
+    _commit_top(lay, tp, ops)
+    return ops.concat_bytes([lay.root_dev])
+
+
 def fri_prove(code_local, log_code, transcript, tp, ops, gather_log=16):
     """FriProof::prove (fri/mod.rs:261-285) of a 2^log_code codeword held in
     the block-(2^log_code / P^2) layout (``reed_solomon``'s output).

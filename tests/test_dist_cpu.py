@@ -186,3 +186,51 @@ def test_sharded_sumcheck_matches_oracle(world, n):
         assert [tuple(p) for p in r[1]] == polys, "rank %d polys" % r[0]
         assert r[2] == rs
         assert r[3] == tr.random()
+
+
+def _commit_worker(rank, world, port, log_c, q):
+    import torch
+    import torch.distributed as tdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from multilinear_amd import dist as D
+        from oracle import coracle as C
+        from oracle import field as F
+        from tests.dist_cpu_ops import CpuOps
+
+        tp, ops = D.Transport(), CpuOps()
+        rng = np.random.default_rng(9)
+        code = rng.integers(0, 2**32, size=(1 << log_c, 4), dtype=np.uint64).astype(np.uint32)
+        code[:, 3] = np.minimum(code[:, 3], 0xFFFFFFFE)
+        log_s = D.cross_log_s(log_c, world.bit_length() - 1)
+        local = torch.from_numpy(D.shard_blocks(code, world, rank, log_s).view(np.int32))
+        root = D.commit_rs_code(local, log_c, tp, ops)
+        want = bytes(C.merkle_commit_pairs(code, log_c)[-1])
+        q.put((rank, root == want, None))
+    except Exception:
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc()))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,log_c", [(2, 8), (4, 10), (8, 9)])
+def test_sharded_merkle_commit_root(world, log_c):
+    """dist.commit_rs_code (local subtrees + all-gathered roots + top) == the
+    single Merkle root of the natural-order code (merkle_tree/mod.rs:65-85)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_commit_worker, args=(r, world, port, log_c, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] is True, r
