@@ -102,6 +102,11 @@ mlh_status mlh_ntt_host(mlh_ctx* ctx, const uint8_t* host_in, uint8_t* host_out,
  * NTT with gen (order 2^(log_n+1)).  dev_code holds 2^(log_n+1) elements. */
 mlh_status mlh_reed_solomon(mlh_ctx* ctx, const void* dev_coeffs, uint32_t log_n,
                             const uint8_t gen[16], void* dev_code);
+/* reed_solomon(bit_reverse_permutation(coeffs)) in one transform: the commit
+ * step of multilinear_pcs.rs:104-107 / batched_pcs.rs:146-147 with the
+ * permutation folded into the first pass's loads (out of place). */
+mlh_status mlh_reed_solomon_brev(mlh_ctx* ctx, const void* dev_coeffs, uint32_t log_n,
+                                 const uint8_t gen[16], void* dev_code);
 /* Bytes of a flattened tree with `leaves` leaves: (2*leaves - 1) * 32. */
 uint64_t mlh_merkle_layers_bytes(uint64_t leaves);
 /* commit_rs_code (fri/mod.rs:45-55) + Merkle::commit (merkle_tree/mod.rs:65-85):

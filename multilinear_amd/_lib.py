@@ -99,6 +99,7 @@ SIGNATURES = {
     "mlh_bit_reverse_permutation": (_I, [_P, _P, _P, _U32]),
     "mlh_ntt_host": (_I, [_P, _P, _P, _U32, _P, _I]),
     "mlh_reed_solomon": (_I, [_P, _P, _U32, _P, _P]),
+    "mlh_reed_solomon_brev": (_I, [_P, _P, _U32, _P, _P]),
     "mlh_merkle_layers_bytes": (_U64, [_U64]),
     "mlh_merkle_commit_pairs": (_I, [_P, _P, _U32, _P, _P]),
     "mlh_merkle_commit": (_I, [_P, _P, _U64, _U64, _P, _P]),

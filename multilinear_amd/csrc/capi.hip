@@ -286,9 +286,10 @@ static bool check_generator(u128 gen, uint32_t log_n) {
   return half == kModulus - 1;  // gen^(N/2) = -1  <=>  order exactly N
 }
 
-// Core NTT on device (in may equal out; zero_top: input has N/2 elements).
+// Core NTT on device (in may equal out; zero_top 1: input has N/2 elements,
+// 2: N/2 elements stored bit-reversed -- then in must not equal out).
 static mlh_status ntt_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, u128 gen,
-                           bool inverse, bool zero_top) {
+                           bool inverse, int zero_top) {
   NttTables tb;
   MLH_TRY(get_ntt_tables(ctx, gen, log_n, inverse, &tb));
   if (log_n <= 10) {
@@ -297,7 +298,7 @@ static mlh_status ntt_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, 
       // small kernel reads everything into LDS before writing; in-place is safe
     }
     HIP_TRY(ctx, launch_ntt_small(in, out, tb.tw_small, log_n, zero_top ? N / 2 : N, tb.scale,
-                                  inverse, ctx->stream));
+                                  inverse, ctx->stream, 1, zero_top == 2));
     return MLH_OK;
   }
   const size_t need = (size_t)16 << log_n;
@@ -510,7 +511,19 @@ mlh_status mlh_reed_solomon(mlh_ctx* ctx, const void* dev_coeffs, uint32_t log_n
   const u128 g = h_load(gen);
   if (!check_generator(g, lc)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != 2n");
   return ntt_core(ctx, reinterpret_cast<const fe*>(dev_coeffs), reinterpret_cast<fe*>(dev_code),
-                  lc, g, false, true);
+                  lc, g, false, 1);
+}
+
+mlh_status mlh_reed_solomon_brev(mlh_ctx* ctx, const void* dev_coeffs, uint32_t log_n,
+                                 const uint8_t gen[16], void* dev_code) {
+  if (!ctx || !dev_coeffs || !dev_code || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_n > 31) return fail(ctx, MLH_ERR_INVALID, "log_n too large");
+  if (dev_coeffs == dev_code) return fail(ctx, MLH_ERR_INVALID, "reed_solomon is out of place");
+  const uint32_t lc = log_n + MLH_LOG_BLOWUP;
+  const u128 g = h_load(gen);
+  if (!check_generator(g, lc)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != 2n");
+  return ntt_core(ctx, reinterpret_cast<const fe*>(dev_coeffs), reinterpret_cast<fe*>(dev_code),
+                  lc, g, false, 2);
 }
 
 uint64_t mlh_merkle_layers_bytes(uint64_t leaves) { return leaves ? (2 * leaves - 1) * 32 : 0; }
@@ -1332,17 +1345,16 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   const u128 gen = h_pow2_generator(log_domain);  // gen_pows[1] (multilinear_pcs.rs:103-104)
   uint8_t genb[16];
   h_store(genb, gen);
-  PoolBuf coeffs(ctx), brev(ctx), code(ctx), matrix(ctx), delta(ctx);
+  PoolBuf coeffs(ctx), code(ctx), matrix(ctx), delta(ctx);
   MLH_TRY(coeffs.alloc(n * 16));
-  MLH_TRY(brev.alloc(n * 16));
   MLH_TRY(code.alloc(2 * n * 16));
   MLH_TRY(matrix.alloc(n * 16));
   MLH_TRY(delta.alloc(n * 16));
-  // to_coefficient (:107), bit reverse (:109), reed_solomon (:112)
-  HIP_TRY(ctx, hipMemcpyAsync(coeffs.p, dev_evals, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
-  MLH_TRY(mlh_mle_to_coefficient(ctx, coeffs.p, n_vars));
-  MLH_TRY(mlh_bit_reverse_permutation(ctx, coeffs.p, brev.p, n_vars));
-  MLH_TRY(mlh_reed_solomon(ctx, brev.p, n_vars, genb, code.p));
+  // to_coefficient (:102), bit reverse (:104), reed_solomon (:107); the copy
+  // and the permutation are folded into the Moebius and first NTT passes
+  HIP_TRY(ctx, launch_mobius(coeffs.as<fe>(), n_vars, false, ctx->stream,
+                             reinterpret_cast<const fe*>(dev_evals)));
+  MLH_TRY(mlh_reed_solomon_brev(ctx, coeffs.p, n_vars, genb, code.p));  // bitrev fused
   // PCSProverData::init (:28-42) + fold loop (:57-75), transcript on the
   // device: per round the sumcheck round kernel absorbs (c1, c2) and derives
   // r, which the sumcheck fold and the FRI fold_step read from HBM.
@@ -1749,21 +1761,18 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   uint8_t genb[16];
   h_store(genb, h_pow2_generator(log_domain));
   // codes: to_coefficient, bit reverse, RS per polynomial (batched_pcs.rs:137-146)
-  PoolBuf coeffs(ctx), brev(ctx), codes(ctx), matrix(ctx), delta(ctx), outs(ctx);
+  PoolBuf coeffs(ctx), codes(ctx), matrix(ctx), delta(ctx), outs(ctx);
   MLH_TRY(coeffs.alloc(n * 16));
-  MLH_TRY(brev.alloc(n * 16));
   MLH_TRY(codes.alloc((uint64_t)num_polys * N * 16));
   MLH_TRY(matrix.alloc(n * 16));
   MLH_TRY(delta.alloc(n * 16));
   MLH_TRY(outs.alloc(16ull * num_polys));
   const uint8_t* ev = reinterpret_cast<const uint8_t*>(dev_evals);
   for (uint32_t j = 0; j < num_polys; ++j) {
-    HIP_TRY(ctx, hipMemcpyAsync(coeffs.p, ev + (uint64_t)j * n * 16, n * 16,
-                                hipMemcpyDeviceToDevice, ctx->stream));
-    MLH_TRY(mlh_mle_to_coefficient(ctx, coeffs.p, n_vars));
-    MLH_TRY(mlh_bit_reverse_permutation(ctx, coeffs.p, brev.p, n_vars));
-    MLH_TRY(mlh_reed_solomon(ctx, brev.p, n_vars, genb,
-                             codes.as<uint8_t>() + (uint64_t)j * N * 16));
+    HIP_TRY(ctx, launch_mobius(coeffs.as<fe>(), n_vars, false, ctx->stream,
+                               reinterpret_cast<const fe*>(ev + (uint64_t)j * n * 16)));
+    MLH_TRY(mlh_reed_solomon_brev(ctx, coeffs.p, n_vars, genb,
+                                  codes.as<uint8_t>() + (uint64_t)j * N * 16));
   }
   // init (batched_pcs.rs:36-78): absorb the claim, batched FRI init
   for (uint32_t i = 0; i < n_vars; ++i) mlh_transcript_absorb(tr, inputs + 16 * i, 16);

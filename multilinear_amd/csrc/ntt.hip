@@ -73,7 +73,11 @@ constexpr int pass_waves_per_simd(int logr) {
   return logr == 8 ? 5 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2));
 }
 
-template <int LOGR, int TW, bool ZERO_TOP>
+// ZT: 0 = full input; 1 = input has N/2 elements, upper half implicit zeros
+// (Reed-Solomon); 2 = as 1, with the N/2 inputs stored bit-reversed, i.e.
+// coefficient j is in[bitrev_{log_n - 1}(j)] (the PCS's bit_reverse_permutation
+// folded into pass 0's loads; pass 0 only, never the last pass).
+template <int LOGR, int TW, int ZT>
 __global__ void __launch_bounds__(kCols * (1 << LOGR) / kEPT,
                                   TW == 2 ? 1 : pass_waves_per_simd(LOGR))
 ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
@@ -125,8 +129,15 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   for (int e = 0; e < kEPT; ++e) {
     const uint32_t row = bitrev((uint32_t)(t * kEPT + e), LOGR);
     // rows >= R/2 are the implicit zero half; bitrev puts them exactly at odd e
-    if (ZERO_TOP && (e & 1)) {
+    if (ZT != 0 && (e & 1)) {
       x[e] = fe_zero();
+    } else if (ZT == 2) {
+      // coefficient row*W + col, row < R/2, lives at bitrev(col)*(R/2) +
+      // bitrev_{LOGR-1}(row) = bitrev(col)*(R/2) + (t*kEPT + e)/2: each lane
+      // reads 4 consecutive elements
+      const uint32_t logw = g.log_n - LOGR;
+      const uint64_t colr = __builtin_bitreverse64(jrest) >> (64 - logw);
+      x[e] = fe_load(in + (colr << (LOGR - 1)) + ((uint32_t)(t * kEPT + e) >> 1));
     } else {
       x[e] = fe_load(src + (uint64_t)row * rstride);
     }
@@ -151,7 +162,7 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
           const int e1 = e0 + d;
           const uint32_t pos = bpos + ((uint32_t)i << s0);
           const uint32_t j = pos & ((1u << s) - 1u);
-          if (ZERO_TOP && s0 == 0 && s == 0) {  // (u, 0) -> (u, u)
+          if (ZT != 0 && s0 == 0 && s == 0) {  // (u, 0) -> (u, u)
             x[e1] = x[e0];
             continue;
           }
@@ -241,14 +252,16 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
 // Single-workgroup NTT for N <= 2^10: LDS-resident radix-2 DIT.
 __global__ void __launch_bounds__(512)
 ntt_small_kernel(const fe* __restrict__ in, fe* __restrict__ out, const fe* __restrict__ tw,
-                 uint32_t log_n, uint32_t in_len, fe scale, int apply_scale) {
+                 uint32_t log_n, uint32_t in_len, fe scale, int apply_scale, int brev_in) {
   __shared__ fe lds[1024];
   const uint32_t N = 1u << log_n;
   in += (uint64_t)blockIdx.x * in_len;
   out += (uint64_t)blockIdx.x * N;
   for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
     const uint32_t src = bitrev(i, (int)log_n);
-    lds[i] = src < in_len ? fe_load(in + src) : fe_zero();
+    // brev_in: coefficient src is stored at bitrev_{log2 in_len}(src) (ZT == 2)
+    const uint32_t at = (brev_in && in_len > 1) ? bitrev(src, 31 - __builtin_clz(in_len)) : src;
+    lds[i] = src < in_len ? fe_load(in + at) : fe_zero();
   }
   __syncthreads();
   for (uint32_t s = 0; s < log_n; ++s) {
@@ -319,29 +332,26 @@ __global__ void pow_series_kernel(fe* __restrict__ out, const fe* __restrict__ t
 // ---- host-side launchers ---------------------------------------------------
 
 template <int LOGR>
-static hipError_t launch_pass(bool last, bool zero_top, const fe* in, fe* out, const fe* tw,
+static hipError_t launch_pass(bool last, int zero_top, const fe* in, fe* out, const fe* tw,
                               const fe* ta, const fe* tb, const PassGeom& g, uint64_t tiles,
                               hipStream_t st) {
   constexpr int threads = kCols * (1 << LOGR) / kEPT;
   const dim3 grid((unsigned)tiles), blk(threads);
+#define MLH_PASS(TWV, ZTV)                                                                  \
+  hipLaunchKernelGGL((ntt_pass_kernel<LOGR, TWV, ZTV>), grid, blk, 0, st, in, out, tw, ta, tb, g)
   if (last) {
-    hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 2, false>), grid, blk, 0, st, in, out, tw, ta, tb,
-                       g);
+    if (zero_top) return hipErrorInvalidValue;  // pass 0 is never the last pass here
+    MLH_PASS(2, 0);
   } else if (!tb) {
-    if (zero_top)
-      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 1, true>), grid, blk, 0, st, in, out, tw, ta, tb,
-                         g);
-    else
-      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 1, false>), grid, blk, 0, st, in, out, tw, ta, tb,
-                         g);
+    if (zero_top == 2) MLH_PASS(1, 2);
+    else if (zero_top == 1) MLH_PASS(1, 1);
+    else MLH_PASS(1, 0);
   } else {
-    if (zero_top)
-      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 0, true>), grid, blk, 0, st, in, out, tw, ta, tb,
-                         g);
-    else
-      hipLaunchKernelGGL((ntt_pass_kernel<LOGR, 0, false>), grid, blk, 0, st, in, out, tw, ta, tb,
-                         g);
+    if (zero_top == 2) MLH_PASS(0, 2);
+    else if (zero_top == 1) MLH_PASS(0, 1);
+    else MLH_PASS(0, 0);
   }
+#undef MLH_PASS
   return hipGetLastError();
 }
 
@@ -376,22 +386,23 @@ void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr) {
 }
 
 hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n, uint64_t in_len,
-                            fe scale, bool apply_scale, hipStream_t st, uint64_t batch) {
+                            fe scale, bool apply_scale, hipStream_t st, uint64_t batch,
+                            bool brev_in) {
   const uint32_t N = 1u << log_n;
   const uint32_t threads = N / 2 < 64 ? 64 : (N / 2 > 512 ? 512 : N / 2);
   hipLaunchKernelGGL(ntt_small_kernel, dim3((unsigned)batch), dim3(threads), 0, st, in, out, tw, log_n,
-                     (uint32_t)in_len, scale, apply_scale ? 1 : 0);
+                     (uint32_t)in_len, scale, apply_scale ? 1 : 0, brev_in ? 1 : 0);
   return hipGetLastError();
 }
 
-void ntt_pass_label(const NttTables& tb, uint32_t p, bool zero_top, char* buf, size_t n) {
+void ntt_pass_label(const NttTables& tb, uint32_t p, int zero_top, char* buf, size_t n) {
   const bool last = p + 1 == tb.nradix;
   const int tw = last ? 2 : (tb.tb[p] ? 0 : 1);
-  snprintf(buf, n, "ntt_pass<%u,%d,%d>", tb.logr[p], tw, (zero_top && p == 0) ? 1 : 0);
+  snprintf(buf, n, "ntt_pass<%u,%d,%d>", tb.logr[p], tw, p == 0 ? zero_top : 0);
 }
 
 hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables& tb,
-                             uint32_t log_n, bool zero_top, hipStream_t st, hipEvent_t* ev,
+                             uint32_t log_n, int zero_top, hipStream_t st, hipEvent_t* ev,
                              uint64_t batch) {
   PassGeom g;
   g.log_n = log_n;
@@ -418,7 +429,7 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
     // not yet resident, blocks still have to read.
     const fe* src = (p == 0) ? in : scratch;
     fe* dst = last ? out : scratch;
-    const bool zt = zero_top && p == 0;
+    const int zt = p == 0 ? zero_top : 0;
     if (ev) (void)hipEventRecord(ev[p], st);
     hipError_t e;
     switch (lr) {

@@ -33,16 +33,18 @@ void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr);
 
 // batch: vectors of in_len inputs / N outputs, contiguous
 hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n, uint64_t in_len,
-                            fe scale, bool apply_scale, hipStream_t st, uint64_t batch = 1);
-// in: N elements (or N/2 when zero_top: the upper half is implicit zeros).
+                            fe scale, bool apply_scale, hipStream_t st, uint64_t batch = 1,
+                            bool brev_in = false);
+// in: N elements, or N/2 when zero_top != 0 (the upper half is implicit
+// zeros); zero_top == 2: those N/2 are stored in bit-reversed order.
 // in may equal out; scratch: N elements, distinct from in and out.
 // ev (optional, nradix + 1 events): ev[p] is recorded before pass p, ev[P]
 // after the last pass (kernel timing on the launch stream).
 hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables& tb,
-                             uint32_t log_n, bool zero_top, hipStream_t st,
+                             uint32_t log_n, int zero_top, hipStream_t st,
                              hipEvent_t* ev = nullptr, uint64_t batch = 1);
 // rocprof-style kernel label of pass p ("ntt_pass<8,0,0>")
-void ntt_pass_label(const NttTables& tb, uint32_t p, bool zero_top, char* buf, size_t n);
+void ntt_pass_label(const NttTables& tb, uint32_t p, int zero_top, char* buf, size_t n);
 hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st,
                             bool expand = false);
 hipError_t launch_pow_table2d(fe* out, fe base, fe scale, uint64_t rows, uint64_t cols,

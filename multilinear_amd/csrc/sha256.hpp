@@ -3,8 +3,8 @@
 // Sigma/sigma 3-way XORs are single v_bitop3_b32 (gfx950).
 // Reference: the sha2 0.10.8 crate (Cargo.lock:261-269) used by
 // src/merkle_tree/mod.rs:178-189 (hash_leaf / hash_node) and
-// src/transcript.rs.  Rotations are v_alignbit_b32, Ch/Maj are v_bfi_b32,
-// the 3-input adds/xors fold to v_add3_u32 / v_xor3_b32.
+// src/transcript.rs.  Rotations are v_alignbit_b32, Ch and Maj one
+// v_bitop3_b32 each, the 3-input adds fold to v_add3_u32.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -19,6 +19,11 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 // v_xor_b32 for the Sigma/sigma functions otherwise.
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// Maj(a, b, c) in one v_bitop3_b32 (table 0xE8: set where >= 2 inputs are);
+// left to itself hipcc emits xor + and + bitop3 per round.
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
 
 #define MLH_SHA_K                                                                               \
@@ -59,7 +64,7 @@ __device__ __forceinline__ void sha256_compress(Sha256State& st, uint32_t w[16])
     const uint32_t ch = (e & f) ^ (~e & g);
     const uint32_t t1 = h + S1 + ch + K[t] + w[t & 15];
     const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-    const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t maj = maj3(a, b, c);
     const uint32_t t2 = S0 + maj;
     h = g;
     g = f;
@@ -110,7 +115,7 @@ __device__ __forceinline__ void sha256_compress_pad64(Sha256State& st) {
     const uint32_t ch = (e & f) ^ (~e & g);
     const uint32_t t1 = h + S1 + ch + KW.v[t];
     const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-    const uint32_t maj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t maj = maj3(a, b, c);
     h = g;
     g = f;
     f = e;

@@ -173,12 +173,13 @@ eq_expand_kernel(const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t 
 }
 
 // Moebius (sign = -1) / zeta (sign = +1) transform over `nbits` consecutive
-// index bits [b0, b0 + nbits) of a 2^log_n table, in place.  A workgroup owns
+// index bits [b0, b0 + nbits) of a 2^log_n table, src -> c (src may equal c:
+// a tile is read whole before it is written).  A workgroup owns
 // a tile of 8 adjacent low-index columns (or 8 consecutive elements of each
 // row when b0 == 0) x 2^nbits rows staged in LDS.
 template <int SIGN>
 __global__ void __launch_bounds__(256)
-mobius_pass_kernel(fe* __restrict__ c, uint32_t log_n, uint32_t b0, uint32_t nbits) {
+mobius_pass_kernel(const fe* src, fe* c, uint32_t log_n, uint32_t b0, uint32_t nbits) {
   __shared__ fe lds[2048];
   const uint64_t R = 1ull << nbits;
   const uint64_t W = 1ull << b0;  // row stride
@@ -192,7 +193,7 @@ mobius_pass_kernel(fe* __restrict__ c, uint32_t log_n, uint32_t b0, uint32_t nbi
   const uint64_t E = R * cols;
   for (uint64_t e = threadIdx.x; e < E; e += blockDim.x) {
     const uint64_t row = e / cols, col = e % cols;
-    lds[e] = fe_load(c + base + row * W + col);
+    lds[e] = fe_load(src + base + row * W + col);
   }
   __syncthreads();
   for (uint32_t b = 0; b < nbits; ++b) {
@@ -285,7 +286,13 @@ hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipS
   return hipGetLastError();
 }
 
-hipError_t launch_mobius(fe* c, uint32_t log_n, bool inverse_zeta, hipStream_t st) {
+hipError_t launch_mobius(fe* c, uint32_t log_n, bool inverse_zeta, hipStream_t st,
+                         const fe* src) {
+  if (!src) src = c;
+  if (log_n == 0 && src != c) {
+    hipError_t e = hipMemcpyAsync(c, src, sizeof(fe), hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return e;
+  }
   uint32_t b0 = 0;
   while (b0 < log_n) {
     const uint32_t nb = (log_n - b0) < 8 ? (log_n - b0) : 8;
@@ -296,11 +303,12 @@ hipError_t launch_mobius(fe* c, uint32_t log_n, bool inverse_zeta, hipStream_t s
     while ((1ull << bits) * cols > 2048) --bits;
     const uint64_t tiles = (1ull << log_n) / ((1ull << bits) * cols);
     if (inverse_zeta)
-      hipLaunchKernelGGL(mobius_pass_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, st, c, log_n,
-                         b0, bits);
+      hipLaunchKernelGGL(mobius_pass_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, st, src, c,
+                         log_n, b0, bits);
     else
-      hipLaunchKernelGGL(mobius_pass_kernel<-1>, dim3((unsigned)tiles), dim3(256), 0, st, c, log_n,
-                         b0, bits);
+      hipLaunchKernelGGL(mobius_pass_kernel<-1>, dim3((unsigned)tiles), dim3(256), 0, st, src, c,
+                         log_n, b0, bits);
+    src = c;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     b0 += bits;

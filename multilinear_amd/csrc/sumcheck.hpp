@@ -25,7 +25,9 @@ hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, 
 hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
                       hipStream_t st);
 hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st);
-hipError_t launch_mobius(fe* c, uint32_t log_n, bool inverse_zeta, hipStream_t st);
+// src (optional): the first pass reads src instead of c (out-of-place transform)
+hipError_t launch_mobius(fe* c, uint32_t log_n, bool inverse_zeta, hipStream_t st,
+                         const fe* src = nullptr);
 hipError_t launch_bitrev(const fe* in, fe* out, uint32_t log_n, hipStream_t st);
 
 }  // namespace mlh

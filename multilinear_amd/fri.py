@@ -24,6 +24,16 @@ def reed_solomon(coeffs, gen, device=0):
     return out
 
 
+def reed_solomon_brev(coeffs, gen, device=0):
+    """reed_solomon(bit_reverse_permutation(coeffs)) in one transform
+    (multilinear_pcs.rs:104-107): the permutation is folded into the loads."""
+    ctx = context(device)
+    n = coeffs.shape[0]
+    out = empty(2 * n, device)
+    check(lib().mlh_reed_solomon_brev(ctx, ptr(coeffs), _log2(n), fe_bytes(gen), ptr(out)), ctx)
+    return out
+
+
 def fold_layer(layer, k, log_domain, r, device=0):
     """The fold loop of FriProverData::fold_step (fri/mod.rs:89-114)."""
     ctx = context(device)

@@ -432,6 +432,20 @@ def test_reed_solomon_and_fri_commit_vs_c_oracle(log_n):
     assert pd.last_element == last
 
 
+@pytest.mark.parametrize("log_n", [0, 1, 4, 9, 10, 11, 13, 17, 20])
+def test_reed_solomon_brev_vs_c_oracle(log_n):
+    """Fused bit reversal (ZT == 2 pass-0 loads / small-kernel path) against
+    the C oracle's reed_solomon of the explicitly permuted coefficients."""
+    C = _c_oracle()
+    n = 1 << log_n
+    g = F.pow_2_generator(log_n + 1)
+    x = D.random_limbs(n, 900 + log_n)
+    perm = np.array([int(format(i, "0%db" % log_n)[::-1], 2) if log_n else 0 for i in range(n)])
+    want = C.reed_solomon(np.ascontiguousarray(x[perm]), log_n, g)
+    got = D.from_device(MF.reed_solomon_brev(D.to_device(x), g))
+    assert (got == want).all()
+
+
 # ---- GPU against the committed golden fixtures ---------------------------------
 
 def _golden():
