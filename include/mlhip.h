@@ -316,6 +316,12 @@ mlh_status mlh_eq_table(mlh_ctx* ctx, const uint8_t* host_points, uint32_t n, vo
 /* MultilinearPolynomialEvals::evaluate (polynomials.rs:165-187). */
 mlh_status mlh_mle_evaluate(mlh_ctx* ctx, const void* dev_evals, uint32_t n,
                             const uint8_t* host_args, uint8_t out[16]);
+/* Trace::evaluate (constraint_system/evaluation.rs:31-48): the row-major
+ * 2^log_height x width trace (dev_matrix, element (i, j) at i*width + j) as
+ * width MLEs evaluated at the log_height host points (big-endian, Mask order):
+ * out[j] = sum_i Mask{i}(points) * matrix[i*width + j]; out: 16*width bytes. */
+mlh_status mlh_trace_evaluate(mlh_ctx* ctx, const void* dev_matrix, uint32_t log_height,
+                              uint32_t width, const uint8_t* host_points, uint8_t* out);
 /* SumcheckTables::partial_sum (sumcheck.rs:204-232), composition x[0]
  * (multilinear_pcs.rs:56), at X = 1 and X = 2: out = s1 ‖ s2.
  * Tables have 2^log_height elements. */

@@ -1254,6 +1254,25 @@ mlh_status mlh_mle_evaluate(mlh_ctx* ctx, const void* dev_evals, uint32_t n,
   return MLH_OK;
 }
 
+mlh_status mlh_trace_evaluate(mlh_ctx* ctx, const void* dev_matrix, uint32_t log_height,
+                             uint32_t width, const uint8_t* host_points, uint8_t* out) {
+  if (!ctx || !dev_matrix || !out || log_height > 40 || width == 0 || width > (1u << 20) ||
+      (log_height && !host_points))
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  const uint64_t height = 1ull << log_height;
+  const uint32_t nc = width < 256 ? width : 256;
+  PoolBuf eq(ctx), partials(ctx), res(ctx);
+  MLH_TRY(eq.alloc(16ull << log_height));
+  MLH_TRY(partials.alloc(16ull * trace_eval_blocks(height, nc) * nc));
+  MLH_TRY(res.alloc(16ull * width));
+  MLH_TRY(mlh_eq_table(ctx, host_points, log_height, eq.p));
+  HIP_TRY(ctx, launch_trace_eval(reinterpret_cast<const fe*>(dev_matrix), eq.as<fe>(), height, width,
+                                 partials.as<fe>(), res.as<fe>(), ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(out, res.p, 16ull * width, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+
 mlh_status mlh_sumcheck_partial_sums(mlh_ctx* ctx, const void* dev_matrix, const void* dev_delta,
                                      uint32_t log_height, uint8_t out[32]) {
   if (!ctx || !dev_matrix || !dev_delta || !out || log_height < 1 || log_height > 40)
@@ -1334,6 +1353,19 @@ mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, u
 // ---------------------------------------------------------------------------
 // multilinear PCS
 // ---------------------------------------------------------------------------
+// Sumcheck fold (+ the next round's partial sums) of a device-resident round,
+// r read from HBM.  (Running it on a second stream beside the FRI fold_step,
+// which needs the same r, measured no faster: the tree tail it would fill is
+// a handful of waves, and the cross-stream events cost about what it saved.)
+static mlh_status sumcheck_fold_dr(mlh_ctx* ctx, fe* m, fe* d, uint64_t S, const fe* r_dev,
+                                   uint32_t* np) {
+  if (S >= 4)
+    HIP_TRY(ctx, launch_fold_sums(m, d, S, fe{}, ctx->partials, ctx->small, ctx->stream, r_dev, np));
+  else
+    HIP_TRY(ctx, launch_fold(m, d, S, fe{}, ctx->stream, r_dev));
+  return MLH_OK;
+}
+
 mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
                          const uint8_t* host_inputs, const uint8_t output[16], mlh_transcript* tr,
                          mlh_pcs_proof* proof) {
@@ -1375,13 +1407,8 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   for (uint32_t k = 0; k < n_vars; ++k) {
     HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
                                        ctx->stream));
-    const uint64_t S = 1ull << (n_vars - k);
-    if (S >= 4) {
-      HIP_TRY(ctx, launch_fold_sums(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->partials, sums,
-                                    ctx->stream, lp.r(k), &np));
-    } else {
-      HIP_TRY(ctx, launch_fold(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->stream, lp.r(k)));
-    }
+    MLH_TRY(sumcheck_fold_dr(ctx, matrix.as<fe>(), delta.as<fe>(), 1ull << (n_vars - k), lp.r(k),
+                             &np));
     MLH_TRY(lp.step(k, lp.r(k), false));
   }
   MLH_TRY(lp.finish(32ull * n_vars));
@@ -1799,12 +1826,8 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   for (uint32_t k = 0; k < n_vars; ++k) {  // fold (batched_pcs.rs:80-125)
     HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
                                        ctx->stream));
-    const uint64_t S = 1ull << (n_vars - k);
-    if (S >= 4)
-      HIP_TRY(ctx, launch_fold_sums(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->partials, sums,
-                                    ctx->stream, lp.r(k), &np));
-    else
-      HIP_TRY(ctx, launch_fold(matrix.as<fe>(), delta.as<fe>(), S, fe{}, ctx->stream, lp.r(k)));
+    MLH_TRY(sumcheck_fold_dr(ctx, matrix.as<fe>(), delta.as<fe>(), 1ull << (n_vars - k), lp.r(k),
+                             &np));
     if (k == 0)
       MLH_TRY(lp.step_batched(lp.r(0), false));
     else

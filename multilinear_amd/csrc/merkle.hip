@@ -159,6 +159,41 @@ top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ 
   }
 }
 
+// The latency-bound tail of a tree (levels of <= kTailLevel digests, ~one
+// wave per SIMD or less): each workgroup reduces a chunk of C = 2*blockDim.x
+// digests to its subtree root through LDS, all log2(C) levels in one launch
+// (a level costs one SHA-256 latency, ~4.1 us, not a launch); top_kernel then
+// finishes the subtree roots.  Level i >= 1 below `level` is written at
+// out + (n/2 + ... + n/2^(i-1)) digests, i.e. the tree's level order.
+// (A last-arriving-workgroup finish in the same launch measured slower: its
+// device-scope fences write back and invalidate L2 in every workgroup.)
+__global__ void __launch_bounds__(512)
+subtree_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ out) {
+  __shared__ Sha256State s[512];
+  const uint32_t t = threadIdx.x;
+  const uint64_t b = blockIdx.x;
+  uint32_t m = blockDim.x;  // nodes of this chunk at the current level
+  const uint8_t* c = level + (b * 2 * m + 2 * t) * 32;
+  Sha256State r = sha256_node(digest_load(c), digest_load(c + 32));
+  uint64_t off = 0, lvl = n / 2;  // offset and size of the current level in out
+  digest_store(out + (off + b * m + t) * 32, r);
+  s[t] = r;
+  while (m > 1) {
+    off += lvl;
+    lvl /= 2;
+    const uint32_t mp = m / 2;
+    __syncthreads();
+    const bool active = t < mp;
+    if (active) r = sha256_node(s[2 * t], s[2 * t + 1]);
+    __syncthreads();
+    if (active) {
+      s[t] = r;
+      digest_store(out + (off + b * mp + t) * 32, r);
+    }
+    m = mp;
+  }
+}
+
 static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 hipError_t launch_leaf_pairs(const fe* code, uint64_t half, uint8_t* leaves, hipStream_t st) {
@@ -184,7 +219,10 @@ hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t b
 // layers: 2L-1 digests, leaves already at [0, L).
 hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st) {
   uint64_t n = L, off = 0;
-  while (n > 1024) {
+  constexpr uint64_t kTailLevel = 1ull << 18;  // 256 workgroups of 1024-digest chunks
+  constexpr uint64_t kChunk = 1024;
+  constexpr unsigned kSpreadLds = 96 * 1024;
+  while (n > kTailLevel) {
     uint8_t* child = layers + off * 32;
     uint8_t* parent = child + n * 32;
     if (n >= 4 * 1024) {
@@ -201,6 +239,21 @@ hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st) {
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+  }
+  if (n > 1024) {
+    // Chunks of 1024 at 2^18 digests (2^17 hashes = 2 waves per SIMD however
+    // they are cut), 512 below it, so that the first level is one wave per
+    // SIMD.  The (unused) dynamic LDS keeps it to one workgroup per CU: two on
+    // a CU would double every level's latency while other CUs idle.
+    const uint64_t chunk = n >= kTailLevel ? kChunk : kChunk / 2;
+    hipLaunchKernelGGL(subtree_kernel, dim3((unsigned)(n / chunk)), dim3((unsigned)(chunk / 2)),
+                       kSpreadLds, st, layers + off * 32, n, layers + (off + n) * 32);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    for (uint64_t c = chunk; c > 1; c /= 2) {  // input level + log2(chunk) - 1 levels
+      off += n;
+      n /= 2;
+    }
   }
   if (n > 1) {
     const unsigned threads = n / 2 < 64 ? 64 : (unsigned)(n / 2);

@@ -150,6 +150,40 @@ dot_kernel(const fe* __restrict__ a, const fe* __restrict__ b, uint64_t n,
   }
 }
 
+// Trace::evaluate (evaluation.rs:31-48) partials: columns [col0, col0 + ncols)
+// of a row-major height x width trace dotted with the eq table.  256 threads
+// = G = 256 / ncols row groups x ncols columns, so a group reads ncols
+// consecutive elements of one row and the block a contiguous run of G rows.
+__global__ void __launch_bounds__(kRedThreads)
+trace_eval_kernel(const fe* __restrict__ m, const fe* __restrict__ eq, uint64_t height,
+                  uint32_t width, uint32_t col0, uint32_t ncols, fe* __restrict__ partials) {
+  __shared__ fe acc[kRedThreads];
+  const uint32_t G = kRedThreads / ncols;
+  const uint32_t g = threadIdx.x / ncols, j = threadIdx.x % ncols;
+  fe s = fe_zero();
+  if (g < G) {
+    const uint64_t step = (uint64_t)gridDim.x * G;
+    for (uint64_t i = (uint64_t)blockIdx.x * G + g; i < height; i += step)
+      s = fe_add(s, fe_mul(fe_load(eq + i), fe_load(m + i * width + col0 + j)));
+  }
+  acc[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < ncols) {
+    fe t = fe_zero();
+    for (uint32_t q = 0; q < G; ++q) t = fe_add(t, acc[q * ncols + threadIdx.x]);
+    fe_store(partials + (uint64_t)blockIdx.x * ncols + threadIdx.x, t);
+  }
+}
+
+__global__ void trace_eval_finish_kernel(const fe* __restrict__ partials, uint32_t nblocks,
+                                         uint32_t ncols, fe* __restrict__ out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ncols) return;
+  fe t = fe_zero();
+  for (uint32_t b = 0; b < nblocks; ++b) t = fe_add(t, fe_load(partials + (uint64_t)b * ncols + j));
+  fe_store(out + j, t);
+}
+
 // eq table of `cnt` points (big-endian): out[x] = prod_{i<cnt} (bit_i(x) ?
 // p[cnt-1-i] : 1 - p[cnt-1-i]).
 __global__ void eq_small_kernel(const fe* __restrict__ pts, uint32_t cnt, fe* __restrict__ out) {
@@ -269,6 +303,28 @@ hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* ou
   hipLaunchKernelGGL(dot_kernel, dim3(nb), dim3(kRedThreads), 0, st, a, b, n, partials);
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, out);
   return hipGetLastError();
+}
+
+uint32_t trace_eval_blocks(uint64_t height, uint32_t ncols) {
+  const uint64_t G = kRedThreads / ncols;
+  uint64_t b = (height + G - 1) / G;
+  if (b > 1024) b = 1024;
+  return (uint32_t)(b ? b : 1);
+}
+
+hipError_t launch_trace_eval(const fe* m, const fe* eq, uint64_t height, uint32_t width,
+                             fe* partials, fe* out, hipStream_t st) {
+  for (uint32_t col0 = 0; col0 < width; col0 += kRedThreads) {
+    const uint32_t nc = width - col0 < (uint32_t)kRedThreads ? width - col0 : kRedThreads;
+    const uint32_t nb = trace_eval_blocks(height, nc);
+    hipLaunchKernelGGL(trace_eval_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, eq, height, width,
+                       col0, nc, partials);
+    hipLaunchKernelGGL(trace_eval_finish_kernel, dim3((nc + 63) / 64), dim3(64), 0, st, partials,
+                       nb, nc, out + col0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // pts: n device points; scratch: 2^(n-a) + 2^a elements.

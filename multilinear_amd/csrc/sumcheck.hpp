@@ -22,6 +22,11 @@ struct DevSha;
 // interpolate, absorb, challenge, new claim
 hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, DevSha* t,
                                  fe* poly_out, fe* r_out, hipStream_t st);
+// Trace::evaluate: out[j] = sum_i eq[i] * m[i * width + j], j < width;
+// partials: trace_eval_blocks(height, min(width, 256)) * min(width, 256) elements.
+uint32_t trace_eval_blocks(uint64_t height, uint32_t ncols);
+hipError_t launch_trace_eval(const fe* m, const fe* eq, uint64_t height, uint32_t width,
+                             fe* partials, fe* out, hipStream_t st);
 hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
                       hipStream_t st);
 hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st);

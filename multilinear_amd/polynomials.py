@@ -42,6 +42,19 @@ def evaluate(evals, args, device=0):
     return fe_from_bytes(out)
 
 
+def trace_evaluate(matrix, width, points, device=0):
+    """Trace::evaluate (constraint_system/evaluation.rs:31-48): the row-major
+    height x width trace on the device, one MLE per column, at `points`."""
+    n = len(points)
+    if matrix.shape[0] != width << n:
+        raise ValueError("trace height must be 2^len(points)")
+    ctx = context(device)
+    out = (ctypes.c_uint8 * (16 * width))()
+    check(lib().mlh_trace_evaluate(ctx, ptr(matrix), n, width, _points(points), out), ctx)
+    raw = bytes(out)
+    return [fe_from_bytes(raw[16 * j:16 * j + 16]) for j in range(width)]
+
+
 def eq_table(points, device=0):
     """delta table of build_tables_for_pcs (sumcheck.rs:133-138)."""
     from .device import empty

@@ -30,6 +30,21 @@ def eq_table(points):
     return tab
 
 
+def trace_evaluate(matrix, width, points):
+    """Trace::evaluate (evaluation.rs:31-48): res[j] = sum_row Mask(row)(points)
+    * matrix[row * width + j] over the row-major height x width trace."""
+    assert width >= 1 and len(matrix) % width == 0
+    height = len(matrix) // width
+    n = len(points)
+    assert height == 1 << n
+    res = [0] * width
+    for row in range(height):
+        c = mask_evaluate(row, n, points)
+        for j in range(width):
+            res[j] = (res[j] + c * matrix[row * width + j]) % F.M
+    return res
+
+
 def delta_evaluate(data, points):
     """Delta::evaluate (evaluation.rs:75-91): prod a*b + (1-a)(1-b)."""
     acc = 1

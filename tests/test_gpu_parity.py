@@ -263,6 +263,27 @@ def test_eq_table_and_evaluate():
     assert MPL.evaluate(dev(ev), args) == OPL.mle_evaluate(ev, args)
 
 
+@pytest.mark.parametrize("n,w", [(0, 1), (0, 5), (3, 1), (5, 3), (10, 7), (6, 300), (4, 513)])
+def test_trace_evaluate_matches_oracle(n, w):
+    """Trace::evaluate (evaluation.rs:31-48); w > 256 runs several column chunks."""
+    mat = rand_vals(w << n, 40 + w)
+    pts = rand_vals(n, 41)
+    assert MPL.trace_evaluate(dev(mat), w, pts) == OS.trace_evaluate(mat, w, pts)
+
+
+def test_trace_evaluate_large_vs_column_mles():
+    """2^20 x 4 trace: each column equals the device MLE evaluate of it."""
+    n, w = 20, 4
+    m = D.random_device(w << n, 42)
+    pts = rand_vals(n, 43)
+    got = MPL.trace_evaluate(m, w, pts)
+    cols = m.view(-1, w, 4)
+    for j in range(w):
+        assert got[j] == MPL.evaluate(cols[:, j, :].contiguous(), pts)
+    with pytest.raises(ValueError):
+        MPL.trace_evaluate(m, w, pts[:-1])
+
+
 def test_sumcheck_rounds_match_oracle():
     n = 10
     ev = rand_vals(1 << n, 8)

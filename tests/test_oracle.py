@@ -238,3 +238,20 @@ def test_c_oracle_intt_roundtrip_2_18(C):
     g = F.pow_2_generator(ln)
     back = C.ntt(C.ntt(x, ln, g), ln, g, inverse=True)
     assert np.array_equal(back, x)
+
+
+def test_trace_evaluate_oracle():
+    """Trace::evaluate (evaluation.rs:31-48): each column is the MLE of that
+    column (MultilinearPolynomialEvals::evaluate, polynomials.rs:165-187 uses
+    the same big-endian point order); n = 1 by hand."""
+    rr = random.Random(77)
+    n, w = 4, 3
+    mat = [rr.randrange(F.M) for _ in range(w << n)]
+    pts = [rr.randrange(F.M) for _ in range(n)]
+    got = OS.trace_evaluate(mat, w, pts)
+    for j in range(w):
+        assert got[j] == OPL.mle_evaluate(mat[j::w], pts)
+    a, b, c, d, p = 3, 5, 7, 11, 13
+    assert OS.trace_evaluate([a, b, c, d], 2, [p]) == [((1 - p) * a + p * c) % F.M,
+                                                       ((1 - p) * b + p * d) % F.M]
+    assert OS.trace_evaluate([9, 8], 2, []) == [9, 8]
