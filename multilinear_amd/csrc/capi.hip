@@ -546,8 +546,7 @@ mlh_status mlh_merkle_commit_pairs(mlh_ctx* ctx, const void* dev_code, uint32_t 
     return fail(ctx, MLH_ERR_NOT_POW2, "Data length must be a power of two");
   const uint64_t L = 1ull << (log_code - 1);
   uint8_t* layers = reinterpret_cast<uint8_t*>(dev_layers);
-  HIP_TRY(ctx, launch_leaf_pairs(reinterpret_cast<const fe*>(dev_code), L, layers, ctx->stream));
-  HIP_TRY(ctx, launch_merkle_levels(layers, L, ctx->stream));
+  HIP_TRY(ctx, launch_commit_pairs(reinterpret_cast<const fe*>(dev_code), L, layers, ctx->stream));
   return read_root(ctx, layers, L, root_out);
 }
 
@@ -810,8 +809,7 @@ struct FriDevLoop {
     MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
     l0.tree = reinterpret_cast<uint8_t*>(tree);
     p->layers.push_back(l0);
-    HIP_TRY(ctx, launch_leaf_pairs(l0.values, L, l0.tree, ctx->stream));
-    HIP_TRY(ctx, launch_merkle_levels(l0.tree, L, ctx->stream));
+    HIP_TRY(ctx, launch_commit_pairs(l0.values, L, l0.tree, ctx->stream));
     HIP_TRY(ctx, launch_transcript_absorb(dt(), l0.tree + (2 * L - 2) * 32, 32,
                                           challenge_after_root0 ? r(0) : nullptr, ctx->stream,
                                           root(0)));

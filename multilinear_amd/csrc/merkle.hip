@@ -36,6 +36,33 @@ leaf_pairs_kernel(const fe* __restrict__ code, uint64_t half, uint8_t* __restric
   digest_store(leaves + i * 32, sha256_msg32(m));
 }
 
+// Leaves 4j..4j+3 of commit_rs_code plus their two parents and grandparent
+// in one lane: the leaf hashes never make a round trip through HBM before the
+// first two levels, and the leaf level costs no launch of its own.
+__global__ void __launch_bounds__(256)
+leaf_pairs_level2_kernel(const fe* __restrict__ code, uint64_t half, uint8_t* __restrict__ layers) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= half / 4) return;
+  Sha256State lf[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint64_t i = 4 * j + q;
+    const fe a = fe_load(code + i), b = fe_load(code + i + half);
+    uint32_t m[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      m[k] = bswap32(a.w[k]);
+      m[4 + k] = bswap32(b.w[k]);
+    }
+    lf[q] = sha256_msg32(m);
+    digest_store(layers + i * 32, lf[q]);
+  }
+  const Sha256State p0 = sha256_node(lf[0], lf[1]), p1 = sha256_node(lf[2], lf[3]);
+  digest_store(layers + (half + 2 * j) * 32, p0);
+  digest_store(layers + (half + 2 * j + 1) * 32, p1);
+  digest_store(layers + (half + half / 2 + j) * 32, sha256_node(p0, p1));
+}
+
 // Generic leaf: SHA256 of `item_len` bytes at items + i*item_len (any length).
 __global__ void leaf_bytes_kernel(const uint8_t* __restrict__ items, uint64_t item_len,
                                   uint64_t count, uint8_t* __restrict__ leaves) {
@@ -216,9 +243,8 @@ hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t b
   return hipGetLastError();
 }
 
-// layers: 2L-1 digests, leaves already at [0, L).
-hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st) {
-  uint64_t n = L, off = 0;
+// Levels above the level of n digests at layers + off digests (level order).
+static hipError_t merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, hipStream_t st) {
   constexpr uint64_t kTailLevel = 1ull << 18;  // 256 workgroups of 1024-digest chunks
   constexpr uint64_t kChunk = 1024;
   constexpr unsigned kSpreadLds = 96 * 1024;
@@ -261,6 +287,24 @@ hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st) {
                        layers + (off + n) * 32);
   }
   return hipGetLastError();
+}
+
+// layers: 2L-1 digests, leaves already at [0, L).
+hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st) {
+  return merkle_levels_from(layers, 0, L, st);
+}
+
+hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipStream_t st) {
+  if (L < 4) {
+    hipError_t e = launch_leaf_pairs(code, L, layers, st);
+    if (e != hipSuccess) return e;
+    return merkle_levels_from(layers, 0, L, st);
+  }
+  hipLaunchKernelGGL(leaf_pairs_level2_kernel, dim3(blocks_for(L / 4, 256)), dim3(256), 0, st,
+                     code, L, layers);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return merkle_levels_from(layers, L + L / 2, L / 4, st);
 }
 
 }  // namespace mlh

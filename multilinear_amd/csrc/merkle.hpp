@@ -13,6 +13,9 @@ hipError_t launch_leaf_bytes(const uint8_t* items, uint64_t item_len, uint64_t c
 hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t batch_stride,
                              uint32_t m, uint64_t count, uint8_t* leaves, hipStream_t st);
 hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st);
+// commit_rs_code tree of the L = n/2 pairs (code[i], code[i + L]): leaves and
+// every level up to the root into layers (2L-1 digests, level order).
+hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipStream_t st);
 
 // Block-cyclic shard layout of a layer spread over 2^log_p ranks: local
 // index l of rank `rank` holds global index
