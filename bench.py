@@ -46,7 +46,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK = 7.864e13   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz full-rate lane-ops/s
 # practical issue rate of the butterfly instruction mix (fe_mul_pre + add + sub,
 # register resident, no memory): tools/bfly_peak.hip measured 5.3e11
-# butterflies/s x 301 VALU per 4 butterflies = 4.0e13 lane-instr/s
+# butterflies/s x 301 VALU per 4 butterflies = 4.0e13 lane-instr/s; the SHA-256
+# mix peaks at the same rate (tools/sha_latency.hip: 1.65-1.75e10 node hashes/s x
+# 2272 VALU): these integer VOP3 ops issue one wave64 instruction per ~4 cycles
+# per SIMD, half the 2-cycle FP32 rate VALU_PEAK assumes
 VALU_PRACTICAL = 4.0e13
 
 
@@ -124,7 +127,7 @@ def load_valu(kernel):
     import glob
 
     r, tw, z = kernel[len("ntt_pass<"):-1].split(",")
-    name = "void mlh::ntt_pass_kernel<%s, %s, %s>" % (r, tw, "true" if z == "1" else "false")
+    name = "void mlh::ntt_pass_kernel<%s, %s, %s>" % (r, tw, z)  # ZT: int template argument
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu.json")), reverse=True):
         try:
             d = json.load(open(path))

@@ -17,13 +17,13 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LABELS = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(3) for z in range(2)]
+LABELS = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(3) for z in range(3)]
 
 
 def prefix(label):
     """kernel-timer label "ntt_pass<8,0,0>" -> demangled rocprof kernel name prefix"""
     r, tw, z = label[len("ntt_pass<"):-1].split(",")
-    return "void mlh::ntt_pass_kernel<%s, %s, %s>" % (r, tw, "true" if z == "1" else "false")
+    return "void mlh::ntt_pass_kernel<%s, %s, %s>" % (r, tw, z)  # ZT is an int template arg
 
 
 def per_kernel(path, counter):
