@@ -682,10 +682,9 @@ mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
   void* tree;
   MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
   nx.tree = reinterpret_cast<uint8_t*>(tree);
-  HIP_TRY(ctx, launch_fri_fold_leaves(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
+  HIP_TRY(ctx, launch_fri_fold_commit(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
                                       nx.tree, rr, tlo, thi, k, 1ull << p->log_code,
                                       ctx->stream));
-  HIP_TRY(ctx, launch_merkle_levels(nx.tree, L, ctx->stream));
   MLH_TRY(read_root(ctx, nx.tree, L, nx.root));
   p->layers.push_back(nx);
   mlh_transcript_absorb(tr, p->layers.back().root, 32);
@@ -845,10 +844,9 @@ struct FriDevLoop {
     MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
     nx.tree = reinterpret_cast<uint8_t*>(tree);
     p->layers.push_back(nx);
-    HIP_TRY(ctx, launch_fri_fold_leaves(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
+    HIP_TRY(ctx, launch_fri_fold_commit(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
                                         nx.tree, fe{}, tlo, thi, k, 1ull << p->log_code,
                                         ctx->stream, ShardMap(), rp));
-    HIP_TRY(ctx, launch_merkle_levels(nx.tree, L, ctx->stream));
     const uint32_t t = (uint32_t)p->layers.size() - 1;
     HIP_TRY(ctx, launch_transcript_absorb(dt(), nx.tree + (2 * L - 2) * 32, 32,
                                           challenge_next ? r(k + 1) : nullptr, ctx->stream,
@@ -1126,10 +1124,9 @@ mlh_status mlh_shard_fri_fold_commit(mlh_ctx* ctx, const void* dev_layer, uint32
   const fe *tlo, *thi;
   MLH_TRY(fold_tables(ctx, log_domain, &tlo, &thi));
   uint8_t* tree = reinterpret_cast<uint8_t*>(dev_tree);
-  HIP_TRY(ctx, launch_fri_fold_leaves(reinterpret_cast<const fe*>(dev_layer), 1ull << log_local,
+  HIP_TRY(ctx, launch_fri_fold_commit(reinterpret_cast<const fe*>(dev_layer), 1ull << log_local,
                                       reinterpret_cast<fe*>(dev_next), tree, to_fe(h_load(r)),
                                       tlo, thi, k, 1ull << log_domain, ctx->stream, m));
-  HIP_TRY(ctx, launch_merkle_levels(tree, 1ull << (log_local - 2), ctx->stream));
   return MLH_OK;
 }
 
@@ -1978,11 +1975,10 @@ mlh_status mlh_shard_fri_fold_commit_dr(mlh_ctx* ctx, const void* dev_layer, uin
   const fe *tlo, *thi;
   MLH_TRY(fold_tables(ctx, log_domain, &tlo, &thi));
   uint8_t* tree = reinterpret_cast<uint8_t*>(dev_tree);
-  HIP_TRY(ctx, launch_fri_fold_leaves(reinterpret_cast<const fe*>(dev_layer), 1ull << log_local,
+  HIP_TRY(ctx, launch_fri_fold_commit(reinterpret_cast<const fe*>(dev_layer), 1ull << log_local,
                                       reinterpret_cast<fe*>(dev_next), tree, fe{}, tlo, thi, k,
                                       1ull << log_domain, ctx->stream, m,
                                       reinterpret_cast<const fe*>(dev_r)));
-  HIP_TRY(ctx, launch_merkle_levels(tree, 1ull << (log_local - 2), ctx->stream));
   return MLH_OK;
 }
 

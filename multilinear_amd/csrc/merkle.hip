@@ -244,7 +244,7 @@ hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t b
 }
 
 // Levels above the level of n digests at layers + off digests (level order).
-static hipError_t merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, hipStream_t st) {
+hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, hipStream_t st) {
   constexpr uint64_t kTailLevel = 1ull << 18;  // 256 workgroups of 1024-digest chunks
   constexpr uint64_t kChunk = 1024;
   constexpr unsigned kSpreadLds = 96 * 1024;
@@ -291,20 +291,20 @@ static hipError_t merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, 
 
 // layers: 2L-1 digests, leaves already at [0, L).
 hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st) {
-  return merkle_levels_from(layers, 0, L, st);
+  return launch_merkle_levels_from(layers, 0, L, st);
 }
 
 hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipStream_t st) {
   if (L < 4) {
     hipError_t e = launch_leaf_pairs(code, L, layers, st);
     if (e != hipSuccess) return e;
-    return merkle_levels_from(layers, 0, L, st);
+    return launch_merkle_levels_from(layers, 0, L, st);
   }
   hipLaunchKernelGGL(leaf_pairs_level2_kernel, dim3(blocks_for(L / 4, 256)), dim3(256), 0, st,
                      code, L, layers);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return merkle_levels_from(layers, L + L / 2, L / 4, st);
+  return launch_merkle_levels_from(layers, L + L / 2, L / 4, st);
 }
 
 }  // namespace mlh

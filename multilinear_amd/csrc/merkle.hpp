@@ -13,6 +13,8 @@ hipError_t launch_leaf_bytes(const uint8_t* items, uint64_t item_len, uint64_t c
 hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t batch_stride,
                              uint32_t m, uint64_t count, uint8_t* leaves, hipStream_t st);
 hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st);
+// the levels above the level of n digests stored at layers + off digests
+hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, hipStream_t st);
 // commit_rs_code tree of the L = n/2 pairs (code[i], code[i + L]): leaves and
 // every level up to the root into layers (2L-1 digests, level order).
 hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipStream_t st);
@@ -39,6 +41,12 @@ hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe
                            ShardMap map = ShardMap(), const fe* r_dev = nullptr);
 // Fold and hash the next layer's leaves (pairs (next[j], next[j + n/4])).
 hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t* leaves, fe r,
+                                  const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
+                                  hipStream_t st, ShardMap map = ShardMap(),
+                                  const fe* r_dev = nullptr);
+// Fold and commit the next layer: its whole tree (L = n/4 leaves, 2L-1
+// digests) into `tree` (leaves hashed by the fold lanes).
+hipError_t launch_fri_fold_commit(const fe* layer, uint64_t n, fe* next, uint8_t* tree, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
                                   hipStream_t st, ShardMap map = ShardMap(),
                                   const fe* r_dev = nullptr);

@@ -215,35 +215,30 @@ template <int SIGN>
 __global__ void __launch_bounds__(256)
 mobius_pass_kernel(const fe* src, fe* c, uint32_t log_n, uint32_t b0, uint32_t nbits) {
   __shared__ fe lds[2048];
-  const uint64_t R = 1ull << nbits;
   const uint64_t W = 1ull << b0;  // row stride
-  uint64_t cols, base;
   // columns = index bits below b0 (contiguous); tile = up to 8 of them
-  cols = W < 8 ? W : 8;
-  const uint64_t lowcount = W / cols;
+  const uint32_t lc = b0 < 3 ? b0 : 3;  // log2(cols)
+  const uint32_t cmask = (1u << lc) - 1;
+  const uint64_t lowcount = W >> lc;
   const uint64_t tile = blockIdx.x;
   const uint64_t hi = tile / lowcount, lo = tile % lowcount;
-  base = hi * R * W + lo * cols;
-  const uint64_t E = R * cols;
-  for (uint64_t e = threadIdx.x; e < E; e += blockDim.x) {
-    const uint64_t row = e / cols, col = e % cols;
-    lds[e] = fe_load(src + base + row * W + col);
-  }
+  const uint64_t base = (hi << (nbits + b0)) + (lo << lc);
+  const uint32_t E = 1u << (nbits + lc);  // <= 2048
+  for (uint32_t e = threadIdx.x; e < E; e += blockDim.x)
+    lds[e] = fe_load(src + base + ((uint64_t)(e >> lc) << b0) + (e & cmask));
   __syncthreads();
   for (uint32_t b = 0; b < nbits; ++b) {
-    const uint64_t bit = 1ull << b;
-    for (uint64_t e = threadIdx.x; e < E / 2; e += blockDim.x) {
-      const uint64_t pr = e / cols, col = e % cols;  // pair index over rows
-      const uint64_t r0 = (pr & (bit - 1)) | ((pr >> b) << (b + 1));
-      const uint64_t i0 = r0 * cols + col, i1 = (r0 | bit) * cols + col;
+    const uint32_t bit = 1u << b;
+    for (uint32_t e = threadIdx.x; e < E / 2; e += blockDim.x) {
+      const uint32_t pr = e >> lc, col = e & cmask;  // pair index over rows
+      const uint32_t r0 = (pr & (bit - 1)) | ((pr >> b) << (b + 1));
+      const uint32_t i0 = (r0 << lc) + col, i1 = ((r0 | bit) << lc) + col;
       lds[i1] = SIGN < 0 ? fe_sub(lds[i1], lds[i0]) : fe_add(lds[i1], lds[i0]);
     }
     __syncthreads();
   }
-  for (uint64_t e = threadIdx.x; e < E; e += blockDim.x) {
-    const uint64_t row = e / cols, col = e % cols;
-    fe_store(c + base + row * W + col, lds[e]);
-  }
+  for (uint32_t e = threadIdx.x; e < E; e += blockDim.x)
+    fe_store(c + base + ((uint64_t)(e >> lc) << b0) + (e & cmask), lds[e]);
   (void)log_n;
 }
 
