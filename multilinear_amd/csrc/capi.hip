@@ -1320,18 +1320,24 @@ mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, u
   HIP_TRY(ctx, hipMemcpyAsync(sb, ctx->pinned, 144, hipMemcpyHostToDevice, ctx->stream));
   fe* m = reinterpret_cast<fe*>(dev_matrix);
   fe* d = reinterpret_cast<fe*>(dev_delta);
+  // rounds on tables > 2^tail entries: partial-sum kernels over HBM + the
+  // one-lane round kernel; the last `tail` rounds in one LDS-resident launch
+  const uint32_t tail = sumcheck_tail_rounds(L);
   uint32_t np = 0;
-  HIP_TRY(ctx, launch_sums(m, d, 1ull << (L - 1), ctx->partials, ctx->small, ctx->stream, &np));
-  for (uint32_t k = 0; k < L; ++k) {
+  if (L > tail)
+    HIP_TRY(ctx, launch_sums(m, d, 1ull << (L - 1), ctx->partials, ctx->small, ctx->stream, &np));
+  for (uint32_t k = 0; k + tail < L; ++k) {
     HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, prev, dt, polys + 2 * k, rs + k,
                                        ctx->stream));
     const uint64_t S = 1ull << (L - k);
-    if (S >= 4)
+    if (k + 1 + tail < L)  // the next round is not a tail round: fold + its sums
       HIP_TRY(ctx, launch_fold_sums(m, d, S, fe{}, ctx->partials, ctx->small, ctx->stream, rs + k,
                                     &np));
     else
       HIP_TRY(ctx, launch_fold(m, d, S, fe{}, ctx->stream, rs + k));
   }
+  HIP_TRY(ctx, launch_sumcheck_tail(m, d, tail, prev, dt, polys + 2 * (L - tail),
+                                    rs + (L - tail), ctx->stream));
   std::vector<uint8_t> host(48ull * L);
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -27,6 +27,7 @@
 namespace mlh {
 
 constexpr int kRedThreads = 256;
+constexpr uint32_t kTailLogMax = 12;  // sumcheck_tail_kernel: 2 x 2^12 x 16 B = 128 KiB LDS
 
 __device__ __forceinline__ fe shfl_xor_fe(const fe& x, int mask) {
   fe r;
@@ -37,7 +38,7 @@ __device__ __forceinline__ fe shfl_xor_fe(const fe& x, int mask) {
 
 // Block reduction of two field sums; thread 0 ends with the totals.
 __device__ __forceinline__ void block_reduce2(fe& a, fe& b) {
-  __shared__ fe sa[kRedThreads / 64], sb[kRedThreads / 64];
+  __shared__ fe sa[16], sb[16];  // up to 1024 threads
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
     a = fe_add(a, shfl_xor_fe(a, m));
@@ -409,6 +410,86 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
   const fe r = dsha_challenge(s);
   fe_store(r_out, r);
   fe_store(prev, fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r)))));
+}
+
+// The last rounds of a device-resident sumcheck (tables of S <= kTailMax
+// entries) in ONE workgroup with m and d staged in LDS: per round the sums,
+// the round polynomial + Fiat-Shamir step (lane 0, as sumcheck_round_kernel)
+// and the fold, separated by barriers instead of two launches.  The tables
+// are folded in place exactly as fold_kernel does and written back at the end.
+__global__ void __launch_bounds__(kRedThreads)
+sumcheck_tail_kernel(fe* __restrict__ m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t,
+                     fe* polys, fe* rs) {
+  extern __shared__ fe tail_lds[];
+  fe* lm = tail_lds;
+  fe* ld = tail_lds + S;
+  __shared__ DevSha sh;
+  __shared__ fe r_sh;
+  for (uint32_t i = threadIdx.x; i < S; i += blockDim.x) {
+    lm[i] = fe_load(m + i);
+    ld[i] = fe_load(d + i);
+  }
+  fe p = fe_zero();
+  if (threadIdx.x == 0) {
+    sh = *t;
+    p = fe_load(prev);
+  }
+  __syncthreads();
+  const uint32_t S0 = S;
+  for (uint32_t k = 0; S > 1; ++k, S /= 2) {
+    const uint32_t h = S / 2;
+    fe s1 = fe_zero(), s2 = fe_zero();
+    for (uint32_t i = threadIdx.x; i < h; i += blockDim.x) {
+      const fe m0 = lm[i], m1 = lm[i + h], d0 = ld[i], d1 = ld[i + h];
+      s1 = fe_add(s1, fe_mul(m1, d1));
+      s2 = fe_add(s2, fe_mul(fe_sub(fe_dbl(m1), m0), fe_sub(fe_dbl(d1), d0)));
+    }
+    block_reduce2(s1, s2);
+    if (threadIdx.x == 0) {
+      const fe e0 = fe_sub(p, s1);
+      const fe c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
+      const fe c1 = fe_sub(fe_sub(s1, e0), c2);
+      fe_store(polys + 2 * k, c1);
+      fe_store(polys + 2 * k + 1, c2);
+      // absorb LE16(c1) || LE16(c2) from where they were just stored (a
+      // local array would be indexed bytewise from scratch)
+      dsha_update(sh, reinterpret_cast<const uint8_t*>(polys + 2 * k), 32);
+      const fe r = dsha_challenge(sh);
+      fe_store(rs + k, r);
+      p = fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r))));
+      r_sh = r;
+    }
+    __syncthreads();
+    const fe r = r_sh;
+    for (uint32_t i = threadIdx.x; i < h; i += blockDim.x) {
+      lm[i] = lerp(lm[i], lm[i + h], r);
+      ld[i] = lerp(ld[i], ld[i + h], r);
+    }
+    __syncthreads();
+  }
+  for (uint32_t i = threadIdx.x; i < S0; i += blockDim.x) {
+    fe_store(m + i, lm[i]);
+    fe_store(d + i, ld[i]);
+  }
+  if (threadIdx.x == 0) {
+    *t = sh;
+    fe_store(prev, p);
+  }
+}
+
+uint32_t sumcheck_tail_rounds(uint32_t log_height) {
+  return log_height < kTailLogMax ? log_height : kTailLogMax;
+}
+
+hipError_t launch_sumcheck_tail(fe* m, fe* d, uint32_t log_s, fe* prev, DevSha* t, fe* polys,
+                                fe* rs, hipStream_t st) {
+  if (log_s == 0 || log_s > kTailLogMax) return hipErrorInvalidValue;
+  const uint32_t S = 1u << log_s;
+  // 256 threads: 1024 measured slower (150 vs 127 us for 12 rounds) -- a
+  // round is dominated by lane 0's SHA-256 work, the rest by barriers
+  hipLaunchKernelGGL(sumcheck_tail_kernel, dim3(1), dim3(kRedThreads), 2 * S * sizeof(fe), st, m,
+                     d, S, prev, t, polys, rs);
+  return hipGetLastError();
 }
 
 hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, DevSha* t,

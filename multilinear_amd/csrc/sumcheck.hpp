@@ -27,6 +27,12 @@ hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, 
 uint32_t trace_eval_blocks(uint64_t height, uint32_t ncols);
 hipError_t launch_trace_eval(const fe* m, const fe* eq, uint64_t height, uint32_t width,
                              fe* partials, fe* out, hipStream_t st);
+// Device-resident sumcheck tail: the last sumcheck_tail_rounds(L) rounds on
+// tables of 2^log_s entries in one workgroup (LDS); polys/rs/prev/t as for
+// sumcheck_round_kernel, round k's outputs at polys + 2k, rs + k.
+uint32_t sumcheck_tail_rounds(uint32_t log_height);
+hipError_t launch_sumcheck_tail(fe* m, fe* d, uint32_t log_s, fe* prev, DevSha* t, fe* polys,
+                                fe* rs, hipStream_t st);
 hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
                       hipStream_t st);
 hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st);

@@ -315,6 +315,31 @@ def test_sumcheck_rounds_match_oracle():
     assert tr.random() == otr.random()
 
 
+@pytest.mark.parametrize("n", [1, 2, 12, 13, 15])
+def test_sumcheck_prove_matches_oracle(n):
+    """Device-resident prove around the LDS tail (sumcheck_tail_kernel takes the
+    last min(n, 12) rounds): polys, challenges, transcript and the folded
+    tables (in place, as SumcheckTables::fold leaves them) vs the oracle."""
+    ev = rand_vals(1 << n, 60 + n)
+    pts = rand_vals(n, 61 + n)
+    total = OPL.mle_evaluate(ev, pts)
+    ot = OS.SumcheckTables.build_tables_for_pcs(pts, ev)
+    otr = OT.Transcript()
+    otr.absorb(b"tail")
+    prev, want_polys, want_rs = total, [], []
+    for _ in range(n):
+        nz, r2, prev = ot.compute_sumcheck_polynomial(prev, otr)
+        want_polys.append(tuple(nz))
+        want_rs.append(r2)
+    mt = MS.SumcheckTables.build_tables_for_pcs(pts, dev(ev))
+    tr = Transcript()
+    tr.absorb(b"tail")
+    polys, rs = mt.compute_sumcheck_polynomials(total, tr)
+    assert polys == want_polys and rs == want_rs
+    assert tr.random() == otr.random()
+    assert host(mt.matrix)[0] == ot.matrix[0] and host(mt.delta)[0] == ot.delta[0]
+
+
 @pytest.mark.parametrize("n", [1, 2, 8, 10])
 def test_pcs_prove_matches_oracle(n):
     """multilinear_pcs_bench_test pattern: evals 7i+3, point (0..n)."""
