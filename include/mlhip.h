@@ -40,7 +40,8 @@ typedef enum mlh_status {
   MLH_ERR_HIP = 4,           /* HIP runtime error / no device                      */
   MLH_ERR_OOM = 5,           /* device allocation failed                           */
   MLH_ERR_NOT_RS_CODE = 6,   /* fri/mod.rs:119-122 "not an RS code"                */
-  MLH_ERR_VERIFY = 7         /* verifier rejected                                  */
+  MLH_ERR_VERIFY = 7,        /* verifier rejected (Merkle: IncompatibleHash)       */
+  MLH_ERR_VERIFY_INDEX = 8   /* Merkle path directions != index (IncompatibleIndex) */
 } mlh_status;
 
 typedef struct mlh_ctx mlh_ctx;               /* device + stream + twiddle caches */
@@ -210,6 +211,21 @@ mlh_status mlh_shard_fri_fold_commit(mlh_ctx* ctx, const void* dev_layer, uint32
                                      uint32_t k, uint32_t log_domain, const uint8_t r[16],
                                      void* dev_next, void* dev_tree, uint32_t log_s,
                                      uint32_t log_p, uint32_t rank);
+/* Merkle::open / batch_open (merkle_tree/mod.rs:31-58, :134-175) on any device
+ * tree of `leaves` leaves (mlh_merkle_commit*, level order): for each
+ * host_idx[q] the log2(leaves) sibling digests, bottom-up, into host out
+ * (nq * 32 * log2(leaves) bytes).  Direction of level i is Right iff bit i of
+ * the index is 0.  MLH_ERR_INVALID for an index >= leaves (the reference
+ * returns None).  The opened value is the caller's item (column) itself. */
+mlh_status mlh_merkle_open(mlh_ctx* ctx, const void* dev_layers, uint64_t leaves,
+                           const uint64_t* host_idx, uint32_t nq, uint8_t* out);
+/* MerkleInclusionPath::verify / batch_verify (merkle_tree/mod.rs:216-293),
+ * host side: value = the leaf bytes (batch_verify: the column items
+ * concatenated), sibs = depth digests, dirs bit i = 1 for Direction::Left.
+ * MLH_OK, MLH_ERR_VERIFY (IncompatibleHash) or MLH_ERR_VERIFY_INDEX
+ * (IncompatibleIndex), checked in that order as the reference does. */
+mlh_status mlh_merkle_verify(const uint8_t* value, uint64_t value_len, const uint8_t* sibs,
+                             uint32_t depth, uint64_t dirs, const uint8_t root[32], uint64_t index);
 /* Merkle::open (merkle_tree/mod.rs:31-58) on a local pair tree: for each
  * local leaf idx[q]: values[idx], values[idx + n/2], then the sibling digests
  * of levels 0..levels-1.  out: nq * 32 * (1 + levels) bytes (host). */

@@ -21,7 +21,9 @@ STATUS_NAMES = {
     5: "MLH_ERR_OOM",
     6: "MLH_ERR_NOT_RS_CODE",
     7: "MLH_ERR_VERIFY",
+    8: "MLH_ERR_VERIFY_INDEX",
 }
+STATUS_CODES = {v: k for k, v in STATUS_NAMES.items()}
 LOG_BLOWUP = 1
 NUM_QUERIES = 128
 
@@ -125,6 +127,8 @@ SIGNATURES = {
     "mlh_shard_fri_fold": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _U32, _U32, _U32]),
     "mlh_shard_fri_fold_commit": (_I, [_P, _P, _U32, _U32, _U32, _P, _P, _P, _U32, _U32, _U32]),
     "mlh_merkle_open_pairs": (_I, [_P, _P, _U32, _P, _U32, _P, _U32, _P]),
+    "mlh_merkle_open": (_I, [_P, _P, _U64, _P, _U32, _P]),
+    "mlh_merkle_verify": (_I, [_P, _U64, _P, _U32, _U64, _P, _U64]),
     "mlh_batched_fri_query_bytes": (_U64, [_U32, _U32]),
     "mlh_batched_fri_prove": (_I, [_P, _P, _U32, _U32, _P, ctypes.POINTER(BatchedFriProofC)]),
     "mlh_batched_fri_verify": (_I, [ctypes.POINTER(BatchedFriProofC)]),

@@ -1465,6 +1465,56 @@ static bool verify_path(const uint8_t* value32, const uint8_t* sibs, uint32_t de
   return verify_path_len(value32, 32, sibs, depth, root, index);
 }
 
+extern "C" {
+
+mlh_status mlh_merkle_open(mlh_ctx* ctx, const void* dev_layers, uint64_t leaves,
+                           const uint64_t* host_idx, uint32_t nq, uint8_t* out) {
+  if (!ctx || !dev_layers || (nq && (!host_idx || !out)))
+    return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (!is_pow2(leaves)) return fail(ctx, MLH_ERR_NOT_POW2, "Data length must be a power of two");
+  for (uint32_t q = 0; q < nq; ++q)
+    if (host_idx[q] >= leaves) return fail(ctx, MLH_ERR_INVALID, "index out of bounds");
+  const uint32_t depth = 63 - __builtin_clzll(leaves);
+  if (nq == 0 || depth == 0) return MLH_OK;
+  const uint64_t rec = 32ull * depth;
+  PoolBuf didx(ctx), dout(ctx);
+  MLH_TRY(didx.alloc(nq * sizeof(uint64_t)));
+  MLH_TRY(dout.alloc(nq * rec));
+  HIP_TRY(ctx, hipMemcpyAsync(didx.p, host_idx, nq * sizeof(uint64_t), hipMemcpyHostToDevice,
+                              ctx->stream));
+  HIP_TRY(ctx, launch_merkle_paths(reinterpret_cast<const uint8_t*>(dev_layers), leaves,
+                                   didx.as<uint64_t>(), nq, dout.as<uint8_t>(), ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(out, dout.p, nq * rec, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MLH_OK;
+}
+
+mlh_status mlh_merkle_verify(const uint8_t* value, uint64_t value_len, const uint8_t* sibs,
+                             uint32_t depth, uint64_t dirs, const uint8_t root[32],
+                             uint64_t index) {
+  if ((value_len && !value) || (depth && !sibs) || !root || depth > 63) return MLH_ERR_INVALID;
+  uint8_t h[32];
+  HostSha256 s;
+  s.update(value, value_len);
+  s.digest(h);
+  uint64_t computed = 0;
+  for (uint32_t l = 0; l < depth; ++l) {
+    uint8_t nh[32];
+    if ((dirs >> l) & 1) {  // Direction::Left
+      computed += 1ull << l;
+      sha_pair(sibs + 32 * l, h, nh);
+    } else {
+      sha_pair(h, sibs + 32 * l, nh);
+    }
+    memcpy(h, nh, 32);
+  }
+  if (memcmp(h, root, 32) != 0) return MLH_ERR_VERIFY;
+  if (computed != index) return MLH_ERR_VERIFY_INDEX;
+  return MLH_OK;
+}
+
+}  // extern "C"
+
 // QueryProof::verify (fri/mod.rs:184-236) over flat records: ntrees paths,
 // tree t has leaves n/2^t (depth log2(n) - t), gen of order 2n.
 static bool query_chain(const uint8_t* rec, const uint8_t* commitments, uint32_t ntrees,

@@ -307,4 +307,28 @@ hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipS
   return launch_merkle_levels_from(layers, L + L / 2, L / 4, st);
 }
 
+// Merkle::open (merkle_tree/mod.rs:31-58): for query q (one workgroup) the
+// sibling of idx[q] on every level below the root, bottom-up.
+__global__ void merkle_path_kernel(const uint8_t* __restrict__ layers, uint64_t L,
+                                   const uint64_t* __restrict__ idx, uint8_t* __restrict__ out) {
+  const uint32_t depth = 63 - __builtin_clzll(L);
+  const uint64_t i = idx[blockIdx.x];
+  uint8_t* rec = out + (uint64_t)blockIdx.x * 32 * depth;
+  for (uint32_t l = threadIdx.x; l < depth; l += blockDim.x) {
+    uint64_t off = 0;
+    for (uint32_t t = 0; t < l; ++t) off += L >> t;
+    const uint4* src = reinterpret_cast<const uint4*>(layers + (off + ((i >> l) ^ 1ull)) * 32);
+    uint4* dst = reinterpret_cast<uint4*>(rec + 32ull * l);
+    dst[0] = src[0];
+    dst[1] = src[1];
+  }
+}
+
+hipError_t launch_merkle_paths(const uint8_t* layers, uint64_t L, const uint64_t* idx, uint32_t nq,
+                               uint8_t* out, hipStream_t st) {
+  if (nq == 0 || L < 2) return hipSuccess;
+  hipLaunchKernelGGL(merkle_path_kernel, dim3(nq), dim3(64), 0, st, layers, L, idx, out);
+  return hipGetLastError();
+}
+
 }  // namespace mlh

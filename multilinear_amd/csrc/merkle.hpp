@@ -15,6 +15,9 @@ hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t b
 hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st);
 // the levels above the level of n digests stored at layers + off digests
 hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, hipStream_t st);
+// sibling paths (depth = log2 L digests, bottom-up) of leaves idx[0..nq) (device array)
+hipError_t launch_merkle_paths(const uint8_t* layers, uint64_t L, const uint64_t* idx, uint32_t nq,
+                               uint8_t* out, hipStream_t st);
 // commit_rs_code tree of the L = n/2 pairs (code[i], code[i + L]): leaves and
 // every level up to the root into layers (2L-1 digests, level order).
 hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipStream_t st);

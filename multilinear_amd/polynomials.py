@@ -10,11 +10,19 @@ def _log2(n):
     return n.bit_length() - 1
 
 
+def _low_bits(n):
+    """trailing_zeros(len): the reference transforms the first 2^tz entries
+    over tz index bits and leaves the rest (len need not be a power of two)."""
+    if n < 1:
+        raise ValueError("empty polynomial")
+    return (n & -n).bit_length() - 1
+
+
 def to_coefficient(evals, device=0):
     """MultilinearPolynomialEvals::to_coefficient (polynomials.rs:150-163); new tensor."""
     ctx = context(device)
     out = evals.clone()
-    check(lib().mlh_mle_to_coefficient(ctx, ptr(out), _log2(evals.shape[0])), ctx)
+    check(lib().mlh_mle_to_coefficient(ctx, ptr(out), _low_bits(evals.shape[0])), ctx)
     return out
 
 
@@ -22,7 +30,7 @@ def to_evaluation(coeffs, device=0):
     """MultilinearPolynomial::to_evaluation (polynomials.rs:111-124); new tensor."""
     ctx = context(device)
     out = coeffs.clone()
-    check(lib().mlh_mle_to_evaluation(ctx, ptr(out), _log2(coeffs.shape[0])), ctx)
+    check(lib().mlh_mle_to_evaluation(ctx, ptr(out), _low_bits(coeffs.shape[0])), ctx)
     return out
 
 

@@ -250,3 +250,25 @@ def test_host_batched_pcs_verifier_accepts_oracle_proof():
     assert bp.verify(Transcript())
     bp.outputs = [outs[0] + 1] + outs[1:]
     assert not bp.verify(Transcript())
+
+
+def test_host_merkle_verify_matches_reference_semantics():
+    """MerkleInclusionPath::verify / batch_verify (merkle_tree/mod.rs:216-293)
+    through mlh_merkle_verify on oracle-built paths: Ok, IncompatibleHash for a
+    wrong value, IncompatibleIndex for directions that do not spell the index."""
+    from multilinear_amd import _lib
+    from multilinear_amd import merkle_tree as MM
+    from oracle import merkle as OM
+
+    data = [bytes([v]) for v in [0, 8, 4, 1, 5, 7, 6, 1]]
+    t = OM.Merkle.commit(data)
+    for i in range(8):
+        value, path = t.open(i)
+        assert MM.verify_status(value, path, t.root(), i) == _lib.MLH_OK
+    value, path = t.open(5)
+    assert MM.verify_status(value, path, t.root(), 4) == _lib.STATUS_CODES["MLH_ERR_VERIFY_INDEX"]
+    assert MM.verify_status(b"\x00", path, t.root(), 5) == _lib.STATUS_CODES["MLH_ERR_VERIFY"]
+    bt = OM.Merkle.batch_commit([data, [bytes([v]) for v in [1, 3, 2, 3, 2, 1, 2, 3]]])
+    col, path = OM.batch_open(bt, 2)
+    assert MM.batch_verify(col, path, bt.root(), 2)
+    assert not MM.batch_verify(col, path, bt.root(), 1)

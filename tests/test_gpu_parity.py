@@ -153,6 +153,50 @@ def test_merkle_commit_generic_items():
     assert MM.Merkle.commit(items).root() == OM.Merkle.commit(items).root()
 
 
+def test_merkle_open_verify_device():
+    """merkle_test (merkle_tree/mod.rs:300-309): open(5) from the device tree
+    equals the oracle's opening and verifies; the wrong index is an
+    IncompatibleIndex, a wrong value an IncompatibleHash; past the end: None."""
+    data = [bytes([v]) for v in [0, 8, 4, 1, 5, 7, 6, 1]]
+    t = MM.Merkle.commit(data)
+    ot = OM.Merkle.commit(data)
+    for i in range(8):
+        assert t.open(i) == ot.open(i)
+    value, path = t.open(5)
+    assert MM.verify(value, path, t.root(), 5)
+    assert MM.verify_status(value, path, t.root(), 4) == _lib.STATUS_CODES["MLH_ERR_VERIFY_INDEX"]
+    assert MM.verify_status(b"\x09", path, t.root(), 5) == _lib.STATUS_CODES["MLH_ERR_VERIFY"]
+    assert t.open(8) is None
+
+
+def test_merkle_batch_open_verify_device():
+    """batched_merkle_test (merkle_tree/mod.rs:311-351)."""
+    data = [[bytes([v]) for v in [0, 8, 4, 1, 5, 7, 6, 1]],
+            [bytes([v]) for v in [1, 3, 2, 3, 2, 1, 2, 3]]]
+    t = MM.Merkle.batch_commit(data)
+    value, path = t.batch_open(5)
+    assert value == [bytes([7]), bytes([1])]
+    assert MM.batch_verify(value, path, t.root(), 5)
+    value, path = t.batch_open(2)
+    assert value == [bytes([4]), bytes([2])]
+    assert MM.batch_verify(value, path, t.root(), 2)
+    assert not MM.batch_verify(value, path, t.root(), 1)
+    assert (value, path) == OM.batch_open(OM.Merkle.batch_commit(data), 2)
+
+
+@pytest.mark.parametrize("log_code", [2, 9, 14])
+def test_merkle_open_pairs_tree(log_code):
+    """Merkle::open on a commit_rs_code tree vs the oracle's (fri/mod.rs:45-55)."""
+    code = rand_vals(1 << log_code, 70 + log_code)
+    t = MM.Merkle.commit_pairs(dev(code))
+    ot = OF.commit_rs_code(code)
+    for i in (0, 1, (1 << (log_code - 1)) - 1, (1 << (log_code - 2)) + 1 if log_code > 2 else 0):
+        value, path = t.open(i)
+        assert value == OF.pair_bytes(code[i], code[i + (1 << (log_code - 1))])
+        assert [bytes(p) for p, _ in path] == [bytes(p) for p, _ in ot.open(i)[1]]
+        assert MM.verify(value, path, t.root(), i)
+
+
 def test_merkle_batch_commit():
     """batched_merkle_test (merkle_tree/mod.rs:311-351)."""
     data = [[bytes([v]) for v in [0, 8, 4, 1, 5, 7, 6, 1]],
@@ -250,6 +294,16 @@ def test_mobius_and_zeta(log_n):
     if log_n <= 11:
         assert host(c) == OPL.to_coefficient(ev)
     assert bool((MPL.to_evaluation(c) == dv).all())
+
+
+@pytest.mark.parametrize("vals", [[0, 1, 4, 8, 9, 3], [5], [2, 7, 1, 8, 2, 8, 1, 8, 2, 8, 4, 5]])
+def test_mle_conversion_any_length(vals):
+    """multilinear_conversion_test (polynomials.rs:206-214): 6 evals, not 2^k --
+    only the low trailing_zeros(len) index bits are transformed."""
+    ev = [F.from_i64(v) for v in vals]
+    c = MPL.to_coefficient(dev(ev))
+    assert host(c) == OPL.to_coefficient(ev)
+    assert host(MPL.to_evaluation(c)) == ev
 
 
 def test_eq_table_and_evaluate():
