@@ -332,6 +332,15 @@ mlh_status mlh_eq_table(mlh_ctx* ctx, const uint8_t* host_points, uint32_t n, vo
 /* MultilinearPolynomialEvals::evaluate (polynomials.rs:165-187). */
 mlh_status mlh_mle_evaluate(mlh_ctx* ctx, const void* dev_evals, uint32_t n,
                             const uint8_t* host_args, uint8_t out[16]);
+/* MultilinearPolynomial::evaluate (polynomials.rs:126-146), coefficient form:
+ * sum_pos coeffs[pos] * prod_{bit b of pos set} args[n-1-b]. */
+mlh_status mlh_mle_coeffs_evaluate(mlh_ctx* ctx, const void* dev_coeffs, uint32_t n,
+                                   const uint8_t* host_args, uint8_t out[16]);
+/* Polynomial::evaluate (ntt/mod.rs:61-67, polynomials.rs:9-14): Horner's
+ * value sum_i coeffs[i] x^i of n device coefficients at host x (canonical);
+ * n = 0 gives 0. */
+mlh_status mlh_poly_evaluate(mlh_ctx* ctx, const void* dev_coeffs, uint64_t n, const uint8_t x[16],
+                             uint8_t out[16]);
 /* Trace::evaluate (constraint_system/evaluation.rs:31-48): the row-major
  * 2^log_height x width trace (dev_matrix, element (i, j) at i*width + j) as
  * width MLEs evaluated at the log_height host points (big-endian, Mask order):

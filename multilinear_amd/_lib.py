@@ -156,6 +156,8 @@ SIGNATURES = {
     "mlh_mle_to_coefficient": (_I, [_P, _P, _U32]),
     "mlh_mle_to_evaluation": (_I, [_P, _P, _U32]),
     "mlh_eq_table": (_I, [_P, _P, _U32, _P]),
+    "mlh_mle_coeffs_evaluate": (_I, [_P, _P, _U32, _P, _P]),
+    "mlh_poly_evaluate": (_I, [_P, _P, _U64, _P, _P]),
     "mlh_trace_evaluate": (_I, [_P, _P, _U32, _U32, _P, _P]),
     "mlh_mle_evaluate": (_I, [_P, _P, _U32, _P, _P]),
     "mlh_sumcheck_partial_sums": (_I, [_P, _P, _P, _U32, _P]),

@@ -1212,7 +1212,15 @@ mlh_status mlh_mle_to_evaluation(mlh_ctx* ctx, void* dev_coeffs, uint32_t log_n)
   return MLH_OK;
 }
 
+static mlh_status eq_table_impl(mlh_ctx* ctx, const uint8_t* host_points, uint32_t n,
+                                void* dev_out, bool mono);
+
 mlh_status mlh_eq_table(mlh_ctx* ctx, const uint8_t* host_points, uint32_t n, void* dev_out) {
+  return eq_table_impl(ctx, host_points, n, dev_out, false);
+}
+
+static mlh_status eq_table_impl(mlh_ctx* ctx, const uint8_t* host_points, uint32_t n,
+                                void* dev_out, bool mono) {
   if (!ctx || !dev_out || (n && !host_points) || n > 40)
     return fail(ctx, MLH_ERR_INVALID, "bad argument");
   PoolBuf pts(ctx), scratch(ctx);
@@ -1221,7 +1229,7 @@ mlh_status mlh_eq_table(mlh_ctx* ctx, const uint8_t* host_points, uint32_t n, vo
   MLH_TRY(scratch.alloc(((1ull << a) + (1ull << b)) * sizeof(fe)));
   if (n) HIP_TRY(ctx, hipMemcpyAsync(pts.p, host_points, n * 16ull, hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, launch_eq_table(pts.as<fe>(), n, scratch.as<fe>(), reinterpret_cast<fe*>(dev_out),
-                               ctx->stream));
+                               ctx->stream, mono));
   // pts/scratch go back to the pool now: a later user of those blocks is
   // ordered after these kernels on the same stream (and the pageable H2D
   // above has consumed host_points before returning)
@@ -1243,6 +1251,44 @@ mlh_status mlh_mle_evaluate(mlh_ctx* ctx, const void* dev_evals, uint32_t n,
   MLH_TRY(mlh_eq_table(ctx, host_args, n, eq.p));
   HIP_TRY(ctx, launch_dot(reinterpret_cast<const fe*>(dev_evals), eq.as<fe>(), 1ull << n,
                           ctx->partials, ctx->small, ctx->stream));
+  uint8_t pair[32];
+  MLH_TRY(read_pair(ctx, ctx->small, pair));
+  memcpy(out, pair, 16);
+  return MLH_OK;
+}
+
+mlh_status mlh_mle_coeffs_evaluate(mlh_ctx* ctx, const void* dev_coeffs, uint32_t n,
+                                   const uint8_t* host_args, uint8_t out[16]) {
+  if (!ctx || !dev_coeffs || !out || n > 40) return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  PoolBuf mono(ctx);
+  MLH_TRY(mono.alloc((16ull << n)));
+  MLH_TRY(eq_table_impl(ctx, host_args, n, mono.p, true));
+  HIP_TRY(ctx, launch_dot(reinterpret_cast<const fe*>(dev_coeffs), mono.as<fe>(), 1ull << n,
+                          ctx->partials, ctx->small, ctx->stream));
+  uint8_t pair[32];
+  MLH_TRY(read_pair(ctx, ctx->small, pair));
+  memcpy(out, pair, 16);
+  return MLH_OK;
+}
+
+mlh_status mlh_poly_evaluate(mlh_ctx* ctx, const void* dev_coeffs, uint64_t n, const uint8_t x[16],
+                             uint8_t out[16]) {
+  if (!ctx || (n && !dev_coeffs) || !x || !out || n > (1ull << 40))
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  if (n == 0) {  // fold over nothing: F::from(0)
+    memset(out, 0, 16);
+    return MLH_OK;
+  }
+  const u128 xv = h_load(x);
+  if (xv >= kModulus) return fail(ctx, MLH_ERR_INVALID, "x not canonical");
+  const uint64_t nlo = n < 4096 ? n : 4096, nhi = (n + 4095) / 4096;
+  PoolBuf tlo(ctx), thi(ctx);
+  MLH_TRY(tlo.alloc(16 * nlo));
+  MLH_TRY(thi.alloc(16 * nhi));
+  HIP_TRY(ctx, launch_pow_table(tlo.as<fe>(), to_fe(xv), to_fe(1), nlo, ctx->stream));
+  HIP_TRY(ctx, launch_pow_table(thi.as<fe>(), to_fe(h_pow(xv, 4096)), to_fe(1), nhi, ctx->stream));
+  HIP_TRY(ctx, launch_poly_eval(reinterpret_cast<const fe*>(dev_coeffs), n, tlo.as<fe>(),
+                                thi.as<fe>(), ctx->partials, ctx->small, ctx->stream));
   uint8_t pair[32];
   MLH_TRY(read_pair(ctx, ctx->small, pair));
   memcpy(out, pair, 16);

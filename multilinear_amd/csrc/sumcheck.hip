@@ -187,15 +187,37 @@ __global__ void trace_eval_finish_kernel(const fe* __restrict__ partials, uint32
 
 // eq table of `cnt` points (big-endian): out[x] = prod_{i<cnt} (bit_i(x) ?
 // p[cnt-1-i] : 1 - p[cnt-1-i]).
-__global__ void eq_small_kernel(const fe* __restrict__ pts, uint32_t cnt, fe* __restrict__ out) {
+// mono: the monomial table instead, bit_i(x) ? p[cnt-1-i] : 1
+// (MultilinearPolynomial::evaluate, polynomials.rs:126-146).
+__global__ void eq_small_kernel(const fe* __restrict__ pts, uint32_t cnt, fe* __restrict__ out,
+                                int mono) {
   const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= (1u << cnt)) return;
   fe acc = fe_one();
   for (uint32_t i = 0; i < cnt; ++i) {
     const fe p = pts[cnt - 1 - i];
-    acc = fe_mul(acc, ((x >> i) & 1u) ? p : fe_sub(fe_one(), p));
+    if ((x >> i) & 1u)
+      acc = fe_mul(acc, p);
+    else if (!mono)
+      acc = fe_mul(acc, fe_sub(fe_one(), p));
   }
   fe_store(out + x, acc);
+}
+
+// Polynomial::evaluate (ntt/mod.rs:61-67, Horner) as sum_i c_i x^i with
+// x^i = tlo[i mod 4096] * thi[i / 4096]: per-block partial sums.
+__global__ void __launch_bounds__(kRedThreads)
+poly_eval_kernel(const fe* __restrict__ c, uint64_t n, const fe* __restrict__ tlo,
+                 const fe* __restrict__ thi, fe* __restrict__ partials) {
+  fe s = fe_zero(), z = fe_zero();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    s = fe_add(s, fe_mul(fe_load(c + i), fe_mul(tlo[i & 4095], thi[i >> 12])));
+  block_reduce2(s, z);
+  if (threadIdx.x == 0) {
+    fe_store(partials + 2 * blockIdx.x, s);
+    fe_store(partials + 2 * blockIdx.x + 1, z);
+  }
 }
 
 // delta[idx] = lo[idx & (2^a - 1)] * hi[idx >> a]
@@ -293,6 +315,15 @@ hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe*
   return hipGetLastError();
 }
 
+hipError_t launch_poly_eval(const fe* c, uint64_t n, const fe* tlo, const fe* thi, fe* partials,
+                            fe* out, hipStream_t st) {
+  const unsigned nb = red_blocks(n);
+  hipLaunchKernelGGL(poly_eval_kernel, dim3(nb), dim3(kRedThreads), 0, st, c, n, tlo, thi,
+                     partials);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
                       hipStream_t st) {
   const unsigned nb = red_blocks(n);
@@ -324,14 +355,16 @@ hipError_t launch_trace_eval(const fe* m, const fe* eq, uint64_t height, uint32_
 }
 
 // pts: n device points; scratch: 2^(n-a) + 2^a elements.
-hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st) {
+hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st,
+                           bool mono) {
   const uint32_t a = n / 2, b = n - a;
   fe* lo = scratch;
   fe* hi = scratch + (1u << a);
   // lo: last a points (bits 0..a-1), hi: first b points (bits a..n-1)
   hipLaunchKernelGGL(eq_small_kernel, dim3(((1u << a) + 255) / 256), dim3(256), 0, st, pts + b, a,
-                     lo);
-  hipLaunchKernelGGL(eq_small_kernel, dim3(((1u << b) + 255) / 256), dim3(256), 0, st, pts, b, hi);
+                     lo, mono ? 1 : 0);
+  hipLaunchKernelGGL(eq_small_kernel, dim3(((1u << b) + 255) / 256), dim3(256), 0, st, pts, b, hi,
+                     mono ? 1 : 0);
   const uint64_t N = 1ull << n;
   hipLaunchKernelGGL(eq_expand_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, lo, hi,
                      a, N, out);

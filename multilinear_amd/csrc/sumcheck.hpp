@@ -35,7 +35,12 @@ hipError_t launch_sumcheck_tail(fe* m, fe* d, uint32_t log_s, fe* prev, DevSha* 
                                 fe* rs, hipStream_t st);
 hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
                       hipStream_t st);
-hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st);
+// mono: monomial table prod_{bit_i set} p[n-1-i] (coefficient-form MLE evaluation)
+hipError_t launch_eq_table(const fe* pts, uint32_t n, fe* scratch, fe* out, hipStream_t st,
+                           bool mono = false);
+// out[0] = sum_i c[i] * tlo[i mod 4096] * thi[i / 4096] (partials: kMaxRedBlocks pairs)
+hipError_t launch_poly_eval(const fe* c, uint64_t n, const fe* tlo, const fe* thi, fe* partials,
+                            fe* out, hipStream_t st);
 // src (optional): the first pass reads src instead of c (out-of-place transform)
 hipError_t launch_mobius(fe* c, uint32_t log_n, bool inverse_zeta, hipStream_t st,
                          const fe* src = nullptr);

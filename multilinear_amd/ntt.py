@@ -55,6 +55,15 @@ class Polynomial:
     def __init__(self, coeffs):
         self.coeffs = coeffs
 
+    def evaluate(self, x, device=0):
+        """ntt/mod.rs:61-67 (Horner): sum_i coeffs[i] x^i, any length."""
+        ctx = context(device)
+        out = (ctypes.c_uint8 * 16)()
+        n = self.coeffs.shape[0]
+        check(lib().mlh_poly_evaluate(ctx, ptr(self.coeffs) if n else None, n, fe_bytes(x), out),
+              ctx)
+        return fe_from_bytes(out)
+
     def ntt(self, gen, device=0):
         """ntt/mod.rs:69-110: natural order in and out."""
         ctx = context(device)

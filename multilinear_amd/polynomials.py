@@ -39,14 +39,39 @@ def _points(args):
     return (ctypes.c_uint8 * max(1, len(raw))).from_buffer_copy(raw or b"\0")
 
 
+def _padded(t, n):
+    """The reference asserts 1 << len(args) == len.next_power_of_two(): a
+    shorter table sums over its own positions only, i.e. zero padding."""
+    m = t.shape[0]
+    if m < 1 or 1 << n != 1 << (m - 1).bit_length():
+        raise ValueError("Wrong number of arguments")
+    if m == 1 << n:
+        return t
+    import torch
+
+    out = torch.zeros((1 << n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    out[:m] = t
+    return out
+
+
 def evaluate(evals, args, device=0):
     """MultilinearPolynomialEvals::evaluate (polynomials.rs:165-187)."""
     n = len(args)
-    if 1 << n != evals.shape[0]:
-        raise ValueError("Wrong number of arguments")
+    evals = _padded(evals, n)
     ctx = context(device)
     out = (ctypes.c_uint8 * 16)()
     check(lib().mlh_mle_evaluate(ctx, ptr(evals), n, _points(args), out), ctx)
+    return fe_from_bytes(out)
+
+
+def coeffs_evaluate(coeffs, args, device=0):
+    """MultilinearPolynomial::evaluate (polynomials.rs:126-146), coefficient
+    form: sum_pos coeffs[pos] * prod_{bit b of pos set} args[n-1-b]."""
+    n = len(args)
+    coeffs = _padded(coeffs, n)
+    ctx = context(device)
+    out = (ctypes.c_uint8 * 16)()
+    check(lib().mlh_mle_coeffs_evaluate(ctx, ptr(coeffs), n, _points(args), out), ctx)
     return fe_from_bytes(out)
 
 

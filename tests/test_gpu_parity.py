@@ -306,6 +306,37 @@ def test_mle_conversion_any_length(vals):
     assert host(MPL.to_evaluation(c)) == ev
 
 
+@pytest.mark.parametrize("n", [0, 1, 5, 4096, 4097, 12345, 1 << 18])
+def test_poly_evaluate_matches_horner(n):
+    """Polynomial::evaluate (ntt/mod.rs:61-67): sum c_i x^i on the GPU equals
+    the oracle's Horner fold."""
+    c = rand_vals(n, 80 + n % 97)
+    x = rand_vals(1, 81)[0]
+    t = dev(c) if n else D.empty(0)
+    assert MN.Polynomial(t).evaluate(x) == OPL.uni_evaluate(c, x)
+
+
+@pytest.mark.parametrize("m,n", [(1, 0), (2, 1), (6, 3), (8, 3), (1 << 10, 10), (1000, 10)])
+def test_mle_evaluations_any_length(m, n):
+    """MultilinearPolynomial::evaluate (coefficient form, polynomials.rs:126-146)
+    and MultilinearPolynomialEvals::evaluate (:165-187) for len <= 2^n with
+    len.next_power_of_two() == 2^n."""
+    v = rand_vals(m, 90 + m)
+    args = rand_vals(n, 91 + n)
+    assert MPL.coeffs_evaluate(dev(v), args) == OPL.mle_coeffs_evaluate(v, args)
+    assert MPL.evaluate(dev(v), args) == OPL.mle_evaluate(v, args)
+    with pytest.raises(ValueError):
+        MPL.evaluate(dev(v), args + [1])
+
+
+def test_mle_coefficient_and_evaluation_forms_agree():
+    """2^16: evaluate(evals) == coeffs_evaluate(to_coefficient(evals)) on the GPU."""
+    n = 16
+    ev = D.random_device(1 << n, 92)
+    args = rand_vals(n, 93)
+    assert MPL.coeffs_evaluate(MPL.to_coefficient(ev), args) == MPL.evaluate(ev, args)
+
+
 def test_eq_table_and_evaluate():
     for n in (1, 2, 5, 9, 12):
         pts = rand_vals(n, 600 + n)
