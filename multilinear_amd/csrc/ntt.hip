@@ -69,21 +69,24 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 
 // TW: 0 = two-table twiddle (TA * TB), 1 = one table (TA; W <= 2^8), 2 = none (last pass)
 // waves per SIMD the LDS tile allows (160 KiB/CU): caps VGPRs to match
-constexpr int pass_waves_per_simd(int logr) {
-  return logr == 8 ? 5 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2));
+constexpr int pass_waves_per_simd(int logr, int ept) {
+  return ept == 16 ? 2 : (logr == 8 ? 5 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2)));
 }
 
 // ZT: 0 = full input; 1 = input has N/2 elements, upper half implicit zeros
 // (Reed-Solomon); 2 = as 1, with the N/2 inputs stored bit-reversed, i.e.
 // coefficient j is in[bitrev_{log_n - 1}(j)] (the PCS's bit_reverse_permutation
 // folded into pass 0's loads; pass 0 only, never the last pass).
-template <int LOGR, int TW, int ZT>
-__global__ void __launch_bounds__(kCols * (1 << LOGR) / kEPT,
-                                  TW == 2 ? 1 : pass_waves_per_simd(LOGR))
+// EPT: elements per thread (8: register phases of 3 stages; 16: of 4 stages,
+// one LDS exchange fewer at R = 2^8, twice the VGPRs).
+template <int LOGR, int TW, int ZT, int EPT = kEPT>
+__global__ void __launch_bounds__(kCols * (1 << LOGR) / EPT,
+                                  TW == 2 ? 1 : pass_waves_per_simd(LOGR, EPT))
 ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
                 const fe* __restrict__ ta, const fe* __restrict__ tb, PassGeom g) {
   constexpr int R = 1 << LOGR;
-  constexpr int TPC = R / kEPT;  // threads per column
+  constexpr int LQ = EPT == 16 ? 4 : 3;  // stages per register phase
+  constexpr int TPC = R / EPT;  // threads per column
   constexpr bool LAST = TW == 2;
   __shared__ fe lds[R * kCols];
 
@@ -124,20 +127,20 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   fe* dst = out + base + (uint64_t)c * cstride;
 
   // ---- phase 1: load bit-reversed rows, stages 0..2 in registers ---------
-  fe x[kEPT];
+  fe x[EPT];
 #pragma unroll
-  for (int e = 0; e < kEPT; ++e) {
-    const uint32_t row = bitrev((uint32_t)(t * kEPT + e), LOGR);
+  for (int e = 0; e < EPT; ++e) {
+    const uint32_t row = bitrev((uint32_t)(t * EPT + e), LOGR);
     // rows >= R/2 are the implicit zero half; bitrev puts them exactly at odd e
     if (ZT != 0 && (e & 1)) {
       x[e] = fe_zero();
     } else if (ZT == 2) {
       // coefficient row*W + col, row < R/2, lives at bitrev(col)*(R/2) +
-      // bitrev_{LOGR-1}(row) = bitrev(col)*(R/2) + (t*kEPT + e)/2: each lane
+      // bitrev_{LOGR-1}(row) = bitrev(col)*(R/2) + (t*EPT + e)/2: each lane
       // reads 4 consecutive elements
       const uint32_t logw = g.log_n - LOGR;
       const uint64_t colr = __builtin_bitreverse64(jrest) >> (64 - logw);
-      x[e] = fe_load(in + (colr << (LOGR - 1)) + ((uint32_t)(t * kEPT + e) >> 1));
+      x[e] = fe_load(in + (colr << (LOGR - 1)) + ((uint32_t)(t * EPT + e) >> 1));
     } else {
       x[e] = fe_load(src + (uint64_t)row * rstride);
     }
@@ -147,7 +150,7 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   auto run_phase = [&](auto S0_, auto Q_) {
     constexpr int s0 = decltype(S0_)::value;
     constexpr int q = decltype(Q_)::value;
-    constexpr int G = kEPT >> q;
+    constexpr int G = EPT >> q;
 #pragma unroll
     for (int s = s0; s < s0 + q; ++s) {
       const int d = 1 << (s - s0);  // element distance inside a group
@@ -183,10 +186,10 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
       }
     }
   };
-  auto positions = [&](auto S0_, auto Q_, uint32_t (&pos)[kEPT]) {
+  auto positions = [&](auto S0_, auto Q_, uint32_t (&pos)[EPT]) {
     constexpr int s0 = decltype(S0_)::value;
     constexpr int q = decltype(Q_)::value;
-    constexpr int G = kEPT >> q;
+    constexpr int G = EPT >> q;
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
       const uint32_t gamma = (uint32_t)(t * G + gi);
@@ -197,30 +200,29 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   };
 
   using I0 = std::integral_constant<int, 0>;
-  using I3 = std::integral_constant<int, 3>;
-  constexpr int Q1 = LOGR < 3 ? LOGR : 3;
+  constexpr int Q1 = LOGR < LQ ? LOGR : LQ;
   run_phase(I0{}, std::integral_constant<int, Q1>{});
-  uint32_t pos[kEPT];
+  uint32_t pos[EPT];
   positions(I0{}, std::integral_constant<int, Q1>{}, pos);
 
   // ---- remaining phases through LDS -------------------------------------
   auto exchange_and_run = [&](auto S0_, auto Q_) {
     __syncthreads();  // previous phase's reads of lds are done
 #pragma unroll
-    for (int e = 0; e < kEPT; ++e) fe_store(&lds[pos[e] * kCols + c], x[e]);
+    for (int e = 0; e < EPT; ++e) fe_store(&lds[pos[e] * kCols + c], x[e]);
     __syncthreads();
     positions(S0_, Q_, pos);
 #pragma unroll
-    for (int e = 0; e < kEPT; ++e) x[e] = fe_load(&lds[pos[e] * kCols + c]);
+    for (int e = 0; e < EPT; ++e) x[e] = fe_load(&lds[pos[e] * kCols + c]);
     run_phase(S0_, Q_);
   };
-  if constexpr (LOGR > 3) {
-    constexpr int Q2 = (LOGR - 3) < 3 ? (LOGR - 3) : 3;
-    exchange_and_run(I3{}, std::integral_constant<int, Q2>{});
-    if constexpr (LOGR > 6) {
-      constexpr int Q3 = LOGR - 6;
-      static_assert(Q3 <= 3, "LOGR <= 9");
-      exchange_and_run(std::integral_constant<int, 6>{}, std::integral_constant<int, Q3>{});
+  if constexpr (LOGR > LQ) {
+    constexpr int Q2 = (LOGR - LQ) < LQ ? (LOGR - LQ) : LQ;
+    exchange_and_run(std::integral_constant<int, LQ>{}, std::integral_constant<int, Q2>{});
+    if constexpr (LOGR > 2 * LQ) {
+      constexpr int Q3 = LOGR - 2 * LQ;
+      static_assert(Q3 <= LQ, "LOGR <= 3 * LQ");
+      exchange_and_run(std::integral_constant<int, 2 * LQ>{}, std::integral_constant<int, Q3>{});
     }
   }
 
@@ -232,7 +234,7 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     kshift = g.log_n - LOGR;
   }
 #pragma unroll
-  for (int e = 0; e < kEPT; ++e) {
+  for (int e = 0; e < EPT; ++e) {
     const uint64_t k = pos[e];
     fe v = x[e];
     if (!LAST) {
@@ -331,14 +333,15 @@ __global__ void pow_series_kernel(fe* __restrict__ out, const fe* __restrict__ t
 
 // ---- host-side launchers ---------------------------------------------------
 
-template <int LOGR>
-static hipError_t launch_pass(bool last, int zero_top, const fe* in, fe* out, const fe* tw,
-                              const fe* ta, const fe* tb, const PassGeom& g, uint64_t tiles,
-                              hipStream_t st) {
-  constexpr int threads = kCols * (1 << LOGR) / kEPT;
+template <int LOGR, int EPT>
+static hipError_t launch_pass_ept(bool last, int zero_top, const fe* in, fe* out, const fe* tw,
+                                  const fe* ta, const fe* tb, const PassGeom& g, uint64_t tiles,
+                                  hipStream_t st) {
+  constexpr int threads = kCols * (1 << LOGR) / EPT;
   const dim3 grid((unsigned)tiles), blk(threads);
 #define MLH_PASS(TWV, ZTV)                                                                  \
-  hipLaunchKernelGGL((ntt_pass_kernel<LOGR, TWV, ZTV>), grid, blk, 0, st, in, out, tw, ta, tb, g)
+  hipLaunchKernelGGL((ntt_pass_kernel<LOGR, TWV, ZTV, EPT>), grid, blk, 0, st, in, out, tw, ta, \
+                     tb, g)
   if (last) {
     if (zero_top) return hipErrorInvalidValue;  // pass 0 is never the last pass here
     MLH_PASS(2, 0);
@@ -353,6 +356,16 @@ static hipError_t launch_pass(bool last, int zero_top, const fe* in, fe* out, co
   }
 #undef MLH_PASS
   return hipGetLastError();
+}
+
+// EPT = 8 throughout: 16 elements per thread (4-stage register phases, one
+// LDS exchange fewer at R = 2^8) measured 23 % slower for a 2^24 NTT -- 190
+// VGPRs leave 2 waves per SIMD against 5, and the extra ILP does not cover it.
+template <int LOGR>
+static hipError_t launch_pass(bool last, int zero_top, const fe* in, fe* out, const fe* tw,
+                              const fe* ta, const fe* tb, const PassGeom& g, uint64_t tiles,
+                              hipStream_t st) {
+  return launch_pass_ept<LOGR, kEPT>(last, zero_top, in, out, tw, ta, tb, g, tiles, st);
 }
 
 void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr) {
