@@ -366,6 +366,17 @@ mlh_status mlh_sumcheck_fold_and_sums(mlh_ctx* ctx, void* dev_matrix, void* dev_
 mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, uint32_t log_height,
                               const uint8_t sum[16], mlh_transcript* tr, uint8_t* polys_out,
                               uint8_t* rs_out);
+/* SumcheckTables::build_tables_for_pcs (sumcheck.rs:128-145) followed by
+ * compute_sumcheck_polynomials (:77-102), with the delta table = eq(points)
+ * never materialised at full size: it stays c_k * eq(p_k..p_{L-1}) (a running
+ * scalar times a two-level factored table) until it has 2^12 entries.  Same
+ * outputs as mlh_eq_table + mlh_sumcheck_prove; half the HBM traffic.
+ * dev_matrix (2^log_height elements) is folded in place; host_points:
+ * log_height elements; delta_out (optional): the fully folded delta. */
+mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, void* dev_matrix, uint32_t log_height,
+                                 const uint8_t* host_points, const uint8_t sum[16],
+                                 mlh_transcript* tr, uint8_t* polys_out, uint8_t* rs_out,
+                                 uint8_t* delta_out);
 
 /* ---- multilinear PCS (src/fri/multilinear_pcs.rs) ------------------------ */
 typedef struct mlh_pcs_proof {

@@ -1413,6 +1413,122 @@ static mlh_status sumcheck_fold_dr(mlh_ctx* ctx, fe* m, fe* d, uint64_t S, const
   return MLH_OK;
 }
 
+// Sumcheck over SumcheckTables::build_tables_for_pcs (sumcheck.rs:128-145:
+// matrix, delta = eq(points)) with delta kept factored while the tables are
+// larger than 2^a entries (sumcheck.hip, "eq-factored rounds"): rounds
+// k < B = L - a stream only the matrix and carry delta as c_k * eq(p_k..);
+// folding round B-1 writes delta_B = c_B * eq(p_B..p_{L-1}) (2^a entries) and
+// the remaining rounds run the two-table kernels on it.  Round polynomials,
+// challenges and the folded matrix equal those of the materialised tables.
+struct EqSumcheck {
+  static constexpr uint32_t kEqLo = 12;  // = sumcheck_tail_rounds' LDS limit
+  mlh_ctx* ctx;
+  fe* m = nullptr;
+  uint32_t L = 0, a = 0, B = 0;
+  PoolBuf buf;
+  std::vector<uint8_t> host;  // pageable upload source, alive until the caller syncs
+  fe *pts = nullptr, *c = nullptr, *lo = nullptr, *d = nullptr, *H = nullptr, *scratch = nullptr;
+  explicit EqSumcheck(mlh_ctx* c_) : ctx(c_), buf(c_) {}
+
+  mlh_status init(fe* matrix, uint32_t L_, const uint8_t* host_points) {
+    m = matrix;
+    L = L_;
+    a = L < kEqLo ? L : kEqLo;
+    B = L - a;
+    // pts[L] | c | scratch[2^(a/2) + 2^(a - a/2)] | lo[2^a] | d[2^a] | H[2^B - 1]
+    const uint64_t ns = (1ull << (a / 2)) + (1ull << (a - a / 2));
+    MLH_TRY(buf.alloc(16 * (L + 1 + ns + 2 * (1ull << a) + (1ull << B))));
+    pts = buf.as<fe>();
+    c = pts + L;
+    scratch = c + 1;
+    lo = scratch + ns;
+    d = B ? lo + (1ull << a) : lo;  // B == 0: delta is the whole eq table
+    H = lo + 2 * (1ull << a);
+    host.assign(16ull * (L + 1), 0);
+    if (L) memcpy(host.data(), host_points, 16ull * L);
+    host[16ull * L] = 1;  // c_0 = 1
+    HIP_TRY(ctx, hipMemcpyAsync(pts, host.data(), host.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_eq_table(pts + B, a, scratch, lo, ctx->stream));
+    if (B) HIP_TRY(ctx, launch_eq_suffix(pts, B, H, ctx->stream));
+    return MLH_OK;
+  }
+  const fe* Hk(uint32_t k) const { return H + ((1ull << B) - (1ull << (B - k))); }
+
+  // round 0's sums into ctx->partials
+  mlh_status first_sums(uint32_t* np) {
+    if (B)
+      HIP_TRY(ctx, launch_sums_eq(m, 1ull << (L - 1), Hk(0), lo, a, ctx->partials, ctx->stream, np));
+    else
+      HIP_TRY(ctx, launch_sums(m, d, 1ull << (L - 1), ctx->partials, ctx->small, ctx->stream, np));
+    return MLH_OK;
+  }
+  mlh_status round(uint32_t k, uint32_t np, fe* prev, DevSha* dt, fe* poly, fe* r) {
+    HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, prev, dt, poly, r, ctx->stream,
+                                       k < B ? pts + k : nullptr, k < B ? c : nullptr));
+    return MLH_OK;
+  }
+  // fold round k's tables with r (HBM); want_sums: also round k+1's sums
+  mlh_status fold(uint32_t k, const fe* r_dev, uint32_t* np, bool want_sums = true) {
+    const uint64_t S = 1ull << (L - k);
+    if (k + 1 < B) {
+      HIP_TRY(ctx, launch_fold_sums_eq(m, S, r_dev, Hk(k + 1), lo, a, ctx->partials, ctx->stream,
+                                       np));
+    } else if (k + 1 == B) {
+      HIP_TRY(ctx, launch_fold(m, nullptr, S, fe{}, ctx->stream, r_dev));
+      HIP_TRY(ctx, launch_scale_dev(lo, c, 1ull << a, d, ctx->stream));
+      if (want_sums)
+        HIP_TRY(ctx, launch_sums(m, d, 1ull << (a - 1), ctx->partials, ctx->small, ctx->stream, np));
+    } else {
+      MLH_TRY(sumcheck_fold_dr(ctx, m, d, S, r_dev, np));
+    }
+    return MLH_OK;
+  }
+};
+
+mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, void* dev_matrix, uint32_t log_height,
+                                 const uint8_t* host_points, const uint8_t sum[16],
+                                 mlh_transcript* tr, uint8_t* polys_out, uint8_t* rs_out,
+                                 uint8_t* delta_out) {
+  if (!ctx || !dev_matrix || !host_points || !sum || !tr || log_height < 1 || log_height > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  const uint32_t L = log_height;
+  PoolBuf sc(ctx);
+  MLH_TRY(sc.alloc(128 + 16 + 48ull * L));
+  uint8_t* sb = sc.as<uint8_t>();
+  DevSha* dt = reinterpret_cast<DevSha*>(sb);
+  fe* prev = reinterpret_cast<fe*>(sb + 128);
+  fe* polys = reinterpret_cast<fe*>(sb + 144);
+  fe* rs = reinterpret_cast<fe*>(sb + 144 + 32ull * L);
+  memcpy(ctx->pinned, &tr->sha, sizeof(DevSha));
+  memcpy(ctx->pinned + 128, sum, 16);
+  HIP_TRY(ctx, hipMemcpyAsync(sb, ctx->pinned, 144, hipMemcpyHostToDevice, ctx->stream));
+  EqSumcheck es(ctx);
+  MLH_TRY(es.init(reinterpret_cast<fe*>(dev_matrix), L, host_points));
+  // head rounds stream only the matrix; the last a rounds (delta materialised,
+  // 2^a entries) run in the LDS-resident tail launch
+  uint32_t np = 0;
+  if (es.B) MLH_TRY(es.first_sums(&np));
+  for (uint32_t k = 0; k < es.B; ++k) {
+    MLH_TRY(es.round(k, np, prev, dt, polys + 2 * k, rs + k));
+    MLH_TRY(es.fold(k, rs + k, &np, false));
+  }
+  HIP_TRY(ctx, launch_sumcheck_tail(es.m, es.d, es.a, prev, dt, polys + 2 * es.B, rs + es.B,
+                                    ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 48ull * L, es.d, 16, hipMemcpyDeviceToHost,
+                              ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  std::vector<uint8_t> host(ctx->pinned, ctx->pinned + 48ull * L + 16);
+  for (uint32_t k = 0; k < L; ++k) {  // host transcript replay (sumcheck.rs:188-199)
+    mlh_transcript_absorb(tr, host.data() + 32 * k, 16);
+    mlh_transcript_absorb(tr, host.data() + 32 * k + 16, 16);
+  }
+  if (polys_out) memcpy(polys_out, host.data(), 32ull * L);
+  if (rs_out) memcpy(rs_out, host.data() + 32ull * L, 16ull * L);
+  if (delta_out) memcpy(delta_out, host.data() + 48ull * L, 16);
+  return MLH_OK;
+}
+
 mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
                          const uint8_t* host_inputs, const uint8_t output[16], mlh_transcript* tr,
                          mlh_pcs_proof* proof) {
@@ -1424,11 +1540,10 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   const u128 gen = h_pow2_generator(log_domain);  // gen_pows[1] (multilinear_pcs.rs:103-104)
   uint8_t genb[16];
   h_store(genb, gen);
-  PoolBuf coeffs(ctx), code(ctx), matrix(ctx), delta(ctx);
+  PoolBuf coeffs(ctx), code(ctx), matrix(ctx);
   MLH_TRY(coeffs.alloc(n * 16));
   MLH_TRY(code.alloc(2 * n * 16));
   MLH_TRY(matrix.alloc(n * 16));
-  MLH_TRY(delta.alloc(n * 16));
   // to_coefficient (:102), bit reverse (:104), reed_solomon (:107); the copy
   // and the permutation are folded into the Moebius and first NTT passes
   HIP_TRY(ctx, launch_mobius(coeffs.as<fe>(), n_vars, false, ctx->stream,
@@ -1443,19 +1558,16 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   FriDevLoop lp(ctx, fp.get());
   MLH_TRY(lp.init(code.p, log_domain, tr, false));
   HIP_TRY(ctx, hipMemcpyAsync(matrix.p, dev_evals, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
-  MLH_TRY(mlh_eq_table(ctx, host_inputs, n_vars, delta.p));
+  EqSumcheck es(ctx);  // delta = eq(inputs), factored (build_tables_for_pcs)
+  MLH_TRY(es.init(matrix.as<fe>(), n_vars, host_inputs));
   memcpy(ctx->pinned + 3072, output, 16);
   HIP_TRY(ctx, hipMemcpyAsync(lp.prev(), ctx->pinned + 3072, 16, hipMemcpyHostToDevice,
                               ctx->stream));
-  fe* sums = ctx->small;
   uint32_t np = 0;
-  HIP_TRY(ctx, launch_sums(matrix.as<fe>(), delta.as<fe>(), n / 2, ctx->partials, sums,
-                           ctx->stream, &np));
+  MLH_TRY(es.first_sums(&np));
   for (uint32_t k = 0; k < n_vars; ++k) {
-    HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
-                                       ctx->stream));
-    MLH_TRY(sumcheck_fold_dr(ctx, matrix.as<fe>(), delta.as<fe>(), 1ull << (n_vars - k), lp.r(k),
-                             &np));
+    MLH_TRY(es.round(k, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k)));
+    MLH_TRY(es.fold(k, lp.r(k), &np));
     MLH_TRY(lp.step(k, lp.r(k), false));
   }
   MLH_TRY(lp.finish(32ull * n_vars));
@@ -1885,11 +1997,10 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   uint8_t genb[16];
   h_store(genb, h_pow2_generator(log_domain));
   // codes: to_coefficient, bit reverse, RS per polynomial (batched_pcs.rs:137-146)
-  PoolBuf coeffs(ctx), codes(ctx), matrix(ctx), delta(ctx), outs(ctx);
+  PoolBuf coeffs(ctx), codes(ctx), matrix(ctx), outs(ctx);
   MLH_TRY(coeffs.alloc(n * 16));
   MLH_TRY(codes.alloc((uint64_t)num_polys * N * 16));
   MLH_TRY(matrix.alloc(n * 16));
-  MLH_TRY(delta.alloc(n * 16));
   MLH_TRY(outs.alloc(16ull * num_polys));
   const uint8_t* ev = reinterpret_cast<const uint8_t*>(dev_evals);
   for (uint32_t j = 0; j < num_polys; ++j) {
@@ -1909,22 +2020,19 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   // fingerprinted MLE + eq table; previous_sum = fingerprint(fr, outputs)
   HIP_TRY(ctx, launch_fingerprint(reinterpret_cast<const fe*>(dev_evals), num_polys, n, lp.fr(),
                                   matrix.as<fe>(), ctx->stream));
-  MLH_TRY(mlh_eq_table(ctx, inputs, n_vars, delta.p));
+  EqSumcheck es(ctx);  // delta = eq(inputs), factored
+  MLH_TRY(es.init(matrix.as<fe>(), n_vars, inputs));
   {
     std::vector<uint8_t> ob(outputs, outputs + 16ull * num_polys);
     HIP_TRY(ctx, hipMemcpyAsync(outs.p, ob.data(), ob.size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // ob is pageable and goes out of scope
   }
   HIP_TRY(ctx, launch_fingerprint_scalar(outs.as<fe>(), num_polys, lp.fr(), lp.prev(), ctx->stream));
-  fe* sums = ctx->small;
   uint32_t np = 0;
-  HIP_TRY(ctx, launch_sums(matrix.as<fe>(), delta.as<fe>(), n / 2, ctx->partials, sums,
-                           ctx->stream, &np));
+  MLH_TRY(es.first_sums(&np));
   for (uint32_t k = 0; k < n_vars; ++k) {  // fold (batched_pcs.rs:80-125)
-    HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k),
-                                       ctx->stream));
-    MLH_TRY(sumcheck_fold_dr(ctx, matrix.as<fe>(), delta.as<fe>(), 1ull << (n_vars - k), lp.r(k),
-                             &np));
+    MLH_TRY(es.round(k, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k)));
+    MLH_TRY(es.fold(k, lp.r(k), &np));
     if (k == 0)
       MLH_TRY(lp.step_batched(lp.r(0), false));
     else

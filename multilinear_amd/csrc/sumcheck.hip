@@ -119,7 +119,101 @@ fold_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r,
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= h) return;
   fe_store(m + i, lerp(fe_load(m + i), fe_load(m + i + h), r));
-  fe_store(d + i, lerp(fe_load(d + i), fe_load(d + i + h), r));
+  if (d) fe_store(d + i, lerp(fe_load(d + i), fe_load(d + i + h), r));  // d == null: m only
+}
+
+// ---- eq-factored rounds (delta never materialised) ---------------------------
+// For the PCS tables delta = eq(p) (big-endian, sumcheck.rs:128-145) the fold
+// keeps delta an eq table: folding the MSB variable (point p_k) with r gives
+//   delta_{k+1}[i] = ((1-r)(1-p_k) + r p_k) * eq(p_{k+1..})[i],
+// so round k's delta is c_k * eq(p_k, ..., p_{L-1}) with a running scalar c_k.
+// Its halves are d[i] = c_k (1-p_k) e(i), d[i+h] = c_k p_k e(i) with
+// e = eq(p_{k+1..}) over h entries, hence (composition x[0])
+//   s1 = c_k p_k E1,  s2 = c_k (3 p_k - 1)(2 E1 - E0),
+//   E0 = sum_{i<h} m[i] e(i),  E1 = sum_{i<h} m[i+h] e(i),
+// and e(i) = H_k[i >> a] * lo[i mod 2^a] (lo = eq of the last a points, H_k =
+// eq(p_{k+1}..p_{L-a-1})).  The kernels stream only m: half the HBM traffic of
+// the two-table rounds, and no 2^L eq table is ever written.  Thread counts are
+// powers of two >= 2^a, so a thread's i mod 2^a is fixed: it accumulates
+// m[i] * H[i >> a] and multiplies by lo once at the end (2 modmuls per pair).
+
+// H_k for k = 0..B-1 concatenated: H_k = eq(p_{k+1}, ..., p_{B-1}) has
+// 2^(B-1-k) entries at offset 2^B - 2^(B-k); entry j = prod_{i < B-1-k}
+// (bit_i(j) ? p[B-1-i] : 1 - p[B-1-i]).
+__global__ void eq_suffix_kernel(const fe* __restrict__ pts, uint32_t B, fe* __restrict__ out) {
+  const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t total = (1ull << B) - 1;
+  if (x >= total) return;
+  const uint64_t y = (1ull << B) - x;                  // >= 2
+  const uint32_t clog = 64 - __builtin_clzll(y - 1);   // ceil(log2 y)
+  const uint32_t k = B - clog;
+  const uint64_t j = x - ((1ull << B) - (1ull << (B - k)));
+  const uint32_t cnt = B - 1 - k;
+  fe acc = fe_one();
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const fe p = pts[B - 1 - i];
+    acc = fe_mul(acc, ((j >> i) & 1) ? p : fe_sub(fe_one(), p));
+  }
+  fe_store(out + x, acc);
+}
+
+__global__ void __launch_bounds__(kRedThreads)
+sums_eq_kernel(const fe* __restrict__ m, uint64_t h, const fe* __restrict__ H,
+               const fe* __restrict__ lo, uint32_t a, fe* __restrict__ partials) {
+  fe e0 = fe_zero(), e1 = fe_zero();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;  // power of two >= 2^a
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t i = i0; i < h; i += stride) {
+    const fe hv = fe_load(H + (i >> a));
+    e0 = fe_add(e0, fe_mul(fe_load(m + i), hv));
+    e1 = fe_add(e1, fe_mul(fe_load(m + i + h), hv));
+  }
+  const fe l = fe_load(lo + (i0 & ((1ull << a) - 1)));
+  e0 = fe_mul(e0, l);
+  e1 = fe_mul(e1, l);
+  block_reduce2(e0, e1);
+  if (threadIdx.x == 0) {
+    fe_store(partials + 2 * blockIdx.x, e0);
+    fe_store(partials + 2 * blockIdx.x + 1, e1);
+  }
+}
+
+// fold m (size S) with r, then the eq-factored sums of the folded table
+// (h' = S/4, next round's H table).
+__global__ void __launch_bounds__(kRedThreads)
+fold_sums_eq_kernel(fe* __restrict__ m, uint64_t S, const fe* __restrict__ rp,
+                    const fe* __restrict__ H, const fe* __restrict__ lo, uint32_t a,
+                    fe* __restrict__ partials) {
+  const fe r = fe_load(rp);
+  const uint64_t h = S / 2, q = S / 4;
+  fe e0 = fe_zero(), e1 = fe_zero();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t i = i0; i < q; i += stride) {
+    const fe ma = fe_load(m + i), mb = fe_load(m + i + q);
+    const fe mc = fe_load(m + i + h), md = fe_load(m + i + h + q);
+    const fe hv = fe_load(H + (i >> a));
+    const fe m0 = lerp(ma, mc, r), m1 = lerp(mb, md, r);
+    fe_store(m + i, m0);
+    fe_store(m + i + q, m1);
+    e0 = fe_add(e0, fe_mul(m0, hv));
+    e1 = fe_add(e1, fe_mul(m1, hv));
+  }
+  const fe l = fe_load(lo + (i0 & ((1ull << a) - 1)));
+  e0 = fe_mul(e0, l);
+  e1 = fe_mul(e1, l);
+  block_reduce2(e0, e1);
+  if (threadIdx.x == 0) {
+    fe_store(partials + 2 * blockIdx.x, e0);
+    fe_store(partials + 2 * blockIdx.x + 1, e1);
+  }
+}
+
+// out[i] = c * src[i], c read from HBM (the running eq scale c_k)
+__global__ void scale_dev_kernel(const fe* __restrict__ src, const fe* __restrict__ c, uint64_t n,
+                                 fe* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) fe_store(out + i, fe_mul(fe_load(c), fe_load(src + i)));
 }
 
 __global__ void __launch_bounds__(kRedThreads)
@@ -315,6 +409,42 @@ hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe*
   return hipGetLastError();
 }
 
+// thread count for the eq-factored kernels: a power of two >= 2^a (work >= 2^a)
+static inline unsigned eq_blocks(uint64_t work) { return red_blocks(work); }
+
+hipError_t launch_eq_suffix(const fe* pts, uint32_t B, fe* H, hipStream_t st) {
+  const uint64_t total = (1ull << B) - 1;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(eq_suffix_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, pts,
+                     B, H);
+  return hipGetLastError();
+}
+
+hipError_t launch_sums_eq(const fe* m, uint64_t h, const fe* H, const fe* lo, uint32_t a,
+                          fe* partials, hipStream_t st, uint32_t* nparts) {
+  if (h < (1ull << a) || a < 8) return hipErrorInvalidValue;  // stride must be a multiple of 2^a
+  const unsigned nb = eq_blocks(h);
+  hipLaunchKernelGGL(sums_eq_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, h, H, lo, a, partials);
+  *nparts = nb;
+  return hipGetLastError();
+}
+
+hipError_t launch_fold_sums_eq(fe* m, uint64_t S, const fe* r_dev, const fe* H, const fe* lo,
+                               uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts) {
+  if (S / 4 < (1ull << a) || a < 8) return hipErrorInvalidValue;
+  const unsigned nb = eq_blocks(S / 4);
+  hipLaunchKernelGGL(fold_sums_eq_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, S, r_dev, H, lo, a,
+                     partials);
+  *nparts = nb;
+  return hipGetLastError();
+}
+
+hipError_t launch_scale_dev(const fe* src, const fe* c, uint64_t n, fe* out, hipStream_t st) {
+  hipLaunchKernelGGL(scale_dev_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, c,
+                     n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_poly_eval(const fe* c, uint64_t n, const fe* tlo, const fe* thi, fe* partials,
                             fe* out, hipStream_t st) {
   const unsigned nb = red_blocks(n);
@@ -417,9 +547,12 @@ namespace mlh {
 // interpolation on x = 0,1,2 (polynomials.rs:51-87): e0 = prev - s1,
 // c2 = (s2 - 2 s1 + e0) / 2, c1 = s1 - e0 - c2; absorb LE16(c1), LE16(c2)
 // (sumcheck.rs:188-199), r = next_challenge(), prev = e0 + r (c1 + c2 r).
+// pk != null: eq-factored round (partials hold (E0, E1); s1 = c p_k E1,
+// s2 = c (3 p_k - 1)(2 E1 - E0)), and the scale advances to
+// c <- c ((1 - r)(1 - p_k) + r p_k) once r is known.
 __global__ void __launch_bounds__(kRedThreads)
 sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev, DevSha* t,
-                      fe* poly_out, fe* r_out) {
+                      fe* poly_out, fe* r_out, const fe* __restrict__ pk, fe* cdev) {
   __shared__ DevSha s;
   // the round sums: reduce the per-workgroup partials (loads unrolled so a
   // lane's few loads are in flight together), then one lane runs the round
@@ -431,6 +564,15 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
   }
   block_reduce2(s1, s2);
   if (threadIdx.x != 0) return;
+  fe c, pv;
+  if (pk) {
+    c = fe_load(cdev);
+    pv = fe_load(pk);
+    const fe E0 = s1, E1 = s2;
+    const fe three_p_1 = fe_sub(fe_add(fe_dbl(pv), pv), fe_one());
+    s1 = fe_mul(fe_mul(c, pv), E1);
+    s2 = fe_mul(fe_mul(c, three_p_1), fe_sub(fe_dbl(E1), E0));
+  }
   const fe p = fe_load(prev);
   const fe e0 = fe_sub(p, s1);
   const fe c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
@@ -443,6 +585,10 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
   const fe r = dsha_challenge(s);
   fe_store(r_out, r);
   fe_store(prev, fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r)))));
+  if (pk) {  // (1 - r)(1 - p) + r p = 1 - p - r + 2 r p
+    const fe f = fe_add(fe_sub(fe_sub(fe_one(), pv), r), fe_dbl(fe_mul(r, pv)));
+    fe_store(cdev, fe_mul(c, f));
+  }
 }
 
 // The last rounds of a device-resident sumcheck (tables of S <= kTailMax
@@ -526,9 +672,9 @@ hipError_t launch_sumcheck_tail(fe* m, fe* d, uint32_t log_s, fe* prev, DevSha* 
 }
 
 hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, DevSha* t,
-                                 fe* poly_out, fe* r_out, hipStream_t st) {
+                                 fe* poly_out, fe* r_out, hipStream_t st, const fe* pk, fe* c) {
   hipLaunchKernelGGL(sumcheck_round_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nparts,
-                     prev, t, poly_out, r_out);
+                     prev, t, poly_out, r_out, pk, c);
   return hipGetLastError();
 }
 

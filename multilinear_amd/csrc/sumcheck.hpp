@@ -20,8 +20,22 @@ hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe*
 struct DevSha;
 // one sumcheck round on the device: reduce the nparts partial sum pairs,
 // interpolate, absorb, challenge, new claim
+// pk/c non-null: eq-factored round (partials are (E0, E1), see sums_eq_kernel;
+// *c is the running eq scale, advanced with r)
 hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, DevSha* t,
-                                 fe* poly_out, fe* r_out, hipStream_t st);
+                                 fe* poly_out, fe* r_out, hipStream_t st,
+                                 const fe* pk = nullptr, fe* c = nullptr);
+// eq-factored sumcheck (delta = c_k eq(p_k..p_{L-1}) never materialised):
+// H_k tables for k < B (concatenated, H_k at offset 2^B - 2^(B-k)); sums of
+// round k over m (h = half size) with e(i) = H_k[i >> a] lo[i mod 2^a]; fold
+// with r (HBM) + the next round's sums.  Require half sizes >= 2^a, a >= 8.
+hipError_t launch_eq_suffix(const fe* pts, uint32_t B, fe* H, hipStream_t st);
+hipError_t launch_sums_eq(const fe* m, uint64_t h, const fe* H, const fe* lo, uint32_t a,
+                          fe* partials, hipStream_t st, uint32_t* nparts);
+hipError_t launch_fold_sums_eq(fe* m, uint64_t S, const fe* r_dev, const fe* H, const fe* lo,
+                               uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts);
+// out[i] = (*c) * src[i]
+hipError_t launch_scale_dev(const fe* src, const fe* c, uint64_t n, fe* out, hipStream_t st);
 // Trace::evaluate: out[j] = sum_i eq[i] * m[i * width + j], j < width;
 // partials: trace_eval_blocks(height, min(width, 256)) * min(width, 256) elements.
 uint32_t trace_eval_blocks(uint64_t height, uint32_t ncols);

@@ -2,22 +2,35 @@
 composition x[0], width 1, on the MI355X (tables folded in place)."""
 import ctypes
 
-from .device import check, context, fe_bytes, fe_from_bytes, lib, ptr
-from .polynomials import eq_table
+from .device import check, context, fe_bytes, fe_from_bytes, ints_to_limbs, lib, ptr, to_device
+from .polynomials import _points, eq_table
 from .transcript import Transcript
 
 
 class SumcheckTables:
     def __init__(self, matrix, delta):
         self.matrix = matrix
-        self.delta = delta
+        self._delta = delta
+        self._points = None  # set by build_tables_for_pcs: delta = eq(points), unbuilt
+        self._device = 0
         self.height = matrix.shape[0]
 
     @staticmethod
     def build_tables_for_pcs(inputs, evals, device=0):
-        """sumcheck.rs:128-145 (matrix = evals clone, delta = eq table)."""
+        """sumcheck.rs:128-145 (matrix = evals clone, delta = eq table).  The
+        delta table is built on first access; compute_sumcheck_polynomials on
+        fresh tables never builds it (mlh_sumcheck_prove_eq keeps it factored)."""
         assert 1 << len(inputs) == evals.shape[0]
-        return SumcheckTables(evals.clone(), eq_table(inputs, device))
+        t = SumcheckTables(evals.clone(), None)
+        t._points = list(inputs)
+        t._device = device
+        return t
+
+    @property
+    def delta(self):
+        if self._delta is None:
+            self._delta = eq_table(self._points, self._device)
+        return self._delta
 
     def _lh(self):
         return self.height.bit_length() - 1
@@ -44,8 +57,15 @@ class SumcheckTables:
         n = self._lh()
         polys = (ctypes.c_uint8 * (32 * n))()
         rs = (ctypes.c_uint8 * (16 * n))()
-        check(lib().mlh_sumcheck_prove(ctx, ptr(self.matrix), ptr(self.delta), n,
-                                       fe_bytes(total_sum), transcript.h, polys, rs), ctx)
+        if self._delta is None:  # delta = eq(points), still unbuilt: factored rounds
+            dl = (ctypes.c_uint8 * 16)()
+            check(lib().mlh_sumcheck_prove_eq(ctx, ptr(self.matrix), n, _points(self._points),
+                                              fe_bytes(total_sum), transcript.h, polys, rs, dl),
+                  ctx)
+            self._delta = to_device(ints_to_limbs([fe_from_bytes(dl)]), device)
+        else:
+            check(lib().mlh_sumcheck_prove(ctx, ptr(self.matrix), ptr(self._delta), n,
+                                           fe_bytes(total_sum), transcript.h, polys, rs), ctx)
         self.height = 1
         P, R = bytes(polys), bytes(rs)
         return ([(fe_from_bytes(P[32 * k:32 * k + 16]), fe_from_bytes(P[32 * k + 16:32 * k + 32]))

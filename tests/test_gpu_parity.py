@@ -400,11 +400,15 @@ def test_sumcheck_rounds_match_oracle():
     assert tr.random() == otr.random()
 
 
-@pytest.mark.parametrize("n", [1, 2, 12, 13, 15])
-def test_sumcheck_prove_matches_oracle(n):
+@pytest.mark.parametrize("factored", [True, False])
+@pytest.mark.parametrize("n", [1, 2, 12, 13, 15, 16])
+def test_sumcheck_prove_matches_oracle(n, factored):
     """Device-resident prove around the LDS tail (sumcheck_tail_kernel takes the
     last min(n, 12) rounds): polys, challenges, transcript and the folded
-    tables (in place, as SumcheckTables::fold leaves them) vs the oracle."""
+    tables (in place, as SumcheckTables::fold leaves them) vs the oracle.
+    factored: fresh build_tables_for_pcs tables (mlh_sumcheck_prove_eq: delta
+    kept as c_k * eq(p_k..) for the first n - 12 rounds); otherwise the delta
+    table is materialised first (mlh_sumcheck_prove, two-table rounds)."""
     ev = rand_vals(1 << n, 60 + n)
     pts = rand_vals(n, 61 + n)
     total = OPL.mle_evaluate(ev, pts)
@@ -417,6 +421,8 @@ def test_sumcheck_prove_matches_oracle(n):
         want_polys.append(tuple(nz))
         want_rs.append(r2)
     mt = MS.SumcheckTables.build_tables_for_pcs(pts, dev(ev))
+    if not factored:
+        mt.delta  # noqa: B018 -- materialise the eq table
     tr = Transcript()
     tr.absorb(b"tail")
     polys, rs = mt.compute_sumcheck_polynomials(total, tr)
@@ -425,7 +431,7 @@ def test_sumcheck_prove_matches_oracle(n):
     assert host(mt.matrix)[0] == ot.matrix[0] and host(mt.delta)[0] == ot.delta[0]
 
 
-@pytest.mark.parametrize("n", [1, 2, 8, 10])
+@pytest.mark.parametrize("n", [1, 2, 8, 10, 13, 14, 16])
 def test_pcs_prove_matches_oracle(n):
     """multilinear_pcs_bench_test pattern: evals 7i+3, point (0..n)."""
     ev = [F.from_i64(7 * i + 3) for i in range(1 << n)]
@@ -455,7 +461,46 @@ def test_pcs_random_point():
     assert not bad.verify(Transcript())
 
 
+def test_pcs_random_point_factored_rounds():
+    """n = 15: three eq-factored sumcheck rounds before delta is materialised."""
+    n = 15
+    ev = rand_vals(1 << n, 23)
+    inputs = rand_vals(n, 24)
+    out = OPL.mle_evaluate(ev, inputs)
+    got = MP.PCSProof.prove(inputs, out, dev(ev), Transcript())
+    want = OP.PCSProof.prove(inputs, out, ev, OT.Transcript())
+    assert got.sumcheck_polynomials == [tuple(p) for p in want.sumcheck_polynomials]
+    assert got.fri_proof.last_random == want.fri_proof.last_random
+    assert got.verify(Transcript())
+
+
 # ---- full-size properties (BASELINE configs) ----------------------------------
+
+def test_sumcheck_factored_equals_two_table_full_size():
+    """Config 4 size class (2^22 here): the eq-factored prove and the two-table
+    prove over the materialised eq table give the same round polynomials,
+    challenges, transcript, folded matrix and folded delta."""
+    n = 22
+    x = D.random_device(1 << n, 77)
+    pts = rand_vals(n, 78)
+    total = MPL.evaluate(x, pts)
+    a = MS.SumcheckTables.build_tables_for_pcs(pts, x)
+    b = MS.SumcheckTables.build_tables_for_pcs(pts, x)
+    b.delta  # noqa: B018
+    ta, tb = Transcript(), Transcript()
+    pa, ra = a.compute_sumcheck_polynomials(total, ta)
+    pb, rb = b.compute_sumcheck_polynomials(total, tb)
+    assert pa == pb and ra == rb
+    assert ta.random() == tb.random()
+    assert host(a.matrix)[0] == host(b.matrix)[0]
+    assert host(a.delta)[0] == host(b.delta)[0]
+    # the round chain closes: p_k(0) + p_k(1) = previous claim (c0 = e0 here)
+    prev = total
+    for (c1, c2), r in zip(pa, ra):
+        e0 = (prev - (c1 + c2)) * pow(2, -1, F.M) % F.M
+        prev = (e0 + r * (c1 + c2 * r)) % F.M
+    assert prev == host(a.matrix)[0] * host(a.delta)[0] % F.M
+
 
 def _sum_mod(t):
     a = D.from_device(t).astype(np.uint64)
@@ -734,7 +779,7 @@ def test_batched_fri_large_verifies():
     assert p.verify()
 
 
-@pytest.mark.parametrize("m,n", [(3, 5), (1, 4), (2, 1), (10, 7)])
+@pytest.mark.parametrize("m,n", [(3, 5), (1, 4), (2, 1), (10, 7), (2, 13)])
 def test_batched_pcs_prove_matches_oracle(m, n):
     from multilinear_amd.batched import BatchedPCSProof
     from oracle import batched as OB
