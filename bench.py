@@ -133,7 +133,8 @@ def load_valu(kernel):
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        k = d.get("kernels", {}).get(name)
+        ks = d.get("kernels", {})
+        k = ks.get(name) or ks.get(name[:-1] + ", 8>")  # EPT template argument (r01e on)
         if k and d.get("log_n", 24) == 24:
             return k["SQ_INSTS_VALU"], os.path.basename(path)
     return None

@@ -225,16 +225,17 @@ static mlh_status get_table(mlh_ctx* ctx, u128 base, uint64_t count, u128 scale,
 
 // 2D table[k * cols + j] = base^(k j mult) * scale, k < rows, cached per context
 static mlh_status get_table2d(mlh_ctx* ctx, u128 base, uint64_t rows, uint64_t cols,
-                              uint64_t mult, u128 scale, const fe** out) {
-  TableKey k{base, rows, scale, 0, cols, mult};
+                              uint64_t mult, u128 scale, const fe** out, bool expand = false) {
+  TableKey k{base, rows, scale, expand ? 1 : 0, cols, mult};
   auto it = ctx->tables.find(k);
   if (it != ctx->tables.end()) {
     *out = it->second;
     return MLH_OK;
   }
   fe* d = nullptr;
-  HIP_TRY(ctx, hipMalloc(&d, rows * cols * sizeof(fe)));
-  HIP_TRY(ctx, launch_pow_table2d(d, to_fe(base), to_fe(scale), rows, cols, mult, ctx->stream));
+  HIP_TRY(ctx, hipMalloc(&d, rows * cols * sizeof(fe) * (expand ? 4 : 1)));
+  HIP_TRY(ctx, launch_pow_table2d(d, to_fe(base), to_fe(scale), rows, cols, mult, ctx->stream,
+                                  expand));
   ctx->tables[k] = d;
   *out = d;
   return MLH_OK;
@@ -269,10 +270,12 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
     const uint32_t loga = logw < kTwLogA ? logw : kTwLogA;
     const u128 ws = h_pow(w, S);
     tb->loga[p] = loga;
-    MLH_TRY(get_table2d(ctx, ws, R, 1ull << loga, 1, p == 0 ? scale : (u128)1, &tb->ta[p]));
+    MLH_TRY(get_table2d(ctx, ws, R, 1ull << loga, 1, p == 0 ? scale : (u128)1, &tb->ta[p],
+                        MLH_XTW));
     tb->tb[p] = nullptr;
     if (logw > loga)
-      MLH_TRY(get_table2d(ctx, ws, R, 1ull << (logw - loga), 1ull << loga, 1, &tb->tb[p]));
+      MLH_TRY(get_table2d(ctx, ws, R, 1ull << (logw - loga), 1ull << loga, 1, &tb->tb[p],
+                          MLH_XTW));
     S <<= tb->logr[p];
   }
   return MLH_OK;

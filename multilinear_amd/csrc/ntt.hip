@@ -69,8 +69,14 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 
 // TW: 0 = two-table twiddle (TA * TB), 1 = one table (TA; W <= 2^8), 2 = none (last pass)
 // waves per SIMD the LDS tile allows (160 KiB/CU): caps VGPRs to match
+#ifndef MLH_WPS8
+#define MLH_WPS8 5
+#endif
+#ifndef MLH_LDS_PAD
+#define MLH_LDS_PAD 0  // extra dynamic LDS per pass workgroup (occupancy experiments)
+#endif
 constexpr int pass_waves_per_simd(int logr, int ept) {
-  return ept == 16 ? 2 : (logr == 8 ? 5 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2)));
+  return ept == 16 ? 2 : (logr == 8 ? MLH_WPS8 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2)));
 }
 
 // ZT: 0 = full input; 1 = input has N/2 elements, upper half implicit zeros
@@ -241,8 +247,13 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
       // w_S^(jrest k) = TA[k][jl] * TB[k][jh]: the 8 columns of a tile are
       // 8 consecutive jl, so a wave's lanes read 8 runs of 128 B per table
       const uint64_t jl = jrest & ((1ull << g.loga) - 1);
+#if MLH_XTW
+      v = fe_mul_pre(v, ta + 4 * ((k << g.loga) + jl));
+      if (TW == 0) v = fe_mul_pre(v, tb + 4 * (k * (g.stride >> g.loga) + (jrest >> g.loga)));
+#else
       v = fe_mul(v, ta[(k << g.loga) + jl]);
       if (TW == 0) v = fe_mul(v, tb[k * (g.stride >> g.loga) + (jrest >> g.loga)]);
+#endif
       fe_store(dst + k * rstride, v);
     } else {
       fe_store(out + kbase + (k << kshift), v);
@@ -306,19 +317,29 @@ __global__ void pow_table_kernel(fe* __restrict__ out, fe base, fe scale, uint64
 }
 
 // 2D table out[k * cols + j] = base^(k * j * mult) * scale (inter-pass twiddles).
+// expand: entry t is the 4 limb-shifted multiples (fe_mul_pre), as pow_table.
 __global__ void pow_table2d_kernel(fe* __restrict__ out, fe base, fe scale, uint64_t rows,
-                                   uint64_t cols, uint64_t mult) {
+                                   uint64_t cols, uint64_t mult, int expand) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= rows * cols) return;
   const uint64_t k = t / cols, j = t % cols;
-  fe_store(out + t, fe_mul(fe_pow(base, k * j * mult), scale));
+  fe v = fe_mul(fe_pow(base, k * j * mult), scale);
+  if (!expand) {
+    fe_store(out + t, v);
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    fe_store(out + 4 * t + q, v);
+    v = fe_mul(v, fe{{0u, 1u, 0u, 0u}});  // * 2^32
+  }
 }
 
 hipError_t launch_pow_table2d(fe* out, fe base, fe scale, uint64_t rows, uint64_t cols,
-                              uint64_t mult, hipStream_t st) {
+                              uint64_t mult, hipStream_t st, bool expand) {
   const uint64_t n = rows * cols;
   hipLaunchKernelGGL(pow_table2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out,
-                     base, scale, rows, cols, mult);
+                     base, scale, rows, cols, mult, expand ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -340,8 +361,8 @@ static hipError_t launch_pass_ept(bool last, int zero_top, const fe* in, fe* out
   constexpr int threads = kCols * (1 << LOGR) / EPT;
   const dim3 grid((unsigned)tiles), blk(threads);
 #define MLH_PASS(TWV, ZTV)                                                                  \
-  hipLaunchKernelGGL((ntt_pass_kernel<LOGR, TWV, ZTV, EPT>), grid, blk, 0, st, in, out, tw, ta, \
-                     tb, g)
+  hipLaunchKernelGGL((ntt_pass_kernel<LOGR, TWV, ZTV, EPT>), grid, blk, MLH_LDS_PAD, st, in, out, \
+                     tw, ta, tb, g)
   if (last) {
     if (zero_top) return hipErrorInvalidValue;  // pass 0 is never the last pass here
     MLH_PASS(2, 0);

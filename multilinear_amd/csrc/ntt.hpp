@@ -8,6 +8,9 @@
 namespace mlh {
 
 constexpr int kMaxPasses = 6;
+#ifndef MLH_XTW
+#define MLH_XTW 0  // inter-pass twiddles as expanded tables (fe_mul_pre)
+#endif
 constexpr uint32_t kTwLogA = 8;  // inter-pass twiddle split: TA covers 2^8 columns
 
 // Device twiddle tables for one (log_n, generator, direction).
@@ -48,7 +51,7 @@ void ntt_pass_label(const NttTables& tb, uint32_t p, int zero_top, char* buf, si
 hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st,
                             bool expand = false);
 hipError_t launch_pow_table2d(fe* out, fe base, fe scale, uint64_t rows, uint64_t cols,
-                              uint64_t mult, hipStream_t st);
+                              uint64_t mult, hipStream_t st, bool expand = false);
 hipError_t launch_pow_series(fe* out, const fe* tlo, const fe* thi, uint64_t count,
                              hipStream_t st);
 

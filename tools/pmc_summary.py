@@ -26,6 +26,13 @@ def prefix(label):
     return "void mlh::ntt_pass_kernel<%s, %s, %s>" % (r, tw, z)  # ZT is an int template arg
 
 
+def norm(kernel_name):
+    """rocprof kernel name -> prefix() form (drops the argument list and the
+    EPT = 8 template argument: "ntt_pass_kernel<8, 0, 0, 8>" -> "<8, 0, 0>")"""
+    k = kernel_name.split("(")[0]
+    return k[:-len(", 8>")] + ">" if k.endswith(", 8>") else k
+
+
 def per_kernel(path, counter):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
@@ -48,8 +55,8 @@ def main():
            "alg_bytes_per_launch": 32 * (1 << log_n), "kernels": {}}
     for label in LABELS:
         pre = prefix(label)
-        fk = [v for k, vs in fetch.items() if k.startswith(pre) for v in vs]
-        wk = [v for k, vs in write.items() if k.startswith(pre) for v in vs]
+        fk = [v for k, vs in fetch.items() if norm(k) == pre for v in vs]
+        wk = [v for k, vs in write.items() if norm(k) == pre for v in vs]
         if not fk or not wk:
             continue
         f_kib = sum(fk) / len(fk)

@@ -20,6 +20,12 @@ for rep in range(3):
     torch.cuda.synchronize(); t3 = time.perf_counter()
     print("eq %.3f ms  sumcheck %.3f ms" % ((t1 - t0) * 1e3, (t3 - t2) * 1e3), flush=True)
     time.sleep(0.01)
+    tabs = MS.SumcheckTables.build_tables_for_pcs(pts, x)
+    torch.cuda.synchronize(); t0 = time.perf_counter()
+    tabs.compute_sumcheck_polynomials(0, Transcript())
+    torch.cuda.synchronize(); t1 = time.perf_counter()
+    print("factored sumcheck %.3f ms" % ((t1 - t0) * 1e3), flush=True)
+    time.sleep(0.01)
 if len(sys.argv) > 2:
     out = MPL.evaluate(x, pts)
     for rep in range(2):

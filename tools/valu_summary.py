@@ -22,7 +22,7 @@ NOMINAL = 7.864e13
 def main():
     tag, d = sys.argv[1], sys.argv[2]
     want = sys.argv[3:] or ["ntt_pass", "level2", "leaf_pairs", "fri_fold_leaves", "top_kernel",
-                            "fold_sums", "shard_dft", "mobius"]
+                            "fold_sums", "shard_dft", "mobius", "sums_eq", "subtree"]
     ctr = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
         ctr[r["Kernel_Name"]][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
@@ -48,19 +48,24 @@ def main():
         insts = sum(c["SQ_INSTS_VALU"] for _, c in rows) / len(rows)
         act = sum(c.get("SQ_ACTIVE_INST_VALU", 0) for _, c in rows) / len(rows)
         wav = sum(c.get("SQ_WAVE_CYCLES", 0) for _, c in rows) / len(rows)
+        grbm = sum(c.get("GRBM_GUI_ACTIVE", 0) for _, c in rows) / len(rows)
         rate = insts * 64 / t if t else 0
         short = name.split("(")[0]
         out["kernels"][short] = {
             "dispatches": len(rows), "avg_ms": t * 1e3, "SQ_INSTS_VALU": insts,
             "lane_instr_per_s": rate, "frac_nominal": rate / NOMINAL,
             "valu_active_frac": act / wav if wav else None,
+            # MI355X_MICROARCH.md "DVFS give-back": GRBM_GUI_ACTIVE summed over the
+            # 8 XCDs / 8 / wall time (reads high on dispatches under ~0.3 ms)
+            "eff_clock_ghz": grbm / 8 / t / 1e9 if (grbm and t) else None,
         }
     path = os.path.join(ROOT, "profiles", "%s_valu.json" % tag)
     json.dump(out, open(path, "w"), indent=1)
     for k, v in sorted(out["kernels"].items(), key=lambda kv: -kv[1]["avg_ms"]):
-        print("%-45s %8.3f ms  %.2e lane-instr/s  %.0f%% nominal  VALU-active %s" % (
+        print("%-45s %8.3f ms  %.2e lane-instr/s  %.0f%% nominal  VALU-active %s  clock %s" % (
             k[:45], v["avg_ms"], v["lane_instr_per_s"], 100 * v["frac_nominal"],
-            "%.0f%%" % (100 * v["valu_active_frac"]) if v["valu_active_frac"] is not None else "-"))
+            "%.0f%%" % (100 * v["valu_active_frac"]) if v["valu_active_frac"] is not None else "-",
+            "%.2f GHz" % v["eff_clock_ghz"] if v["eff_clock_ghz"] else "-"))
 
 
 if __name__ == "__main__":
