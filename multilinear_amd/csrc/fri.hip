@@ -110,14 +110,39 @@ namespace mlh {
 __global__ void transcript_absorb_kernel(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out,
                                          uint8_t* copy_out) {
   // the state lives in LDS while a single lane updates it (the byte buffer is
-  // indexed dynamically; in VGPRs it would spill to scratch)
+  // indexed dynamically; in VGPRs it would spill to scratch).  State and
+  // source are loaded by parallel lanes (one word each); lane 0 then absorbs
+  // from registers (a global source costs a dependent load per word).
   __shared__ DevSha s;
-  if (threadIdx.x != 0) return;
-  s = *t;
-  dsha_update(s, src, n);
+  __shared__ uint32_t stage[8], stage2[8];
+  const uint32_t tid = threadIdx.x;
+  const bool words = (n == 32 || n == 16) &&
+                     (((uintptr_t)src | (uintptr_t)copy_out) & 3) == 0;
+  if (tid < sizeof(DevSha) / 4)
+    reinterpret_cast<uint32_t*>(&s)[tid] = reinterpret_cast<const uint32_t*>(t)[tid];
+  if (words && tid < n / 4) {
+    const uint32_t v = reinterpret_cast<const uint32_t*>(src)[tid];
+    stage[tid] = v;
+    if (copy_out) reinterpret_cast<uint32_t*>(copy_out)[tid] = v;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  if (words && n == 32) {
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = stage[i];
+    dsha_absorb<8>(s, w, stage2);
+  } else if (words) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = stage[i];
+    dsha_absorb<4>(s, w, stage2);
+  } else {
+    dsha_update(s, src, n);
+    if (copy_out)
+      for (uint32_t i = 0; i < n; ++i) copy_out[i] = src[i];
+  }
   *t = s;
-  if (copy_out)
-    for (uint32_t i = 0; i < n; ++i) copy_out[i] = src[i];
   if (r_out) fe_store(r_out, dsha_challenge(s));
 }
 
@@ -130,12 +155,16 @@ hipError_t launch_transcript_absorb(DevSha* t, const uint8_t* src, uint32_t n, f
 
 __global__ void fri_last_kernel(const fe* vals, DevSha* t, uint32_t* flag, fe* last_out) {
   __shared__ DevSha s;
+  __shared__ uint32_t stage[4];
+  if (threadIdx.x < sizeof(DevSha) / 4)
+    reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
+  __syncthreads();
   if (threadIdx.x != 0) return;
   const fe a = fe_load(vals), b = fe_load(vals + 1);
   *flag = fe_eq(a, b) ? 0u : 1u;
   fe_store(last_out, a);
-  s = *t;
-  dsha_update(s, reinterpret_cast<const uint8_t*>(&a), 16);
+  const uint32_t w[4] = {a.w[0], a.w[1], a.w[2], a.w[3]};
+  dsha_absorb<4>(s, w, stage);  // LE16(last)
   *t = s;
 }
 

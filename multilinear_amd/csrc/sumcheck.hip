@@ -554,6 +554,19 @@ __global__ void __launch_bounds__(kRedThreads)
 sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev, DevSha* t,
                       fe* poly_out, fe* r_out, const fe* __restrict__ pk, fe* cdev) {
   __shared__ DevSha s;
+  __shared__ uint32_t stage[8];
+  // the transcript state (one word per lane) and lane 0's scalars are loaded
+  // first, so their latency overlaps the partial-sum reduction
+  if (threadIdx.x < sizeof(DevSha) / 4)
+    reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
+  fe p = fe_zero(), c = fe_zero(), pv = fe_zero();
+  if (threadIdx.x == 0) {
+    p = fe_load(prev);
+    if (pk) {
+      c = fe_load(cdev);
+      pv = fe_load(pk);
+    }
+  }
   // the round sums: reduce the per-workgroup partials (loads unrolled so a
   // lane's few loads are in flight together), then one lane runs the round
   fe s1 = fe_zero(), s2 = fe_zero();
@@ -562,25 +575,21 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
     s1 = fe_add(s1, fe_load(partials + 2 * i));
     s2 = fe_add(s2, fe_load(partials + 2 * i + 1));
   }
-  block_reduce2(s1, s2);
+  block_reduce2(s1, s2);  // (its barriers also publish the staged state)
   if (threadIdx.x != 0) return;
-  fe c, pv;
   if (pk) {
-    c = fe_load(cdev);
-    pv = fe_load(pk);
     const fe E0 = s1, E1 = s2;
     const fe three_p_1 = fe_sub(fe_add(fe_dbl(pv), pv), fe_one());
     s1 = fe_mul(fe_mul(c, pv), E1);
     s2 = fe_mul(fe_mul(c, three_p_1), fe_sub(fe_dbl(E1), E0));
   }
-  const fe p = fe_load(prev);
   const fe e0 = fe_sub(p, s1);
   const fe c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
   const fe c1 = fe_sub(fe_sub(s1, e0), c2);
   fe_store(poly_out, c1);
   fe_store(poly_out + 1, c2);
-  s = *t;
-  dsha_update(s, reinterpret_cast<const uint8_t*>(poly_out), 32);
+  const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
+  dsha_absorb<8>(s, w, stage);  // LE16(c1) || LE16(c2)
   *t = s;
   const fe r = dsha_challenge(s);
   fe_store(r_out, r);
@@ -604,6 +613,7 @@ sumcheck_tail_kernel(fe* __restrict__ m, fe* __restrict__ d, uint32_t S, fe* pre
   fe* ld = tail_lds + S;
   __shared__ DevSha sh;
   __shared__ fe r_sh;
+  __shared__ uint32_t stage[8];
   for (uint32_t i = threadIdx.x; i < S; i += blockDim.x) {
     lm[i] = fe_load(m + i);
     ld[i] = fe_load(d + i);
@@ -630,9 +640,8 @@ sumcheck_tail_kernel(fe* __restrict__ m, fe* __restrict__ d, uint32_t S, fe* pre
       const fe c1 = fe_sub(fe_sub(s1, e0), c2);
       fe_store(polys + 2 * k, c1);
       fe_store(polys + 2 * k + 1, c2);
-      // absorb LE16(c1) || LE16(c2) from where they were just stored (a
-      // local array would be indexed bytewise from scratch)
-      dsha_update(sh, reinterpret_cast<const uint8_t*>(polys + 2 * k), 32);
+      const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
+      dsha_absorb<8>(sh, w, stage);  // LE16(c1) || LE16(c2)
       const fe r = dsha_challenge(sh);
       fe_store(rs + k, r);
       p = fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r))));

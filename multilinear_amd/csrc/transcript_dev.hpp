@@ -52,9 +52,47 @@ __device__ inline void dsha_update(DevSha& s, const uint8_t* p, uint32_t n) {
   }
 }
 
-// digest of a clone (the state itself is unchanged); the clone is padded in
-// place (at most two compressions)
-__device__ inline void dsha_digest(const DevSha& s0, uint8_t out[32]) {
+// Absorb N words held in registers (memory byte order: the bytes as stored),
+// for a state with len % 4 == 0: at most one compression (N <= 16), no
+// loads from the source.  dsha_update on a global source costs a dependent
+// global load per word; on a register array with a byte fallback the array
+// lands in scratch.
+template <int N>
+__device__ inline void dsha_absorb_words(DevSha& s, const uint32_t (&w)[N]) {
+  static_assert(N >= 1 && N <= 16, "at most one block per call");
+  uint32_t* bw = reinterpret_cast<uint32_t*>(s.buf);
+  const uint32_t pos = (uint32_t)(s.len % 64) / 4;
+  const uint32_t first = 16 - pos < (uint32_t)N ? 16 - pos : (uint32_t)N;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if ((uint32_t)i < first) bw[pos + i] = w[i];
+  if (pos + N >= 16) {
+    dsha_compress_buf(s);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if ((uint32_t)i >= first) bw[i - first] = w[i];
+  }
+  s.len += 4 * N;
+}
+
+// absorb N words (registers); a state whose length is not a multiple of 4
+// (bytes absorbed on the host before the device loop) goes bytewise through
+// the LDS staging area `stage` (>= N words)
+template <int N>
+__device__ inline void dsha_absorb(DevSha& s, const uint32_t (&w)[N], uint32_t* stage) {
+  if ((s.len & 3) == 0) {
+    dsha_absorb_words<N>(s, w);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) stage[i] = w[i];
+  dsha_update(s, reinterpret_cast<const uint8_t*>(stage), 4 * N);
+}
+
+// Final state words of a clone (the state itself is unchanged); the clone is
+// padded in place (at most two compressions).  Digest byte 4i+j is byte
+// (3 - j) of h[i] (big-endian words).
+__device__ inline void dsha_final(const DevSha& s0, uint32_t h[8]) {
   __shared__ DevSha c;
   c = s0;
   const uint64_t bits = c.len * 8;
@@ -79,22 +117,27 @@ __device__ inline void dsha_digest(const DevSha& s0, uint8_t out[32]) {
     for (int i = 0; i < 8; ++i) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
     dsha_update(c, lb, 8);
   }
+  for (int i = 0; i < 8; ++i) h[i] = c.h[i];
+}
+
+__device__ inline void dsha_digest(const DevSha& s0, uint8_t out[32]) {
+  uint32_t h[8];
+  dsha_final(s0, h);
   for (int i = 0; i < 8; ++i) {
-    out[4 * i] = (uint8_t)(c.h[i] >> 24);
-    out[4 * i + 1] = (uint8_t)(c.h[i] >> 16);
-    out[4 * i + 2] = (uint8_t)(c.h[i] >> 8);
-    out[4 * i + 3] = (uint8_t)c.h[i];
+    out[4 * i] = (uint8_t)(h[i] >> 24);
+    out[4 * i + 1] = (uint8_t)(h[i] >> 16);
+    out[4 * i + 2] = (uint8_t)(h[i] >> 8);
+    out[4 * i + 3] = (uint8_t)h[i];
   }
 }
 
 // Field128::from(u128) (field.rs:138-142): one conditional subtraction of M.
+// The u128 is LE over digest bytes 0..15, i.e. limb i = bswap(h[i]).
 __device__ inline fe dsha_challenge(const DevSha& s) {
-  uint8_t d[32];
-  dsha_digest(s, d);
+  uint32_t h[8];
+  dsha_final(s, h);
   fe v;
-  for (int i = 0; i < 4; ++i)
-    v.w[i] = (uint32_t)d[4 * i] | ((uint32_t)d[4 * i + 1] << 8) | ((uint32_t)d[4 * i + 2] << 16) |
-             ((uint32_t)d[4 * i + 3] << 24);
+  for (int i = 0; i < 4; ++i) v.w[i] = bswap32(h[i]);
   return canon_with_carry(v, 0u);
 }
 
