@@ -758,9 +758,7 @@ struct FriDevLoop {
     MLH_TRY(btree.alloc(mlh_merkle_layers_bytes(L)));
     uint8_t* bt = btree.as<uint8_t>();
     HIP_TRY(ctx, launch_batch_pairs_leaves(codes, m, N, bt, ctx->stream));
-    HIP_TRY(ctx, launch_merkle_levels(bt, L, ctx->stream));
-    HIP_TRY(ctx, launch_transcript_absorb(dt(), bt + (2 * L - 2) * 32, 32, fr(), ctx->stream,
-                                          sb() + off_broot));
+    HIP_TRY(ctx, launch_merkle_levels(bt, L, ctx->stream, RootAbsorb{dt(), fr(), sb() + off_broot}));
     HIP_TRY(ctx, launch_transcript_absorb(dt(), reinterpret_cast<const uint8_t*>(fr()), 16,
                                           challenge_r0 ? r(0) : nullptr, ctx->stream));
     return MLH_OK;
@@ -794,9 +792,8 @@ struct FriDevLoop {
     p->layers.push_back(nx);
     HIP_TRY(ctx, launch_batched_fold_leaves(codes, m, N, fr(), rp, tlo, thi,
                                             reinterpret_cast<fe*>(vals), nx.tree, ctx->stream));
-    HIP_TRY(ctx, launch_merkle_levels(nx.tree, leaves, ctx->stream));
-    HIP_TRY(ctx, launch_transcript_absorb(dt(), nx.tree + (2 * leaves - 2) * 32, 32,
-                                          challenge_next ? r(1) : nullptr, ctx->stream, root(0)));
+    HIP_TRY(ctx, launch_merkle_levels(nx.tree, leaves, ctx->stream,
+                                      RootAbsorb{dt(), challenge_next ? r(1) : nullptr, root(0)}));
     return MLH_OK;
   }
 
@@ -811,10 +808,9 @@ struct FriDevLoop {
     MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
     l0.tree = reinterpret_cast<uint8_t*>(tree);
     p->layers.push_back(l0);
-    HIP_TRY(ctx, launch_commit_pairs(l0.values, L, l0.tree, ctx->stream));
-    HIP_TRY(ctx, launch_transcript_absorb(dt(), l0.tree + (2 * L - 2) * 32, 32,
-                                          challenge_after_root0 ? r(0) : nullptr, ctx->stream,
-                                          root(0)));
+    HIP_TRY(ctx, launch_commit_pairs(
+                     l0.values, L, l0.tree, ctx->stream,
+                     RootAbsorb{dt(), challenge_after_root0 ? r(0) : nullptr, root(0)}));
     return MLH_OK;
   }
 
@@ -847,13 +843,11 @@ struct FriDevLoop {
     MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
     nx.tree = reinterpret_cast<uint8_t*>(tree);
     p->layers.push_back(nx);
-    HIP_TRY(ctx, launch_fri_fold_commit(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
-                                        nx.tree, fe{}, tlo, thi, k, 1ull << p->log_code,
-                                        ctx->stream, ShardMap(), rp));
     const uint32_t t = (uint32_t)p->layers.size() - 1;
-    HIP_TRY(ctx, launch_transcript_absorb(dt(), nx.tree + (2 * L - 2) * 32, 32,
-                                          challenge_next ? r(k + 1) : nullptr, ctx->stream,
-                                          root(t)));
+    HIP_TRY(ctx, launch_fri_fold_commit(
+                     cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), nx.tree, fe{}, tlo,
+                     thi, k, 1ull << p->log_code, ctx->stream, ShardMap(), rp,
+                     RootAbsorb{dt(), challenge_next ? r(k + 1) : nullptr, root(t)}));
     return MLH_OK;
   }
 

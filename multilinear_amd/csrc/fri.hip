@@ -77,11 +77,11 @@ fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict_
 // 129 VGPRs, 3 waves per SIMD, against the fold's 4 memory streams.)
 hipError_t launch_fri_fold_commit(const fe* layer, uint64_t n, fe* next, uint8_t* tree, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
-                                  hipStream_t st, ShardMap map, const fe* r_dev) {
+                                  hipStream_t st, ShardMap map, const fe* r_dev, RootAbsorb ra) {
   hipError_t e = launch_fri_fold_leaves(layer, n, next, tree, r, tlo_inv, thi_inv, k, n0, st, map,
                                         r_dev);
   if (e != hipSuccess) return e;
-  return launch_merkle_levels(tree, n / 4, st);
+  return launch_merkle_levels(tree, n / 4, st, ra);
 }
 
 hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe* tlo_inv,

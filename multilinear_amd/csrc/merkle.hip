@@ -19,6 +19,7 @@
 #include "field.hpp"
 #include "merkle.hpp"
 #include "sha256.hpp"
+#include "transcript_dev.hpp"
 
 namespace mlh {
 
@@ -163,10 +164,17 @@ level1_kernel(const uint8_t* __restrict__ child, uint8_t* __restrict__ parent, u
 }
 
 // Finish a level of n <= 1024 digests (n a power of two >= 2) to the root in
-// one workgroup; writes every level into `out` consecutively.
+// one workgroup; writes every level into `out` consecutively.  ra.t: lane 0
+// then absorbs the root into the device transcript (RootAbsorb); the state is
+// staged into LDS by parallel lanes while the levels run.
 __global__ void __launch_bounds__(512)
-top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ out) {
+top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ out,
+           RootAbsorb ra) {
   __shared__ Sha256State s[1024];
+  __shared__ DevSha ts;
+  __shared__ uint32_t stage[8];
+  if (ra.t && threadIdx.x < sizeof(DevSha) / 4)
+    reinterpret_cast<uint32_t*>(&ts)[threadIdx.x] = reinterpret_cast<const uint32_t*>(ra.t)[threadIdx.x];
   for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) s[i] = digest_load(level + i * 32);
   __syncthreads();
   uint64_t off = 0;
@@ -183,6 +191,20 @@ top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ 
     __syncthreads();
     off += np;
     n = np;
+  }
+  if (ra.t && threadIdx.x == 0) {  // s[0] is the root (memory bytes = bswap of the words)
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = bswap32(s[0].h[i]);
+    dsha_absorb<8>(ts, w, stage);
+    DevSha* t = ra.t;
+    *t = ts;
+    if (ra.copy_out) {
+      uint4* q = reinterpret_cast<uint4*>(ra.copy_out);
+      q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+    if (ra.r_out) fe_store(ra.r_out, dsha_challenge(ts));
   }
 }
 
@@ -244,7 +266,8 @@ hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t b
 }
 
 // Levels above the level of n digests at layers + off digests (level order).
-hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, hipStream_t st) {
+hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, hipStream_t st,
+                                     RootAbsorb ra) {
   constexpr uint64_t kTailLevel = 1ull << 18;  // 256 workgroups of 1024-digest chunks
   constexpr uint64_t kChunk = 1024;
   constexpr unsigned kSpreadLds = 96 * 1024;
@@ -284,27 +307,32 @@ hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, 
   if (n > 1) {
     const unsigned threads = n / 2 < 64 ? 64 : (unsigned)(n / 2);
     hipLaunchKernelGGL(top_kernel, dim3(1), dim3(threads), 0, st, layers + off * 32, n,
-                       layers + (off + n) * 32);
+                       layers + (off + n) * 32, ra);
+  } else if (ra.t) {  // the level is the root already (one leaf)
+    hipError_t e = launch_transcript_absorb(ra.t, layers + off * 32, 32, ra.r_out, st,
+                                            ra.copy_out);
+    if (e != hipSuccess) return e;
   }
   return hipGetLastError();
 }
 
 // layers: 2L-1 digests, leaves already at [0, L).
-hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st) {
-  return launch_merkle_levels_from(layers, 0, L, st);
+hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st, RootAbsorb ra) {
+  return launch_merkle_levels_from(layers, 0, L, st, ra);
 }
 
-hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipStream_t st) {
+hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipStream_t st,
+                               RootAbsorb ra) {
   if (L < 4) {
     hipError_t e = launch_leaf_pairs(code, L, layers, st);
     if (e != hipSuccess) return e;
-    return launch_merkle_levels_from(layers, 0, L, st);
+    return launch_merkle_levels_from(layers, 0, L, st, ra);
   }
   hipLaunchKernelGGL(leaf_pairs_level2_kernel, dim3(blocks_for(L / 4, 256)), dim3(256), 0, st,
                      code, L, layers);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_merkle_levels_from(layers, L + L / 2, L / 4, st);
+  return launch_merkle_levels_from(layers, L + L / 2, L / 4, st, ra);
 }
 
 // Merkle::open (merkle_tree/mod.rs:31-58): for query q (one workgroup) the

@@ -12,15 +12,29 @@ hipError_t launch_leaf_bytes(const uint8_t* items, uint64_t item_len, uint64_t c
                              uint8_t* leaves, hipStream_t st);
 hipError_t launch_leaf_batch(const uint8_t* items, uint64_t item_len, uint64_t batch_stride,
                              uint32_t m, uint64_t count, uint8_t* leaves, hipStream_t st);
-hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st);
+struct DevSha;
+// Optional Fiat-Shamir step fused into the launch that writes a tree's root:
+// absorb the 32 root bytes into the device transcript t, copy them to
+// copy_out, and write next_challenge() to r_out (each pointer optional; t
+// null = no transcript step).  Same effect as launch_transcript_absorb(t,
+// root, 32, r_out, st, copy_out) after the tree, without its launch.
+struct RootAbsorb {
+  DevSha* t = nullptr;
+  fe* r_out = nullptr;
+  uint8_t* copy_out = nullptr;
+};
+hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st,
+                                RootAbsorb ra = RootAbsorb());
 // the levels above the level of n digests stored at layers + off digests
-hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, hipStream_t st);
+hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, hipStream_t st,
+                                     RootAbsorb ra = RootAbsorb());
 // sibling paths (depth = log2 L digests, bottom-up) of leaves idx[0..nq) (device array)
 hipError_t launch_merkle_paths(const uint8_t* layers, uint64_t L, const uint64_t* idx, uint32_t nq,
                                uint8_t* out, hipStream_t st);
 // commit_rs_code tree of the L = n/2 pairs (code[i], code[i + L]): leaves and
 // every level up to the root into layers (2L-1 digests, level order).
-hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipStream_t st);
+hipError_t launch_commit_pairs(const fe* code, uint64_t L, uint8_t* layers, hipStream_t st,
+                               RootAbsorb ra = RootAbsorb());
 
 // Block-cyclic shard layout of a layer spread over 2^log_p ranks: local
 // index l of rank `rank` holds global index
@@ -52,6 +66,6 @@ hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t
 hipError_t launch_fri_fold_commit(const fe* layer, uint64_t n, fe* next, uint8_t* tree, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
                                   hipStream_t st, ShardMap map = ShardMap(),
-                                  const fe* r_dev = nullptr);
+                                  const fe* r_dev = nullptr, RootAbsorb ra = RootAbsorb());
 
 }  // namespace mlh
