@@ -63,6 +63,8 @@ struct mlh_ctx {
   fe* partials = nullptr;             // 2 * kMaxRedBlocks
   fe* small = nullptr;                // 64 elements scratch (sums, points)
   uint8_t* pinned = nullptr;          // 4 KiB pinned host staging
+  uint8_t* qstage = nullptr;          // pinned staging of query phases (grow-only)
+  size_t qstage_bytes = 0;
   fe* ntt_scratch = nullptr;          // NTT ping-pong buffer (grow-only)
   size_t ntt_scratch_bytes = 0;
   // kernel timer (mlh_profile_*): HIP events on the launch stream
@@ -367,6 +369,7 @@ void mlh_context_destroy(mlh_ctx* ctx) {
   (void)hipFree(ctx->partials);
   (void)hipFree(ctx->small);
   (void)hipHostFree(ctx->pinned);
+  if (ctx->qstage) (void)hipHostFree(ctx->qstage);
   delete ctx;
 }
 
@@ -974,16 +977,34 @@ __global__ void gather_queries_kernel(const QueryTree* __restrict__ trees, uint3
 
 // Launch the per-tree gathers of p's layers into device records (qbytes
 // each, this part starting at byte `base` of a record).
+// Pinned host staging for a query phase (indices up, tree table up, records
+// down): pageable copies of these cost ~0.1 ms each on the critical path.
+// Grow-only; a caller's stream sync ends every use before the next one.
+static mlh_status query_stage(mlh_ctx* ctx, size_t bytes, uint8_t** out) {
+  if (bytes > ctx->qstage_bytes) {
+    if (ctx->qstage) HIP_TRY(ctx, hipHostFree(ctx->qstage));
+    ctx->qstage = nullptr;
+    ctx->qstage_bytes = 0;
+    void* h = nullptr;
+    HIP_TRY(ctx, hipHostMalloc(&h, bytes, 0));
+    ctx->qstage = reinterpret_cast<uint8_t*>(h);
+    ctx->qstage_bytes = bytes;
+  }
+  *out = ctx->qstage;
+  return MLH_OK;
+}
+
+// qt_stage: pinned host space for the tree table (layers.size() entries)
 static mlh_status gather_queries_dev(mlh_ctx* ctx, const mlh_fri_prover* p, const uint64_t* d_idx,
                                      uint32_t nq, uint64_t qbytes, uint64_t base, uint8_t* d_out,
-                                     PoolBuf& dtrees) {
+                                     PoolBuf& dtrees, uint8_t* qt_stage) {
   const uint32_t nt = (uint32_t)p->layers.size();
   if (nt == 0 || nq == 0) return MLH_OK;
-  std::vector<QueryTree> qt(nt);
+  QueryTree* qt = reinterpret_cast<QueryTree*>(qt_stage);
   for (uint32_t t = 0; t < nt; ++t)
     qt[t] = QueryTree{p->layers[t].values, p->layers[t].tree, p->layers[t].log_n};
   MLH_TRY(dtrees.alloc(nt * sizeof(QueryTree)));
-  HIP_TRY(ctx, hipMemcpyAsync(dtrees.p, qt.data(), nt * sizeof(QueryTree), hipMemcpyHostToDevice,
+  HIP_TRY(ctx, hipMemcpyAsync(dtrees.p, qt, nt * sizeof(QueryTree), hipMemcpyHostToDevice,
                               ctx->stream));
   hipLaunchKernelGGL(gather_queries_kernel, dim3(nq), dim3(64), 0, ctx->stream,
                      dtrees.as<QueryTree>(), nt, d_idx, nq, qbytes, base, d_out);
@@ -994,14 +1015,20 @@ static mlh_status gather_queries_dev(mlh_ctx* ctx, const mlh_fri_prover* p, cons
 static mlh_status gather_queries(mlh_ctx* ctx, const mlh_fri_prover* p, const uint64_t* idx,
                                  uint32_t nq, uint8_t* host_out) {
   const uint64_t qbytes = mlh_fri_query_bytes(p->log_code);
+  const size_t off_qt = 8ull * nq, off_out = off_qt + sizeof(QueryTree) * (p->layers.size() + 1);
+  uint8_t* h;
+  MLH_TRY(query_stage(ctx, off_out + nq * qbytes, &h));
+  memcpy(h, idx, 8ull * nq);
   PoolBuf dtrees(ctx), didx(ctx), dout(ctx);
   MLH_TRY(didx.alloc(nq * sizeof(uint64_t)));
   MLH_TRY(dout.alloc(nq * qbytes));
-  HIP_TRY(ctx, hipMemcpyAsync(didx.p, idx, nq * sizeof(uint64_t), hipMemcpyHostToDevice,
+  HIP_TRY(ctx, hipMemcpyAsync(didx.p, h, nq * sizeof(uint64_t), hipMemcpyHostToDevice,
                               ctx->stream));
-  MLH_TRY(gather_queries_dev(ctx, p, didx.as<uint64_t>(), nq, qbytes, 0, dout.as<uint8_t>(), dtrees));
-  HIP_TRY(ctx, hipMemcpyAsync(host_out, dout.p, nq * qbytes, hipMemcpyDeviceToHost, ctx->stream));
+  MLH_TRY(gather_queries_dev(ctx, p, didx.as<uint64_t>(), nq, qbytes, 0, dout.as<uint8_t>(), dtrees,
+                             h + off_qt));
+  HIP_TRY(ctx, hipMemcpyAsync(h + off_out, dout.p, nq * qbytes, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(host_out, h + off_out, nq * qbytes);
   return MLH_OK;
 }
 
@@ -1423,7 +1450,6 @@ struct EqSumcheck {
   fe* m = nullptr;
   uint32_t L = 0, a = 0, B = 0;
   PoolBuf buf;
-  std::vector<uint8_t> host;  // pageable upload source, alive until the caller syncs
   fe *pts = nullptr, *c = nullptr, *lo = nullptr, *d = nullptr, *H = nullptr, *scratch = nullptr;
   explicit EqSumcheck(mlh_ctx* c_) : ctx(c_), buf(c_) {}
 
@@ -1441,10 +1467,14 @@ struct EqSumcheck {
     lo = scratch + ns;
     d = B ? lo + (1ull << a) : lo;  // B == 0: delta is the whole eq table
     H = lo + 2 * (1ull << a);
-    host.assign(16ull * (L + 1), 0);
-    if (L) memcpy(host.data(), host_points, 16ull * L);
-    host[16ull * L] = 1;  // c_0 = 1
-    HIP_TRY(ctx, hipMemcpyAsync(pts, host.data(), host.size(), hipMemcpyHostToDevice, ctx->stream));
+    // points and c_0 = 1 through the pinned staging area (pinned + 1024, at
+    // most 41 x 16 B; callers use [0, 144) and [3072, 3088) for other uploads
+    // and download into [0, ...) only after these kernels, on the same stream)
+    uint8_t* hp = ctx->pinned + 1024;
+    memset(hp, 0, 16ull * (L + 1));
+    if (L) memcpy(hp, host_points, 16ull * L);
+    hp[16ull * L] = 1;
+    HIP_TRY(ctx, hipMemcpyAsync(pts, hp, 16ull * (L + 1), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, launch_eq_table(pts + B, a, scratch, lo, ctx->stream));
     if (B) HIP_TRY(ctx, launch_eq_suffix(pts, B, H, ctx->stream));
     return MLH_OK;
@@ -1909,18 +1939,23 @@ static mlh_status batched_queries(mlh_ctx* ctx, FriDevLoop& lp, mlh_transcript* 
   if (pf->commitments) mlh_fri_prover_roots(lp.p, pf->commitments);
   if (!pf->queries) return MLH_OK;
   const uint64_t qbytes = mlh_batched_fri_query_bytes(L, m);
+  const size_t off_qt = 8ull * MLH_NUM_QUERIES,
+               off_out = off_qt + sizeof(QueryTree) * (lp.p->layers.size() + 1);
+  uint8_t* h;
+  MLH_TRY(query_stage(ctx, off_out + MLH_NUM_QUERIES * qbytes, &h));
+  memcpy(h, idx.data(), 8ull * MLH_NUM_QUERIES);
   PoolBuf didx(ctx), dout(ctx), dtrees(ctx);
   MLH_TRY(didx.alloc(MLH_NUM_QUERIES * sizeof(uint64_t)));
   MLH_TRY(dout.alloc(MLH_NUM_QUERIES * qbytes));
-  HIP_TRY(ctx, hipMemcpyAsync(didx.p, idx.data(), MLH_NUM_QUERIES * 8, hipMemcpyHostToDevice,
-                              ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(didx.p, h, MLH_NUM_QUERIES * 8, hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, launch_batch_queries(lp.codes, m, N, lp.btree.as<uint8_t>(), didx.as<uint64_t>(),
                                     MLH_NUM_QUERIES, qbytes, dout.as<uint8_t>(), ctx->stream));
   MLH_TRY(gather_queries_dev(ctx, lp.p, didx.as<uint64_t>(), MLH_NUM_QUERIES, qbytes,
-                             32ull * m + 32ull * (L - 1), dout.as<uint8_t>(), dtrees));
-  HIP_TRY(ctx, hipMemcpyAsync(pf->queries, dout.p, MLH_NUM_QUERIES * qbytes,
+                             32ull * m + 32ull * (L - 1), dout.as<uint8_t>(), dtrees, h + off_qt));
+  HIP_TRY(ctx, hipMemcpyAsync(h + off_out, dout.p, MLH_NUM_QUERIES * qbytes,
                               hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(pf->queries, h + off_out, MLH_NUM_QUERIES * qbytes);
   return MLH_OK;
 }
 

@@ -2,10 +2,71 @@
 // Reference: src/transcript.rs (sha2 0.10.8 Sha256: update / finalize of a
 // clone).  Incremental, copyable state.
 #pragma once
+#include <immintrin.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 namespace mlh {
+
+static const uint32_t kHostShaK[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+    0xc67178f2u};
+
+// One compression with the x86 SHA extensions (sha256rnds2 does two rounds on
+// the ABEF/CDGH state halves; sha256msg1/msg2 extend the schedule).  The host
+// transcript replays every device absorb and derives the 128 query indices,
+// so its speed is on the prove's critical path.
+__attribute__((target("sha,sse4.1,ssse3"))) static inline void host_sha256_compress_ni(
+    uint32_t h[8], const uint8_t* blk) {
+  const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+  __m128i tmp = _mm_loadu_si128(reinterpret_cast<const __m128i*>(h));      // a b c d
+  __m128i st1 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(h + 4));  // e f g h
+  tmp = _mm_shuffle_epi32(tmp, 0xB1);
+  st1 = _mm_shuffle_epi32(st1, 0x1B);
+  __m128i st0 = _mm_alignr_epi8(tmp, st1, 8);   // ABEF
+  st1 = _mm_blend_epi16(st1, tmp, 0xF0);        // CDGH
+  const __m128i abef = st0, cdgh = st1;
+  __m128i m[4];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (j < 4)
+      m[j] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(blk + 16 * j)), bswap);
+    const __m128i cur = m[j & 3];
+    __m128i msg = _mm_add_epi32(cur, _mm_loadu_si128(reinterpret_cast<const __m128i*>(kHostShaK + 4 * j)));
+    st1 = _mm_sha256rnds2_epu32(st1, st0, msg);
+    if (j >= 3 && j <= 14) {
+      const __m128i t = _mm_alignr_epi8(cur, m[(j - 1) & 3], 4);
+      m[(j + 1) & 3] = _mm_sha256msg2_epu32(_mm_add_epi32(m[(j + 1) & 3], t), cur);
+    }
+    msg = _mm_shuffle_epi32(msg, 0x0E);
+    st0 = _mm_sha256rnds2_epu32(st0, st1, msg);
+    if (j >= 1 && j <= 12) m[(j - 1) & 3] = _mm_sha256msg1_epu32(m[(j - 1) & 3], cur);
+  }
+  st0 = _mm_add_epi32(st0, abef);
+  st1 = _mm_add_epi32(st1, cdgh);
+  tmp = _mm_shuffle_epi32(st0, 0x1B);           // FEBA
+  st1 = _mm_shuffle_epi32(st1, 0xB1);           // DCHG
+  st0 = _mm_blend_epi16(tmp, st1, 0xF0);        // DCBA
+  st1 = _mm_alignr_epi8(st1, tmp, 8);           // HGFE
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(h), st0);
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(h + 4), st1);
+}
+
+// SHA extensions present and not disabled (MLH_NO_SHANI=1 forces the portable
+// compression; tests run both)
+static inline bool host_sha_ni() {
+  static const int ok = __builtin_cpu_supports("sha") && !getenv("MLH_NO_SHANI") ? 1 : 0;
+  return ok != 0;
+}
 
 struct HostSha256 {
   uint32_t h[8];
@@ -21,17 +82,11 @@ struct HostSha256 {
   }
   static inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
   void compress(const uint8_t* blk) {
-    static const uint32_t K[64] = {
-        0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
-        0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
-        0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
-        0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
-        0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
-        0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
-        0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
-        0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
-        0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
-        0xc67178f2u};
+    if (host_sha_ni()) {
+      host_sha256_compress_ni(h, blk);
+      return;
+    }
+    const uint32_t* K = kHostShaK;
     uint32_t w[64];
     for (int i = 0; i < 16; ++i)
       w[i] = ((uint32_t)blk[4 * i] << 24) | ((uint32_t)blk[4 * i + 1] << 16) |
@@ -90,13 +145,11 @@ struct HostSha256 {
   void digest(uint8_t out[32]) const {
     HostSha256 c = *this;
     const uint64_t bits = c.len * 8;
-    const uint8_t pad0 = 0x80;
-    c.update(&pad0, 1);
-    const uint8_t z = 0;
-    while (c.len % 64 != 56) c.update(&z, 1);
-    uint8_t lb[8];
-    for (int i = 0; i < 8; ++i) lb[i] = (uint8_t)(bits >> (56 - 8 * i));
-    c.update(lb, 8);
+    uint8_t pad[72] = {0x80};  // 0x80, zeros up to 56 mod 64, then the bit length
+    const size_t fill = (size_t)(c.len % 64);
+    const size_t np = (fill < 56 ? 56 - fill : 120 - fill);
+    for (int i = 0; i < 8; ++i) pad[np + i] = (uint8_t)(bits >> (56 - 8 * i));
+    c.update(pad, np + 8);
     for (int i = 0; i < 8; ++i) {
       out[4 * i] = (uint8_t)(c.h[i] >> 24);
       out[4 * i + 1] = (uint8_t)(c.h[i] >> 16);

@@ -67,6 +67,40 @@ def test_transcript_matches_reference_semantics():
     assert c.random() != t.random()
 
 
+_SHA_STREAM = r"""
+import hashlib, random, sys
+sys.path.insert(0, %r)
+from multilinear_amd.transcript import Transcript
+rr = random.Random(11)
+t, h = Transcript(), hashlib.sha256()
+for _ in range(300):
+    b = bytes(rr.randrange(256) for _ in range(rr.choice([0, 1, 3, 8, 16, 32, 55, 56, 63, 64, 65, 200])))
+    t.absorb(b)
+    h.update(b)
+    assert t.random() == h.digest()
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("no_shani", [False, True])
+def test_host_sha256_both_compressions(no_shani):
+    """The host transcript's SHA-256 (x86 SHA extensions when present, else
+    portable) against hashlib over random absorb chunk sizes; the portable
+    path forced with MLH_NO_SHANI=1 in a fresh process."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env.pop("MLH_NO_SHANI", None)
+    if no_shani:
+        env["MLH_NO_SHANI"] = "1"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _SHA_STREAM % root], env=env, capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr
+
+
 def test_proof_sizes():
     lib = _lib.load()
     assert lib.mlh_merkle_layers_bytes(1 << 10) == (2 * 1024 - 1) * 32
