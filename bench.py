@@ -409,9 +409,10 @@ def main():
         torch.cuda.synchronize()
         sc_ms = (time.perf_counter() - t0) * 1e3 / 5
         result["sumcheck_ms"] = sc_ms
-        # algorithmic bytes of the factored rounds: round 0 reads the matrix,
-        # each fold reads S and writes S/2 (the matrix clone is 2 x 16 N)
-        sc_bytes = 32 * N + 16 * N + sum(24 * (N >> k) for k in range(log_n))
+        # algorithmic bytes of the factored rounds: round 0 reads the evaluations,
+        # each fold reads S and writes S/2 (the first fold reads the evaluations
+        # and writes a half-size table: no matrix clone)
+        sc_bytes = 16 * N + sum(24 * (N >> k) for k in range(log_n))
         result["sumcheck_hbm_frac"] = sc_bytes / (sc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
 
         # PCSProof::prove (multilinear_pcs.rs:90-136) on the 2^log_n evaluations:

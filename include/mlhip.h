@@ -371,12 +371,16 @@ mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, u
  * never materialised at full size: it stays c_k * eq(p_k..p_{L-1}) (a running
  * scalar times a two-level factored table) until it has 2^12 entries.  Same
  * outputs as mlh_eq_table + mlh_sumcheck_prove; half the HBM traffic.
- * dev_matrix (2^log_height elements) is folded in place; host_points:
- * log_height elements; delta_out (optional): the fully folded delta. */
-mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, void* dev_matrix, uint32_t log_height,
-                                 const uint8_t* host_points, const uint8_t sum[16],
-                                 mlh_transcript* tr, uint8_t* polys_out, uint8_t* rs_out,
-                                 uint8_t* delta_out);
+ * dev_evals: the MLE (2^log_height elements).  dev_work (2^(log_height-1)
+ * elements) receives the folded matrix (the first half of the table as
+ * SumcheckTables::fold leaves it) and dev_evals is not modified -- the
+ * matrix clone of build_tables_for_pcs is never made; dev_work = NULL folds
+ * dev_evals in place.  host_points: log_height elements; delta_out
+ * (optional): the fully folded delta. */
+mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_work,
+                                 uint32_t log_height, const uint8_t* host_points,
+                                 const uint8_t sum[16], mlh_transcript* tr, uint8_t* polys_out,
+                                 uint8_t* rs_out, uint8_t* delta_out);
 
 /* ---- multilinear PCS (src/fri/multilinear_pcs.rs) ------------------------ */
 typedef struct mlh_pcs_proof {

@@ -164,7 +164,7 @@ SIGNATURES = {
     "mlh_sumcheck_fold": (_I, [_P, _P, _P, _U32, _P]),
     "mlh_sumcheck_fold_and_sums": (_I, [_P, _P, _P, _U32, _P, _P]),
     "mlh_sumcheck_prove": (_I, [_P, _P, _P, _U32, _P, _P, _P, _P]),
-    "mlh_sumcheck_prove_eq": (_I, [_P, _P, _U32, _P, _P, _P, _P, _P, _P]),
+    "mlh_sumcheck_prove_eq": (_I, [_P, _P, _P, _U32, _P, _P, _P, _P, _P, _P]),
     "mlh_pcs_prove": (_I, [_P, _P, _U32, _P, _P, _P, ctypes.POINTER(PcsProofC)]),
     "mlh_pcs_verify": (_I, [ctypes.POINTER(PcsProofC), _U32, _P, _P, _P]),
     "mlh_bench_ntt": (_I, [_P, _P, _U32, _U32, ctypes.POINTER(ctypes.c_float)]),

@@ -1429,11 +1429,12 @@ mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, u
 // which needs the same r, measured no faster: the tree tail it would fill is
 // a handful of waves, and the cross-stream events cost about what it saved.)
 static mlh_status sumcheck_fold_dr(mlh_ctx* ctx, fe* m, fe* d, uint64_t S, const fe* r_dev,
-                                   uint32_t* np) {
+                                   uint32_t* np, const fe* m_src = nullptr) {
   if (S >= 4)
-    HIP_TRY(ctx, launch_fold_sums(m, d, S, fe{}, ctx->partials, ctx->small, ctx->stream, r_dev, np));
+    HIP_TRY(ctx, launch_fold_sums(m, d, S, fe{}, ctx->partials, ctx->small, ctx->stream, r_dev, np,
+                                  m_src));
   else
-    HIP_TRY(ctx, launch_fold(m, d, S, fe{}, ctx->stream, r_dev));
+    HIP_TRY(ctx, launch_fold(m, d, S, fe{}, ctx->stream, r_dev, m_src));
   return MLH_OK;
 }
 
@@ -1447,14 +1448,19 @@ static mlh_status sumcheck_fold_dr(mlh_ctx* ctx, fe* m, fe* d, uint64_t S, const
 struct EqSumcheck {
   static constexpr uint32_t kEqLo = 12;  // = sumcheck_tail_rounds' LDS limit
   mlh_ctx* ctx;
-  fe* m = nullptr;
+  const fe* src = nullptr;  // round 0's matrix (read only)
+  fe* m = nullptr;          // the folded matrix (== src: folded in place)
   uint32_t L = 0, a = 0, B = 0;
   PoolBuf buf;
   fe *pts = nullptr, *c = nullptr, *lo = nullptr, *d = nullptr, *H = nullptr, *scratch = nullptr;
   explicit EqSumcheck(mlh_ctx* c_) : ctx(c_), buf(c_) {}
 
-  mlh_status init(fe* matrix, uint32_t L_, const uint8_t* host_points) {
-    m = matrix;
+  // matrix: round 0's table; work (2^(L-1) entries, optional) receives the
+  // folded table -- the first fold reads `matrix` and writes `work`, so the
+  // caller's evaluations are never copied (build_tables_for_pcs's clone)
+  mlh_status init(const fe* matrix, fe* work, uint32_t L_, const uint8_t* host_points) {
+    src = matrix;
+    m = work ? work : const_cast<fe*>(matrix);
     L = L_;
     a = L < kEqLo ? L : kEqLo;
     B = L - a;
@@ -1484,9 +1490,10 @@ struct EqSumcheck {
   // round 0's sums into ctx->partials
   mlh_status first_sums(uint32_t* np) {
     if (B)
-      HIP_TRY(ctx, launch_sums_eq(m, 1ull << (L - 1), Hk(0), lo, a, ctx->partials, ctx->stream, np));
+      HIP_TRY(ctx, launch_sums_eq(src, 1ull << (L - 1), Hk(0), lo, a, ctx->partials, ctx->stream,
+                                  np));
     else
-      HIP_TRY(ctx, launch_sums(m, d, 1ull << (L - 1), ctx->partials, ctx->small, ctx->stream, np));
+      HIP_TRY(ctx, launch_sums(src, d, 1ull << (L - 1), ctx->partials, ctx->small, ctx->stream, np));
     return MLH_OK;
   }
   mlh_status round(uint32_t k, uint32_t np, fe* prev, DevSha* dt, fe* poly, fe* r) {
@@ -1497,26 +1504,27 @@ struct EqSumcheck {
   // fold round k's tables with r (HBM); want_sums: also round k+1's sums
   mlh_status fold(uint32_t k, const fe* r_dev, uint32_t* np, bool want_sums = true) {
     const uint64_t S = 1ull << (L - k);
+    const fe* in = k == 0 ? src : m;
     if (k + 1 < B) {
       HIP_TRY(ctx, launch_fold_sums_eq(m, S, r_dev, Hk(k + 1), lo, a, ctx->partials, ctx->stream,
-                                       np));
+                                       np, in));
     } else if (k + 1 == B) {
-      HIP_TRY(ctx, launch_fold(m, nullptr, S, fe{}, ctx->stream, r_dev));
+      HIP_TRY(ctx, launch_fold(m, nullptr, S, fe{}, ctx->stream, r_dev, in));
       HIP_TRY(ctx, launch_scale_dev(lo, c, 1ull << a, d, ctx->stream));
       if (want_sums)
         HIP_TRY(ctx, launch_sums(m, d, 1ull << (a - 1), ctx->partials, ctx->small, ctx->stream, np));
     } else {
-      MLH_TRY(sumcheck_fold_dr(ctx, m, d, S, r_dev, np));
+      MLH_TRY(sumcheck_fold_dr(ctx, m, d, S, r_dev, np, in));
     }
     return MLH_OK;
   }
 };
 
-mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, void* dev_matrix, uint32_t log_height,
-                                 const uint8_t* host_points, const uint8_t sum[16],
-                                 mlh_transcript* tr, uint8_t* polys_out, uint8_t* rs_out,
-                                 uint8_t* delta_out) {
-  if (!ctx || !dev_matrix || !host_points || !sum || !tr || log_height < 1 || log_height > 40)
+mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_work,
+                                 uint32_t log_height, const uint8_t* host_points,
+                                 const uint8_t sum[16], mlh_transcript* tr, uint8_t* polys_out,
+                                 uint8_t* rs_out, uint8_t* delta_out) {
+  if (!ctx || !dev_evals || !host_points || !sum || !tr || log_height < 1 || log_height > 40)
     return fail(ctx, MLH_ERR_INVALID, "bad argument");
   const uint32_t L = log_height;
   PoolBuf sc(ctx);
@@ -1530,7 +1538,8 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, void* dev_matrix, uint32_t log_he
   memcpy(ctx->pinned + 128, sum, 16);
   HIP_TRY(ctx, hipMemcpyAsync(sb, ctx->pinned, 144, hipMemcpyHostToDevice, ctx->stream));
   EqSumcheck es(ctx);
-  MLH_TRY(es.init(reinterpret_cast<fe*>(dev_matrix), L, host_points));
+  MLH_TRY(es.init(reinterpret_cast<const fe*>(dev_evals), reinterpret_cast<fe*>(dev_work), L,
+                  host_points));
   // head rounds stream only the matrix; the last a rounds (delta materialised,
   // 2^a entries) run in the LDS-resident tail launch
   uint32_t np = 0;
@@ -1540,7 +1549,7 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, void* dev_matrix, uint32_t log_he
     MLH_TRY(es.fold(k, rs + k, &np, false));
   }
   HIP_TRY(ctx, launch_sumcheck_tail(es.m, es.d, es.a, prev, dt, polys + 2 * es.B, rs + es.B,
-                                    ctx->stream));
+                                    ctx->stream, es.B ? es.m : es.src));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 48ull * L, es.d, 16, hipMemcpyDeviceToHost,
                               ctx->stream));
@@ -1570,7 +1579,7 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   PoolBuf coeffs(ctx), code(ctx), matrix(ctx);
   MLH_TRY(coeffs.alloc(n * 16));
   MLH_TRY(code.alloc(2 * n * 16));
-  MLH_TRY(matrix.alloc(n * 16));
+  MLH_TRY(matrix.alloc(n / 2 * 16));  // the folded table (the first fold reads dev_evals)
   // to_coefficient (:102), bit reverse (:104), reed_solomon (:107); the copy
   // and the permutation are folded into the Moebius and first NTT passes
   HIP_TRY(ctx, launch_mobius(coeffs.as<fe>(), n_vars, false, ctx->stream,
@@ -1584,9 +1593,8 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   fp->log_code = log_domain;
   FriDevLoop lp(ctx, fp.get());
   MLH_TRY(lp.init(code.p, log_domain, tr, false));
-  HIP_TRY(ctx, hipMemcpyAsync(matrix.p, dev_evals, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
   EqSumcheck es(ctx);  // delta = eq(inputs), factored (build_tables_for_pcs)
-  MLH_TRY(es.init(matrix.as<fe>(), n_vars, host_inputs));
+  MLH_TRY(es.init(reinterpret_cast<const fe*>(dev_evals), matrix.as<fe>(), n_vars, host_inputs));
   memcpy(ctx->pinned + 3072, output, 16);
   HIP_TRY(ctx, hipMemcpyAsync(lp.prev(), ctx->pinned + 3072, 16, hipMemcpyHostToDevice,
                               ctx->stream));
@@ -2053,7 +2061,7 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   HIP_TRY(ctx, launch_fingerprint(reinterpret_cast<const fe*>(dev_evals), num_polys, n, lp.fr(),
                                   matrix.as<fe>(), ctx->stream));
   EqSumcheck es(ctx);  // delta = eq(inputs), factored
-  MLH_TRY(es.init(matrix.as<fe>(), n_vars, inputs));
+  MLH_TRY(es.init(matrix.as<fe>(), nullptr, n_vars, inputs));
   {
     std::vector<uint8_t> ob(outputs, outputs + 16ull * num_polys);
     HIP_TRY(ctx, hipMemcpyAsync(outs.p, ob.data(), ob.size(), hipMemcpyHostToDevice, ctx->stream));

@@ -84,15 +84,15 @@ __device__ __forceinline__ fe lerp(const fe& lo, const fe& hi, const fe& r) {
 // Fold tables of size S with r (in place, first half) and emit the next
 // round's sums over the folded tables (h' = S/4).
 __global__ void __launch_bounds__(kRedThreads)
-fold_sums_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r,
-                 fe* __restrict__ partials, const fe* __restrict__ rp) {
+fold_sums_kernel(fe* m, fe* __restrict__ d, uint64_t S, fe r, fe* __restrict__ partials,
+                 const fe* __restrict__ rp, const fe* msrc) {
   if (rp) r = fe_load(rp);
   const uint64_t h = S / 2, q = S / 4;
   fe s1 = fe_zero(), s2 = fe_zero();
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < q; i += stride) {
-    const fe ma = fe_load(m + i), mb = fe_load(m + i + q);
-    const fe mc = fe_load(m + i + h), md = fe_load(m + i + h + q);
+    const fe ma = fe_load(msrc + i), mb = fe_load(msrc + i + q);
+    const fe mc = fe_load(msrc + i + h), md = fe_load(msrc + i + h + q);
     const fe da = fe_load(d + i), db = fe_load(d + i + q);
     const fe dc = fe_load(d + i + h), dd = fe_load(d + i + h + q);
     const fe m0 = lerp(ma, mc, r), m1 = lerp(mb, md, r);
@@ -112,13 +112,13 @@ fold_sums_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r,
 }
 
 __global__ void __launch_bounds__(256)
-fold_kernel(fe* __restrict__ m, fe* __restrict__ d, uint64_t S, fe r,
-            const fe* __restrict__ rp) {
+fold_kernel(fe* m, fe* __restrict__ d, uint64_t S, fe r, const fe* __restrict__ rp,
+            const fe* msrc) {
   if (rp) r = fe_load(rp);
   const uint64_t h = S / 2;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= h) return;
-  fe_store(m + i, lerp(fe_load(m + i), fe_load(m + i + h), r));
+  fe_store(m + i, lerp(fe_load(msrc + i), fe_load(msrc + i + h), r));
   if (d) fe_store(d + i, lerp(fe_load(d + i), fe_load(d + i + h), r));  // d == null: m only
 }
 
@@ -179,19 +179,21 @@ sums_eq_kernel(const fe* __restrict__ m, uint64_t h, const fe* __restrict__ H,
 }
 
 // fold m (size S) with r, then the eq-factored sums of the folded table
-// (h' = S/4, next round's H table).
+// (h' = S/4, next round's H table).  msrc: the table folded (== m in place; a
+// separate source lets the first fold read the caller's evaluations without
+// the build_tables_for_pcs clone).
 __global__ void __launch_bounds__(kRedThreads)
-fold_sums_eq_kernel(fe* __restrict__ m, uint64_t S, const fe* __restrict__ rp,
-                    const fe* __restrict__ H, const fe* __restrict__ lo, uint32_t a,
-                    fe* __restrict__ partials) {
+fold_sums_eq_kernel(fe* m, uint64_t S, const fe* __restrict__ rp, const fe* __restrict__ H,
+                    const fe* __restrict__ lo, uint32_t a, fe* __restrict__ partials,
+                    const fe* msrc) {
   const fe r = fe_load(rp);
   const uint64_t h = S / 2, q = S / 4;
   fe e0 = fe_zero(), e1 = fe_zero();
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (uint64_t i = i0; i < q; i += stride) {
-    const fe ma = fe_load(m + i), mb = fe_load(m + i + q);
-    const fe mc = fe_load(m + i + h), md = fe_load(m + i + h + q);
+    const fe ma = fe_load(msrc + i), mb = fe_load(msrc + i + q);
+    const fe mc = fe_load(msrc + i + h), md = fe_load(msrc + i + h + q);
     const fe hv = fe_load(H + (i >> a));
     const fe m0 = lerp(ma, mc, r), m1 = lerp(mb, md, r);
     fe_store(m + i, m0);
@@ -390,10 +392,10 @@ hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* o
 }
 
 hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* out,
-                            hipStream_t st, const fe* r_dev, uint32_t* nparts) {
+                            hipStream_t st, const fe* r_dev, uint32_t* nparts, const fe* m_src) {
   const unsigned nb = red_blocks(S / 4);
   hipLaunchKernelGGL(fold_sums_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, d, S, r, partials,
-                     r_dev);
+                     r_dev, m_src ? m_src : m);
   if (nparts)
     *nparts = nb;
   else
@@ -402,10 +404,11 @@ hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* ou
   return hipGetLastError();
 }
 
-hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe* r_dev) {
+hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe* r_dev,
+                       const fe* m_src) {
   const uint64_t h = S / 2;
   hipLaunchKernelGGL(fold_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, st, m, d, S, r,
-                     r_dev);
+                     r_dev, m_src ? m_src : m);
   return hipGetLastError();
 }
 
@@ -430,11 +433,12 @@ hipError_t launch_sums_eq(const fe* m, uint64_t h, const fe* H, const fe* lo, ui
 }
 
 hipError_t launch_fold_sums_eq(fe* m, uint64_t S, const fe* r_dev, const fe* H, const fe* lo,
-                               uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts) {
+                               uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts,
+                               const fe* m_src) {
   if (S / 4 < (1ull << a) || a < 8) return hipErrorInvalidValue;
   const unsigned nb = eq_blocks(S / 4);
   hipLaunchKernelGGL(fold_sums_eq_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, S, r_dev, H, lo, a,
-                     partials);
+                     partials, m_src ? m_src : m);
   *nparts = nb;
   return hipGetLastError();
 }
@@ -606,8 +610,8 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
 // and the fold, separated by barriers instead of two launches.  The tables
 // are folded in place exactly as fold_kernel does and written back at the end.
 __global__ void __launch_bounds__(kRedThreads)
-sumcheck_tail_kernel(fe* __restrict__ m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t,
-                     fe* polys, fe* rs) {
+sumcheck_tail_kernel(fe* m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t, fe* polys,
+                     fe* rs, const fe* msrc) {
   extern __shared__ fe tail_lds[];
   fe* lm = tail_lds;
   fe* ld = tail_lds + S;
@@ -615,7 +619,7 @@ sumcheck_tail_kernel(fe* __restrict__ m, fe* __restrict__ d, uint32_t S, fe* pre
   __shared__ fe r_sh;
   __shared__ uint32_t stage[8];
   for (uint32_t i = threadIdx.x; i < S; i += blockDim.x) {
-    lm[i] = fe_load(m + i);
+    lm[i] = fe_load(msrc + i);
     ld[i] = fe_load(d + i);
   }
   fe p = fe_zero();
@@ -655,7 +659,9 @@ sumcheck_tail_kernel(fe* __restrict__ m, fe* __restrict__ d, uint32_t S, fe* pre
     }
     __syncthreads();
   }
-  for (uint32_t i = threadIdx.x; i < S0; i += blockDim.x) {
+  // the folds only ever write the first half (entries >= S0/2 keep their
+  // input values), so that half is all there is to write back
+  for (uint32_t i = threadIdx.x; i < S0 / 2; i += blockDim.x) {
     fe_store(m + i, lm[i]);
     fe_store(d + i, ld[i]);
   }
@@ -670,13 +676,13 @@ uint32_t sumcheck_tail_rounds(uint32_t log_height) {
 }
 
 hipError_t launch_sumcheck_tail(fe* m, fe* d, uint32_t log_s, fe* prev, DevSha* t, fe* polys,
-                                fe* rs, hipStream_t st) {
+                                fe* rs, hipStream_t st, const fe* m_src) {
   if (log_s == 0 || log_s > kTailLogMax) return hipErrorInvalidValue;
   const uint32_t S = 1u << log_s;
   // 256 threads: 1024 measured slower (150 vs 127 us for 12 rounds) -- a
   // round is dominated by lane 0's SHA-256 work, the rest by barriers
   hipLaunchKernelGGL(sumcheck_tail_kernel, dim3(1), dim3(kRedThreads), 2 * S * sizeof(fe), st, m,
-                     d, S, prev, t, polys, rs);
+                     d, S, prev, t, polys, rs, m_src ? m_src : m);
   return hipGetLastError();
 }
 

@@ -14,9 +14,12 @@ hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* o
                        hipStream_t st, uint32_t* nparts = nullptr);
 // fold size-S tables with r, then sums of the folded (size S/2) tables.
 // nparts != null: skip the partials reduction and report the partial count
+// m_src (optional): fold from m_src into m (out of place; m needs S/2 entries)
 hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* out,
-                            hipStream_t st, const fe* r_dev = nullptr, uint32_t* nparts = nullptr);
-hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe* r_dev = nullptr);
+                            hipStream_t st, const fe* r_dev = nullptr, uint32_t* nparts = nullptr,
+                            const fe* m_src = nullptr);
+hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe* r_dev = nullptr,
+                       const fe* m_src = nullptr);
 struct DevSha;
 // one sumcheck round on the device: reduce the nparts partial sum pairs,
 // interpolate, absorb, challenge, new claim
@@ -33,7 +36,8 @@ hipError_t launch_eq_suffix(const fe* pts, uint32_t B, fe* H, hipStream_t st);
 hipError_t launch_sums_eq(const fe* m, uint64_t h, const fe* H, const fe* lo, uint32_t a,
                           fe* partials, hipStream_t st, uint32_t* nparts);
 hipError_t launch_fold_sums_eq(fe* m, uint64_t S, const fe* r_dev, const fe* H, const fe* lo,
-                               uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts);
+                               uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts,
+                               const fe* m_src = nullptr);
 // out[i] = (*c) * src[i]
 hipError_t launch_scale_dev(const fe* src, const fe* c, uint64_t n, fe* out, hipStream_t st);
 // Trace::evaluate: out[j] = sum_i eq[i] * m[i * width + j], j < width;
@@ -45,8 +49,9 @@ hipError_t launch_trace_eval(const fe* m, const fe* eq, uint64_t height, uint32_
 // tables of 2^log_s entries in one workgroup (LDS); polys/rs/prev/t as for
 // sumcheck_round_kernel, round k's outputs at polys + 2k, rs + k.
 uint32_t sumcheck_tail_rounds(uint32_t log_height);
+// m_src (optional): read the tables' m from m_src, write the folded half to m
 hipError_t launch_sumcheck_tail(fe* m, fe* d, uint32_t log_s, fe* prev, DevSha* t, fe* polys,
-                                fe* rs, hipStream_t st);
+                                fe* rs, hipStream_t st, const fe* m_src = nullptr);
 hipError_t launch_dot(const fe* a, const fe* b, uint64_t n, fe* partials, fe* out,
                       hipStream_t st);
 // mono: monomial table prod_{bit_i set} p[n-1-i] (coefficient-form MLE evaluation)

@@ -2,29 +2,40 @@
 composition x[0], width 1, on the MI355X (tables folded in place)."""
 import ctypes
 
-from .device import check, context, fe_bytes, fe_from_bytes, ints_to_limbs, lib, ptr, to_device
+from .device import (check, context, empty, fe_bytes, fe_from_bytes, ints_to_limbs, lib, ptr,
+                     to_device)
 from .polynomials import _points, eq_table
 from .transcript import Transcript
 
 
 class SumcheckTables:
     def __init__(self, matrix, delta):
-        self.matrix = matrix
+        self._matrix = matrix
         self._delta = delta
-        self._points = None  # set by build_tables_for_pcs: delta = eq(points), unbuilt
+        self._evals = None   # build_tables_for_pcs: matrix = clone of these, not yet made
+        self._points = None  # build_tables_for_pcs: delta = eq(points), not yet built
         self._device = 0
-        self.height = matrix.shape[0]
+        self.height = matrix.shape[0] if matrix is not None else 0
 
     @staticmethod
     def build_tables_for_pcs(inputs, evals, device=0):
-        """sumcheck.rs:128-145 (matrix = evals clone, delta = eq table).  The
-        delta table is built on first access; compute_sumcheck_polynomials on
-        fresh tables never builds it (mlh_sumcheck_prove_eq keeps it factored)."""
+        """sumcheck.rs:128-145 (matrix = evals clone, delta = eq table).  Both
+        tables are built on first access; compute_sumcheck_polynomials on fresh
+        tables builds neither (mlh_sumcheck_prove_eq keeps delta factored and
+        its first fold reads the evaluations, which are never modified)."""
         assert 1 << len(inputs) == evals.shape[0]
-        t = SumcheckTables(evals.clone(), None)
+        t = SumcheckTables(None, None)
+        t._evals = evals
         t._points = list(inputs)
         t._device = device
+        t.height = evals.shape[0]
         return t
+
+    @property
+    def matrix(self):
+        if self._matrix is None:
+            self._matrix = self._evals.clone()
+        return self._matrix
 
     @property
     def delta(self):
@@ -59,9 +70,15 @@ class SumcheckTables:
         rs = (ctypes.c_uint8 * (16 * n))()
         if self._delta is None:  # delta = eq(points), still unbuilt: factored rounds
             dl = (ctypes.c_uint8 * 16)()
-            check(lib().mlh_sumcheck_prove_eq(ctx, ptr(self.matrix), n, _points(self._points),
-                                              fe_bytes(total_sum), transcript.h, polys, rs, dl),
-                  ctx)
+            if self._matrix is None:  # read the evaluations, fold into a half-size table
+                src, work = self._evals, empty(self.height // 2, device)
+            else:
+                src, work = self._matrix, None
+            check(lib().mlh_sumcheck_prove_eq(ctx, ptr(src), ptr(work) if work is not None else None,
+                                              n, _points(self._points), fe_bytes(total_sum),
+                                              transcript.h, polys, rs, dl), ctx)
+            if work is not None:
+                self._matrix = work
             self._delta = to_device(ints_to_limbs([fe_from_bytes(dl)]), device)
         else:
             check(lib().mlh_sumcheck_prove(ctx, ptr(self.matrix), ptr(self._delta), n,

@@ -400,15 +400,17 @@ def test_sumcheck_rounds_match_oracle():
     assert tr.random() == otr.random()
 
 
-@pytest.mark.parametrize("factored", [True, False])
+@pytest.mark.parametrize("factored", [True, "inplace", False])
 @pytest.mark.parametrize("n", [1, 2, 12, 13, 15, 16])
 def test_sumcheck_prove_matches_oracle(n, factored):
     """Device-resident prove around the LDS tail (sumcheck_tail_kernel takes the
     last min(n, 12) rounds): polys, challenges, transcript and the folded
     tables (in place, as SumcheckTables::fold leaves them) vs the oracle.
     factored: fresh build_tables_for_pcs tables (mlh_sumcheck_prove_eq: delta
-    kept as c_k * eq(p_k..) for the first n - 12 rounds); otherwise the delta
-    table is materialised first (mlh_sumcheck_prove, two-table rounds)."""
+    kept as c_k * eq(p_k..) for the first n - 12 rounds; the first fold reads
+    the evaluations, which stay unmodified); "inplace": the same with the
+    matrix clone made first and folded in place; False: the delta table is
+    materialised first (mlh_sumcheck_prove, two-table rounds)."""
     ev = rand_vals(1 << n, 60 + n)
     pts = rand_vals(n, 61 + n)
     total = OPL.mle_evaluate(ev, pts)
@@ -420,15 +422,19 @@ def test_sumcheck_prove_matches_oracle(n, factored):
         nz, r2, prev = ot.compute_sumcheck_polynomial(prev, otr)
         want_polys.append(tuple(nz))
         want_rs.append(r2)
-    mt = MS.SumcheckTables.build_tables_for_pcs(pts, dev(ev))
+    evd = dev(ev)
+    mt = MS.SumcheckTables.build_tables_for_pcs(pts, evd)
     if not factored:
         mt.delta  # noqa: B018 -- materialise the eq table
+    if factored == "inplace":
+        mt.matrix  # noqa: B018 -- materialise the matrix clone
     tr = Transcript()
     tr.absorb(b"tail")
     polys, rs = mt.compute_sumcheck_polynomials(total, tr)
     assert polys == want_polys and rs == want_rs
     assert tr.random() == otr.random()
     assert host(mt.matrix)[0] == ot.matrix[0] and host(mt.delta)[0] == ot.delta[0]
+    assert host(evd) == ev  # build_tables_for_pcs clones: the evaluations are untouched
 
 
 @pytest.mark.parametrize("n", [1, 2, 8, 10, 13, 14, 16])
@@ -494,6 +500,9 @@ def test_sumcheck_factored_equals_two_table_full_size():
     assert ta.random() == tb.random()
     assert host(a.matrix)[0] == host(b.matrix)[0]
     assert host(a.delta)[0] == host(b.delta)[0]
+    import torch
+
+    assert torch.equal(x, D.random_device(1 << n, 77))  # the evaluations are untouched
     # the round chain closes: p_k(0) + p_k(1) = previous claim (c0 = e0 here)
     prev = total
     for (c1, c2), r in zip(pa, ra):
