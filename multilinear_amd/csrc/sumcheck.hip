@@ -413,7 +413,13 @@ hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe*
 }
 
 // thread count for the eq-factored kernels: a power of two >= 2^a (work >= 2^a)
-static inline unsigned eq_blocks(uint64_t work) { return red_blocks(work); }
+#ifndef MLH_EQ_BLOCKS
+#define MLH_EQ_BLOCKS 1024  // 2048 and 512 measured 1-2 % slower (tools/sumcheck_ab.py)
+#endif
+static inline unsigned eq_blocks(uint64_t work) {
+  const unsigned b = red_blocks(work);
+  return b < MLH_EQ_BLOCKS ? b : MLH_EQ_BLOCKS;
+}
 
 hipError_t launch_eq_suffix(const fe* pts, uint32_t B, fe* H, hipStream_t st) {
   const uint64_t total = (1ull << B) - 1;
@@ -605,11 +611,25 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
 }
 
 // The last rounds of a device-resident sumcheck (tables of S <= kTailMax
-// entries) in ONE workgroup with m and d staged in LDS: per round the sums,
-// the round polynomial + Fiat-Shamir step (lane 0, as sumcheck_round_kernel)
-// and the fold, separated by barriers instead of two launches.  The tables
-// are folded in place exactly as fold_kernel does and written back at the end.
-__global__ void __launch_bounds__(kRedThreads)
+// entries) in ONE workgroup with m and d staged in LDS: per round the round
+// polynomial + Fiat-Shamir step (lane 0, as sumcheck_round_kernel), then one
+// phase that folds with r AND accumulates the next round's sums over the
+// folded values (as fold_sums_kernel: lane i owns pairs i, i + q of the
+// folded table, so no other lane touches its entries), then the reduction.
+// The tables are folded in place exactly as fold_kernel does; the folded half
+// is written back at the end.
+#ifndef MLH_TAIL_THREADS
+#define MLH_TAIL_THREADS 256
+#endif
+__device__ __forceinline__ void tail_sums(const fe* lm, const fe* ld, uint32_t h, fe& s1, fe& s2) {
+  for (uint32_t i = threadIdx.x; i < h; i += blockDim.x) {
+    const fe m0 = lm[i], m1 = lm[i + h], d0 = ld[i], d1 = ld[i + h];
+    s1 = fe_add(s1, fe_mul(m1, d1));
+    s2 = fe_add(s2, fe_mul(fe_sub(fe_dbl(m1), m0), fe_sub(fe_dbl(d1), d0)));
+  }
+}
+
+__global__ void __launch_bounds__(MLH_TAIL_THREADS)
 sumcheck_tail_kernel(fe* m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t, fe* polys,
                      fe* rs, const fe* msrc) {
   extern __shared__ fe tail_lds[];
@@ -618,25 +638,20 @@ sumcheck_tail_kernel(fe* m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t,
   __shared__ DevSha sh;
   __shared__ fe r_sh;
   __shared__ uint32_t stage[8];
+  if (threadIdx.x < sizeof(DevSha) / 4)
+    reinterpret_cast<uint32_t*>(&sh)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
+  fe p = fe_zero();
+  if (threadIdx.x == 0) p = fe_load(prev);
   for (uint32_t i = threadIdx.x; i < S; i += blockDim.x) {
     lm[i] = fe_load(msrc + i);
     ld[i] = fe_load(d + i);
   }
-  fe p = fe_zero();
-  if (threadIdx.x == 0) {
-    sh = *t;
-    p = fe_load(prev);
-  }
   __syncthreads();
   const uint32_t S0 = S;
+  fe s1 = fe_zero(), s2 = fe_zero();
+  tail_sums(lm, ld, S / 2, s1, s2);
   for (uint32_t k = 0; S > 1; ++k, S /= 2) {
     const uint32_t h = S / 2;
-    fe s1 = fe_zero(), s2 = fe_zero();
-    for (uint32_t i = threadIdx.x; i < h; i += blockDim.x) {
-      const fe m0 = lm[i], m1 = lm[i + h], d0 = ld[i], d1 = ld[i + h];
-      s1 = fe_add(s1, fe_mul(m1, d1));
-      s2 = fe_add(s2, fe_mul(fe_sub(fe_dbl(m1), m0), fe_sub(fe_dbl(d1), d0)));
-    }
     block_reduce2(s1, s2);
     if (threadIdx.x == 0) {
       const fe e0 = fe_sub(p, s1);
@@ -653,12 +668,28 @@ sumcheck_tail_kernel(fe* m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t,
     }
     __syncthreads();
     const fe r = r_sh;
-    for (uint32_t i = threadIdx.x; i < h; i += blockDim.x) {
-      lm[i] = lerp(lm[i], lm[i + h], r);
-      ld[i] = lerp(ld[i], ld[i + h], r);
+    s1 = fe_zero();
+    s2 = fe_zero();
+    if (h >= 2) {  // fold S -> h, next round's sums over pairs (i, i + q) of the folded table
+      const uint32_t q = h / 2;
+      for (uint32_t i = threadIdx.x; i < q; i += blockDim.x) {
+        const fe m0 = lerp(lm[i], lm[i + h], r), m1 = lerp(lm[i + q], lm[i + q + h], r);
+        const fe d0 = lerp(ld[i], ld[i + h], r), d1 = lerp(ld[i + q], ld[i + q + h], r);
+        lm[i] = m0;
+        lm[i + q] = m1;
+        ld[i] = d0;
+        ld[i + q] = d1;
+        s1 = fe_add(s1, fe_mul(m1, d1));
+        s2 = fe_add(s2, fe_mul(fe_sub(fe_dbl(m1), m0), fe_sub(fe_dbl(d1), d0)));
+      }
+    } else if (threadIdx.x == 0) {  // last round: fold the final pair
+      lm[0] = lerp(lm[0], lm[1], r);
+      ld[0] = lerp(ld[0], ld[1], r);
     }
-    __syncthreads();
+    // (block_reduce2 at the top of the next round orders these LDS writes
+    // before any other lane reads them)
   }
+  __syncthreads();
   // the folds only ever write the first half (entries >= S0/2 keep their
   // input values), so that half is all there is to write back
   for (uint32_t i = threadIdx.x; i < S0 / 2; i += blockDim.x) {
@@ -681,8 +712,8 @@ hipError_t launch_sumcheck_tail(fe* m, fe* d, uint32_t log_s, fe* prev, DevSha* 
   const uint32_t S = 1u << log_s;
   // 256 threads: 1024 measured slower (150 vs 127 us for 12 rounds) -- a
   // round is dominated by lane 0's SHA-256 work, the rest by barriers
-  hipLaunchKernelGGL(sumcheck_tail_kernel, dim3(1), dim3(kRedThreads), 2 * S * sizeof(fe), st, m,
-                     d, S, prev, t, polys, rs, m_src ? m_src : m);
+  hipLaunchKernelGGL(sumcheck_tail_kernel, dim3(1), dim3(MLH_TAIL_THREADS), 2 * S * sizeof(fe), st,
+                     m, d, S, prev, t, polys, rs, m_src ? m_src : m);
   return hipGetLastError();
 }
 

@@ -89,27 +89,39 @@ __device__ inline void dsha_absorb(DevSha& s, const uint32_t (&w)[N], uint32_t* 
   dsha_update(s, reinterpret_cast<const uint8_t*>(stage), 4 * N);
 }
 
-// Final state words of a clone (the state itself is unchanged); the clone is
-// padded in place (at most two compressions).  Digest byte 4i+j is byte
-// (3 - j) of h[i] (big-endian words).
+// Final state words of a clone (the state itself is unchanged; at most two
+// compressions).  Digest byte 4i+j is byte (3 - j) of h[i] (big-endian words).
 __device__ inline void dsha_final(const DevSha& s0, uint32_t h[8]) {
+  const uint64_t bits = s0.len * 8;
+  if ((s0.len & 3) == 0) {
+    // word fill (every device absorb): the padded block(s) are built in
+    // registers straight from the buffer words -- no copy of the state
+    const uint32_t* bw = reinterpret_cast<const uint32_t*>(s0.buf);
+    const uint32_t pos = (uint32_t)(s0.len % 64) / 4;
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t b = bw[i];
+      w[i] = (uint32_t)i < pos ? bswap32(b) : ((uint32_t)i == pos ? 0x80000000u : 0u);
+    }
+    Sha256State st;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st.h[i] = s0.h[i];
+    if (pos >= 14) {  // no room for the length: 0x80 block, then a zero block
+      sha256_compress(st, w);
+#pragma unroll
+      for (int i = 0; i < 14; ++i) w[i] = 0;
+    }
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+    sha256_compress(st, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = st.h[i];
+    return;
+  }
   __shared__ DevSha c;
   c = s0;
-  const uint64_t bits = c.len * 8;
-  if ((c.len & 3) == 0) {
-    uint32_t* bw = reinterpret_cast<uint32_t*>(c.buf);
-    uint32_t pos = (uint32_t)(c.len % 64) / 4;
-    bw[pos++] = 0x80u;  // byte 0x80 then zeros, memory order
-    if (pos > 14) {
-      for (; pos < 16; ++pos) bw[pos] = 0;
-      dsha_compress_buf(c);
-      pos = 0;
-    }
-    for (; pos < 14; ++pos) bw[pos] = 0;
-    bw[14] = bswap32((uint32_t)(bits >> 32));
-    bw[15] = bswap32((uint32_t)bits);
-    dsha_compress_buf(c);
-  } else {
+  {
     const uint8_t one = 0x80, z = 0;
     dsha_update(c, &one, 1);
     while (c.len % 64 != 56) dsha_update(c, &z, 1);
