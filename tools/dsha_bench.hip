@@ -63,6 +63,18 @@ __global__ void compress_chain_uniform(const uint32_t* __restrict__ io, uint32_t
   }
 }
 
+// a Merkle-top style chain: one lane, node = SHA256(node || node) (two
+// compressions, the second with the constant padding schedule)
+__global__ void node_chain(uint32_t* io, int iters, uint64_t* clk) {
+  if (threadIdx.x != 0) return;
+  const uint64_t c0 = __builtin_amdgcn_s_memtime();
+  Sha256State st;
+  for (int i = 0; i < 8; ++i) st.h[i] = io[i];
+  for (int i = 0; i < iters; ++i) st = sha256_node(st, st);
+  for (int i = 0; i < 8; ++i) io[i] = st.h[i];
+  clk[0] = __builtin_amdgcn_s_memtime() - c0;
+}
+
 // the same chain while `busy` other workgroups keep the chip loaded
 __global__ void spin(uint32_t* sink, int iters) {
   uint32_t x = threadIdx.x;
@@ -121,6 +133,19 @@ int main() {
            "matches VALU chain: %s\n", iters, ms * 1e3 / iters, (double)h[0] / iters,
            memcmp(hu, hr, 32) == 0 ? "yes" : "NO");
     hipFree(ref);
+  }
+  for (int iters : {10, 100}) {
+    hipLaunchKernelGGL(node_chain, dim3(1), dim3(64), 0, 0, io + 32, iters, clk);
+    hipEventRecord(a);
+    hipLaunchKernelGGL(node_chain, dim3(1), dim3(64), 0, 0, io + 32, iters, clk);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    uint64_t h[1];
+    hipMemcpy(h, clk, 8, hipMemcpyDeviceToHost);
+    printf("node_chain iters %d: %.2f us per node (2 compressions), %.0f cycles per node\n", iters,
+           ms * 1e3 / iters, (double)h[0] / iters);
   }
   for (int loaded : {0, 1}) {
     for (int iters : {10, 100}) {
