@@ -75,6 +75,22 @@ __global__ void node_chain(uint32_t* io, int iters, uint64_t* clk) {
   clk[0] = __builtin_amdgcn_s_memtime() - c0;
 }
 
+// the same with the state pinned to VGPRs (an empty asm the compiler must
+// treat as divergent): pure VALU, no v_readfirstlane round trips
+__global__ void node_chain_v(uint32_t* io, int iters, uint64_t* clk) {
+  if (threadIdx.x != 0) return;
+  const uint64_t c0 = __builtin_amdgcn_s_memtime();
+  Sha256State st;
+  for (int i = 0; i < 8; ++i) st.h[i] = io[i];
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(st.h[j]));
+    st = sha256_node(st, st);
+  }
+  for (int i = 0; i < 8; ++i) io[i] = st.h[i];
+  clk[0] = __builtin_amdgcn_s_memtime() - c0;
+}
+
 // the same chain while `busy` other workgroups keep the chip loaded
 __global__ void spin(uint32_t* sink, int iters) {
   uint32_t x = threadIdx.x;
@@ -146,6 +162,19 @@ int main() {
     hipMemcpy(h, clk, 8, hipMemcpyDeviceToHost);
     printf("node_chain iters %d: %.2f us per node (2 compressions), %.0f cycles per node\n", iters,
            ms * 1e3 / iters, (double)h[0] / iters);
+    hipLaunchKernelGGL(node_chain_v, dim3(1), dim3(64), 0, 0, io + 48, iters, clk);
+    hipEventRecord(a);
+    hipLaunchKernelGGL(node_chain_v, dim3(1), dim3(64), 0, 0, io + 48, iters, clk);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    hipEventElapsedTime(&ms, a, b);
+    hipMemcpy(h, clk, 8, hipMemcpyDeviceToHost);
+    uint32_t h1[8], h2[8];
+    hipMemcpy(h1, io + 32, 32, hipMemcpyDeviceToHost);
+    hipMemcpy(h2, io + 48, 32, hipMemcpyDeviceToHost);
+    printf("node_chain_v iters %d: %.2f us per node, %.0f cycles per node (same digest as node_chain "
+           "after 2 launches each: %s)\n", iters, ms * 1e3 / iters, (double)h[0] / iters,
+           memcmp(h1, h2, 32) == 0 ? "yes" : "NO");
   }
   for (int loaded : {0, 1}) {
     for (int iters : {10, 100}) {
