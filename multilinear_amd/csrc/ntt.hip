@@ -72,6 +72,9 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 #ifndef MLH_WPS8
 #define MLH_WPS8 5
 #endif
+#ifndef MLH_LAST_STAGED
+#define MLH_LAST_STAGED 1  // last pass loads through LDS (coalesced runs): pass -3..6 %
+#endif
 #ifndef MLH_LDS_PAD
 #define MLH_LDS_PAD 0  // extra dynamic LDS per pass workgroup (occupancy experiments)
 #endif
@@ -134,6 +137,25 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
 
   // ---- phase 1: load bit-reversed rows, stages 0..2 in registers ---------
   fe x[EPT];
+#if MLH_LAST_STAGED
+  // last pass: its rows are consecutive elements, so a lane's bit-reversed
+  // rows scatter one wave's loads over 64 separate 16-B pieces.  Load the tile
+  // as 8 x 128-B runs per wave instruction (8 consecutive rows x 8 columns)
+  // into LDS, then read the bit-reversed rows from there.
+  if constexpr (LAST && ZT == 0) {
+    constexpr int NT = kCols * R / EPT;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const uint32_t idx = (uint32_t)(e * NT + tid);
+      const uint32_t l = idx & 63, grp = idx >> 6;
+      const uint32_t row = grp * 8 + (l & 7), col = l >> 3;
+      lds[row * kCols + col] = fe_load(in + base + (uint64_t)col * cstride + row);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) x[e] = lds[bitrev((uint32_t)(t * EPT + e), LOGR) * kCols + c];
+  } else
+#endif
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
     const uint32_t row = bitrev((uint32_t)(t * EPT + e), LOGR);
