@@ -267,7 +267,7 @@ def main():
 
     # dominant kernel timing (HIP events on the launch stream, timed region)
     kernels = {}
-    labels = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(3)
+    labels = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(4)
               for z in range(3)] + ["shard_dft<%d,0>" % p for p in range(1, 5)]
     for lab in labels:
         cnt = ctypes.c_uint64()

@@ -269,7 +269,8 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
   for (uint32_t p = 0; p + 1 < tb->nradix; ++p) {  // the last pass has no twiddle
     const uint64_t R = 1ull << tb->logr[p];
     const uint32_t logw = log_n - (uint32_t)__builtin_ctzll(S) - tb->logr[p];
-    const uint32_t loga = logw < kTwLogA ? logw : kTwLogA;
+    const uint32_t loga =
+        tb->logr[p] + logw <= kFullTwLog ? logw : (logw < kTwLogA ? logw : kTwLogA);
     const u128 ws = h_pow(w, S);
     tb->loga[p] = loga;
     MLH_TRY(get_table2d(ctx, ws, R, 1ull << loga, 1, p == 0 ? scale : (u128)1, &tb->ta[p],

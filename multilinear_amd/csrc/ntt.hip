@@ -67,7 +67,9 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
   return rev;
 }
 
-// TW: 0 = two-table twiddle (TA * TB), 1 = one table (TA; W <= 2^8), 2 = none (last pass)
+// TW: 0 = two-table twiddle (TA * TB), 1 = one table (TA), 2 = none (last pass),
+// 3 = one table on pass 0 (same code as 1; its own kernel so that rocprof and
+// the kernel timer tell the first pass from the middle ones)
 // waves per SIMD the LDS tile allows (160 KiB/CU): caps VGPRs to match
 #ifndef MLH_WPS8
 #define MLH_WPS8 5
@@ -388,10 +390,13 @@ static hipError_t launch_pass_ept(bool last, int zero_top, const fe* in, fe* out
   if (last) {
     if (zero_top) return hipErrorInvalidValue;  // pass 0 is never the last pass here
     MLH_PASS(2, 0);
+  } else if (!tb && g.p == 0) {  // TW 3: as 1, a distinct kernel for the first pass
+    if (zero_top == 2) MLH_PASS(3, 2);
+    else if (zero_top == 1) MLH_PASS(3, 1);
+    else MLH_PASS(3, 0);
   } else if (!tb) {
-    if (zero_top == 2) MLH_PASS(1, 2);
-    else if (zero_top == 1) MLH_PASS(1, 1);
-    else MLH_PASS(1, 0);
+    if (zero_top) return hipErrorInvalidValue;  // only pass 0 has an implicit zero half
+    MLH_PASS(1, 0);
   } else {
     if (zero_top == 2) MLH_PASS(0, 2);
     else if (zero_top == 1) MLH_PASS(0, 1);
@@ -453,7 +458,7 @@ hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n,
 
 void ntt_pass_label(const NttTables& tb, uint32_t p, int zero_top, char* buf, size_t n) {
   const bool last = p + 1 == tb.nradix;
-  const int tw = last ? 2 : (tb.tb[p] ? 0 : 1);
+  const int tw = last ? 2 : (tb.tb[p] ? 0 : (p == 0 ? 3 : 1));
   snprintf(buf, n, "ntt_pass<%u,%d,%d>", tb.logr[p], tw, p == 0 ? zero_top : 0);
 }
 

@@ -11,7 +11,15 @@ constexpr int kMaxPasses = 6;
 #ifndef MLH_XTW
 #define MLH_XTW 0  // inter-pass twiddles as expanded tables (fe_mul_pre)
 #endif
-constexpr uint32_t kTwLogA = 8;  // inter-pass twiddle split: TA covers 2^8 columns
+// Inter-pass twiddles w_S^(jrest k) of a pass with W columns, R rows: one
+// table TA[k][jrest] (one modmul per element) while R * W <= 2^kFullTwLog
+// entries (64 MiB), else split TA[k][jl] * TB[k][jh] with 2^kTwLogA columns
+// in TA (two modmuls).  The full table measured -6 % per transform at 2^22
+// and -11 % at 2^20 (it stays in the MALL); at 2^24 (256 MiB read at 16 B per
+// element beside the 32 B of data) pass 0 was no faster, so there the split
+// tables stay.
+constexpr uint32_t kTwLogA = 8;
+constexpr uint32_t kFullTwLog = 22;
 
 // Device twiddle tables for one (log_n, generator, direction).
 struct NttTables {

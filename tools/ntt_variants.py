@@ -6,7 +6,7 @@ import torch
 from multilinear_amd import _lib
 from multilinear_amd import device as D
 
-LABELS = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(3) for z in range(2)]
+LABELS = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(4) for z in range(2)]
 
 REF = [None]
 for path in sys.argv[1:]:
