@@ -540,6 +540,102 @@ def test_ntt_2_24_properties():
     assert bool((back == x).all())
 
 
+def _const_device(v, n):
+    import torch
+
+    row = D.ints_to_limbs([v])
+    return D.to_device(np.tile(row, (n, 1))) if n else torch.empty((0, 4), dtype=torch.int32)
+
+
+@pytest.mark.parametrize("log_n", [11, 20, 24])
+def test_ntt_extreme_values(log_n):
+    """Operands at the top of the canonical range, which the uniform generator
+    (top limb <= 0xFFFFFFFE) never produces and random intermediates reach with
+    probability ~2^-32: all coefficients M-1 -> (N(M-1), 0, ..., 0); a single
+    M-1 at index 1 -> -g^i; both round-trip through the INTT; Reed-Solomon of
+    a single M-1 at index 0 is the constant codeword, at index 1 it is -g2^i."""
+    import torch
+
+    lib = _lib.load()
+    ctx = D.context(0)
+    n = 1 << log_n
+    top = F.M - 1
+    g = F.pow_2_generator(log_n)
+    x = _const_device(top, n)
+    ev = MN.Polynomial(x).ntt(g).evals
+    assert D.limbs_to_ints(D.from_device(ev[:1]))[0] == n * top % F.M
+    assert bool((ev[1:] == 0).all())
+    assert bool((MN.LagrangePolynomial(g, ev).intt().coeffs == x).all())
+    # single M-1 at index 1: evals[i] = -g^i
+    d = torch.zeros_like(x)
+    d[1] = x[0]
+    ev = MN.Polynomial(d).ntt(g).evals
+    gp = MN.pow_2_generator_powers(log_n)
+    want = torch.empty_like(gp)
+    D.check(lib.mlh_field_neg(ctx, D.ptr(gp), D.ptr(want), n), ctx)
+    assert bool((ev == want).all())
+    assert bool((MN.LagrangePolynomial(g, ev).intt().coeffs == d).all())
+    # Reed-Solomon (implicit zero upper half in pass 0)
+    g2 = F.pow_2_generator(log_n + 1)
+    e0 = torch.zeros_like(x)
+    e0[0] = x[0]
+    assert bool((MF.reed_solomon(e0, g2) == _const_device(top, 2 * n)).all())
+    code = MF.reed_solomon(d, g2)
+    gp2 = MN.pow_2_generator_powers(log_n + 1)
+    want2 = torch.empty_like(gp2)
+    D.check(lib.mlh_field_neg(ctx, D.ptr(gp2), D.ptr(want2), 2 * n), ctx)
+    assert bool((code == want2).all())
+
+
+@pytest.mark.parametrize("log_n", [12, 16])
+def test_ntt_near_modulus_inputs_match_oracle(log_n):
+    """Random inputs drawn from the top of the range, M - 1 - u with u < 2^64
+    (mixed with zeros and small values), vs the oracle: forward, inverse, RS."""
+    rr = random.Random(900 + log_n)
+    n = 1 << log_n
+    vals = [rr.choice([F.M - 1 - rr.randrange(1 << 64), F.M - 1, 0, 1, rr.randrange(1 << 64)])
+            for _ in range(n)]
+    g = F.pow_2_generator(log_n)
+    got = host(MN.Polynomial(dev(vals)).ntt(g).evals)
+    want = ON.ntt(vals, g)
+    assert got == want
+    assert host(MN.LagrangePolynomial(g, dev(want)).intt().coeffs) == vals
+    g2 = F.pow_2_generator(log_n + 1)
+    assert host(MF.reed_solomon(dev(vals), g2)) == OF.reed_solomon(vals, g2)
+
+
+def test_fri_and_sumcheck_extreme_values_match_oracle():
+    """FRI prove of the RS codeword of the all-(M-1) coefficient vector and of
+    near-modulus random coefficients, and an eq-factored sumcheck with M-1
+    evaluations and points, vs the oracle (roots, last element, transcript,
+    round polynomials)."""
+    top = F.M - 1
+    ln = 10
+    g = F.pow_2_generator(ln + 1)
+    rr = random.Random(77)
+    for coeffs in ([top] * (1 << ln),
+                   [F.M - 1 - rr.randrange(1 << 64) for _ in range(1 << ln)]):
+        code = OF.reed_solomon(coeffs, g)
+        want = OF.FriProof.prove(code, F.pow_2_generator_powers(ln + 1), OT.Transcript())
+        got = MF.FriProof.prove(dev(code), Transcript())
+        assert got.commitments == want.commitments
+        assert got.last_elem == want.last_elem and got.last_random == want.last_random
+        assert got.verify()
+    n = 13
+    ev = [top] * (1 << n)
+    pts = [top] * n
+    total = OPL.mle_evaluate(ev, pts)
+    ot = OS.SumcheckTables.build_tables_for_pcs(pts, ev)
+    otr = OT.Transcript()
+    prev, want_polys = total, []
+    for _ in range(n):
+        nz, _r, prev = ot.compute_sumcheck_polynomial(prev, otr)
+        want_polys.append(tuple(nz))
+    polys, _rs = MS.SumcheckTables.build_tables_for_pcs(pts, dev(ev)).compute_sumcheck_polynomials(
+        total, Transcript())
+    assert polys == want_polys
+
+
 @pytest.mark.slow
 def test_fri_commit_2_24_verifies():
     """Config 3 shape: 2^24 coefficients -> RS code 2^25 -> full FRI prove,
