@@ -171,6 +171,8 @@ def main():
     ap.add_argument("--extra-reps", type=int, default=3, help="reps of the secondary timings")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--extras-budget-s", type=float, default=420.0,
+                    help="watchdog on the secondary timings (0: off)")
     ap.add_argument("--fri-log", type=int, default=28, help="config 5 codeword size (log2)")
     ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas",
                     help="N > 1 headline step: each GPU transforms its own 2^24 polynomial "
@@ -338,6 +340,12 @@ def main():
             "source": "SQ_INSTS_VALU per launch (%s) x 64 lanes / live avg launch time" % valu[1],
         }
 
+    # The extras run collectives at N > 1; if one of them stalls (a rank raising
+    # inside a sharded prove leaves the others waiting in RCCL), every rank's
+    # watchdog prints the headline line measured above and ends the process, so
+    # the driver still gets the K-step measurement.
+    watchdog = _ExtrasWatchdog(result, rank, args.extras_budget_s)
+
     if not args.no_extras and world == 1:
         reps = args.extra_reps
         # inverse NTT (out = NTT(x), so x is rewritten with itself); one
@@ -478,9 +486,51 @@ def main():
 
     if dist is not None:
         dist.barrier()
+    if not watchdog.claim():
+        return  # the watchdog has printed the line and is ending the process
+    if dist is not None:
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+class _ExtrasWatchdog:
+    """After budget_s seconds: rank 0 prints the headline fields (snapshot taken
+    when armed) plus "extras_error", then the process exits with status 0.
+    claim() is called by the main thread when the extras finished in time; the
+    first of the two to take the lock prints."""
+
+    def __init__(self, result, rank, budget_s):
+        import threading
+
+        self._snap = json.loads(json.dumps(result))
+        self._rank = rank
+        self._lock = threading.Lock()
+        self._done = False
+        self._timer = threading.Timer(budget_s, self._fire)
+        self._timer.daemon = True
+        if budget_s > 0:
+            self._timer.start()
+
+    def _take(self):
+        with self._lock:
+            if self._done:
+                return False
+            self._done = True
+            return True
+
+    def claim(self):
+        self._timer.cancel()
+        return self._take()
+
+    def _fire(self):
+        if not self._take():
+            return
+        if self._rank == 0:
+            self._snap["extras_error"] = "secondary timings exceeded the watchdog budget"
+            print(json.dumps(self._snap), flush=True)
+        sys.stdout.flush()
+        os._exit(0)
 
 
 def sharded_ntt_extra(args, pipe, x, world, barrier, log_n, log_p, lib, ctx):
