@@ -357,6 +357,18 @@ def main():
             D.check(lib.mlh_intt(ctx, D.ptr(out), D.ptr(x), log_n, gen), ctx)
         torch.cuda.synchronize()
         result["intt_ms"] = (time.perf_counter() - t0) / 10 * 1e3
+        # Vec -> Vec through pageable host buffers (mlh_ntt_host: the reference's
+        # Polynomial::ntt signature, PCIe copies included) -- reported, never `value`
+        hin = (ctypes.c_uint8 * (16 * N)).from_buffer(bytearray(x.cpu().numpy().tobytes()))
+        hout = (ctypes.c_uint8 * (16 * N))()
+        D.check(lib.mlh_ntt_host(ctx, hin, hout, log_n, gen, 0), ctx)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            D.check(lib.mlh_ntt_host(ctx, hin, hout, log_n, gen, 0), ctx)
+        host_ms = (time.perf_counter() - t0) / reps * 1e3
+        result["ntt_host_pcie_inclusive"] = {"ms": host_ms, "field_elems_per_s": N / (host_ms * 1e-3),
+                                             "note": "host in -> H2D -> NTT -> D2H -> host out"}
+        del hin, hout
         # FRI commit (config 3): coeffs (2^log_n) -> RS code -> Merkle root
         code = D.empty(2 * N, local)
         layers = torch.empty((N * 2 - 1, 32), dtype=torch.uint8, device="cuda:%d" % local)
