@@ -278,7 +278,7 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
     tb->tb[p] = nullptr;
     if (logw > loga)
       MLH_TRY(get_table2d(ctx, ws, R, 1ull << (logw - loga), 1ull << loga, 1, &tb->tb[p],
-                          MLH_XTW));
+                          MLH_XTW == 1));
     S <<= tb->logr[p];
   }
   return MLH_OK;

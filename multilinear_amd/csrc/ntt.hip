@@ -72,13 +72,16 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 // the kernel timer tell the first pass from the middle ones)
 // waves per SIMD the LDS tile allows (160 KiB/CU): caps VGPRs to match
 #ifndef MLH_WPS8
-#define MLH_WPS8 5
+#define MLH_WPS8 4  // R = 2^8: 32 KiB tile + 8 KiB twiddle copy -> 4 workgroups per CU
 #endif
 #ifndef MLH_LAST_STAGED
 #define MLH_LAST_STAGED 1  // last pass loads through LDS (coalesced runs): pass -3..6 %
 #endif
 #ifndef MLH_LDS_PAD
 #define MLH_LDS_PAD 0  // extra dynamic LDS per pass workgroup (occupancy experiments)
+#endif
+#ifndef MLH_LDS_TW
+#define MLH_LDS_TW 1  // stage twiddles of the lane-dependent phases read from an LDS copy
 #endif
 constexpr int pass_waves_per_simd(int logr, int ept) {
   return ept == 16 ? 2 : (logr == 8 ? MLH_WPS8 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2)));
@@ -100,6 +103,21 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   constexpr int TPC = R / EPT;  // threads per column
   constexpr bool LAST = TW == 2;
   __shared__ fe lds[R * kCols];
+#if MLH_LDS_TW
+  // The expanded stage twiddles (R/2 entries x 4 limb-shifted multiples, 2R
+  // fe).  Phase 1 indexes them by compile-time j (scalar loads); the later
+  // phases by a lane-dependent j, where 4 global dwordx4 loads per twiddle per
+  // lane were 3/4 of the pass's vector loads: those read this broadcast copy.
+  // Written here; read only after the first exchange's barriers.
+  __shared__ fe lds_tw[LOGR > LQ ? 2 * R : 1];
+  if constexpr (LOGR > LQ) {
+    constexpr int NT = kCols * R / EPT;  // threads per workgroup
+    static_assert((2 * R) % NT == 0, "twiddle copy: whole rounds");
+#pragma unroll
+    for (int e = 0; e < 2 * R / NT; ++e)
+      lds_tw[e * NT + threadIdx.x] = fe_load(tw + e * NT + threadIdx.x);
+  }
+#endif
 
   const int tid = threadIdx.x;
   const int c = tid % kCols;
@@ -202,10 +220,15 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
           fe v = x[e1];
           if (s > 0) {
             // phase 1 (s0 == 0): j is a compile-time function of i -> uniform load
-            const fe* w = tw + 4 * (j << (LOGR - 1 - s));  // expanded table
             if (s0 == 0) {
+              const fe* w = tw + 4 * (j << (LOGR - 1 - s));  // expanded table
               if ((i & ((1 << s) - 1)) != 0) v = fe_mul_pre(v, w);
             } else {
+#if MLH_LDS_TW
+              const fe* w = lds_tw + 4 * (j << (LOGR - 1 - s));
+#else
+              const fe* w = tw + 4 * (j << (LOGR - 1 - s));
+#endif
               v = fe_mul_pre(v, w);
             }
           }
@@ -273,7 +296,11 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
       const uint64_t jl = jrest & ((1ull << g.loga) - 1);
 #if MLH_XTW
       v = fe_mul_pre(v, ta + 4 * ((k << g.loga) + jl));
+#if MLH_XTW == 1
       if (TW == 0) v = fe_mul_pre(v, tb + 4 * (k * (g.stride >> g.loga) + (jrest >> g.loga)));
+#else
+      if (TW == 0) v = fe_mul(v, tb[k * (g.stride >> g.loga) + (jrest >> g.loga)]);
+#endif
 #else
       v = fe_mul(v, ta[(k << g.loga) + jl]);
       if (TW == 0) v = fe_mul(v, tb[k * (g.stride >> g.loga) + (jrest >> g.loga)]);

@@ -9,7 +9,8 @@ namespace mlh {
 
 constexpr int kMaxPasses = 6;
 #ifndef MLH_XTW
-#define MLH_XTW 0  // inter-pass twiddles as expanded tables (fe_mul_pre)
+#define MLH_XTW 0  // inter-pass twiddles as expanded tables (fe_mul_pre): 1 = TA and TB, 2 = TA only
+
 #endif
 // Inter-pass twiddles w_S^(jrest k) of a pass with W columns, R rows: one
 // table TA[k][jrest] (one modmul per element) while R * W <= 2^kFullTwLog
