@@ -17,8 +17,11 @@
 //     HBM (the permutation is on the per-lane global address, free), so the
 //     DIT output is in natural order;
 //   * passes p < P multiply by the inter-pass twiddle w^(j_rest*k*S_p), read
-//     from a two-level table (T_lo[e & 4095] * T_hi[e >> 12]); for the
-//     inverse, T_lo carries the n^-1 scale so no extra pass is needed;
+//     from one table TA[k][j_rest] or, when that would exceed 2^22 entries,
+//     TA[k][j_lo] * TB[k][j_hi] (TB staged through LDS: one j_hi per tile);
+//     for the inverse, pass 0's TA carries the n^-1 scale (no extra pass);
+//   * stage twiddles: expanded tables (fe_mul_pre), the lane-dependent ones
+//     read from a per-workgroup LDS copy;
 //   * the last pass tiles 8 consecutive k_1 values so its scattered natural-
 //     order stores are still 128-byte runs.
 // Sizes N <= 2^10 use one LDS-resident workgroup (ntt_small).
@@ -82,6 +85,12 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 #endif
 #ifndef MLH_LDS_TW
 #define MLH_LDS_TW 1  // stage twiddles of the lane-dependent phases read from an LDS copy
+#endif
+#ifndef MLH_LDS_TB
+#define MLH_LDS_TB 1  // two-table passes: the tile's TB column staged through LDS
+#endif
+#if MLH_LDS_TB && MLH_XTW
+#error "MLH_LDS_TB assumes plain (non-expanded) inter-pass tables"
 #endif
 constexpr int pass_waves_per_simd(int logr, int ept) {
   return ept == 16 ? 2 : (logr == 8 ? MLH_WPS8 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2)));
@@ -154,6 +163,21 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   }
   const fe* src = in + base + (uint64_t)c * cstride;
   fe* dst = out + base + (uint64_t)c * cstride;
+
+#if MLH_LDS_TB
+  // Two-table twiddle: TB[k][jh] has one jh for the tile's 8 columns (loga >=
+  // 3), so the 8 lanes of a row read the same entry.  One row per thread is
+  // loaded here (its latency hides behind the phases) and shared through LDS
+  // in the epilogue: 8 lane-replicated global loads per thread become 1.
+  constexpr int kTbPerThread = (TW == 0) ? R / (kCols * R / EPT) : 1;
+  fe tbv[kTbPerThread];
+  if constexpr (TW == 0) {
+    constexpr int NT = kCols * R / EPT;
+    const uint64_t jh = jrest >> g.loga, tcols = g.stride >> g.loga;
+#pragma unroll
+    for (int e = 0; e < kTbPerThread; ++e) tbv[e] = fe_load(tb + (uint64_t)(e * NT + tid) * tcols + jh);
+  }
+#endif
 
   // ---- phase 1: load bit-reversed rows, stages 0..2 in registers ---------
   fe x[EPT];
@@ -280,6 +304,15 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   }
 
   // ---- epilogue: inter-pass twiddle, store --------------------------------
+#if MLH_LDS_TB
+  if constexpr (TW == 0) {
+    constexpr int NT = kCols * R / EPT;
+    __syncthreads();  // every lane's reads of the exchange tile are done
+#pragma unroll
+    for (int e = 0; e < kTbPerThread; ++e) lds[e * NT + tid] = tbv[e];
+    __syncthreads();
+  }
+#endif
   uint64_t kbase = 0;
   uint32_t kshift = 0;
   if (LAST) {
@@ -303,7 +336,11 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
 #endif
 #else
       v = fe_mul(v, ta[(k << g.loga) + jl]);
+#if MLH_LDS_TB
+      if (TW == 0) v = fe_mul(v, lds[k]);
+#else
       if (TW == 0) v = fe_mul(v, tb[k * (g.stride >> g.loga) + (jrest >> g.loga)]);
+#endif
 #endif
       fe_store(dst + k * rstride, v);
     } else {
