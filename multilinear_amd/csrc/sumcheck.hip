@@ -29,6 +29,20 @@ namespace mlh {
 constexpr int kRedThreads = 256;
 constexpr uint32_t kTailLogMax = 12;  // sumcheck_tail_kernel: 2 x 2^12 x 16 B = 128 KiB LDS
 
+// Phase timestamps of sumcheck_tail_kernel (tools/tail_bench.hip builds this
+// file with -DMLH_TAIL_PROF; compiled out otherwise).
+#ifdef MLH_TAIL_PROF
+__device__ uint64_t g_tail_ts[64];
+#define MLH_TAIL_TS(i)                                        \
+  do {                                                        \
+    if (threadIdx.x == 0 && (i) < 64) g_tail_ts[i] = wall_clock64(); \
+  } while (0)
+#else
+#define MLH_TAIL_TS(i) \
+  do {                 \
+  } while (0)
+#endif
+
 __device__ __forceinline__ fe shfl_xor_fe(const fe& x, int mask) {
   fe r;
 #pragma unroll
@@ -640,6 +654,7 @@ sumcheck_tail_kernel(fe* m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t,
   __shared__ uint32_t stage[8];
   if (threadIdx.x < sizeof(DevSha) / 4)
     reinterpret_cast<uint32_t*>(&sh)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
+  MLH_TAIL_TS(0);
   fe p = fe_zero();
   if (threadIdx.x == 0) p = fe_load(prev);
   for (uint32_t i = threadIdx.x; i < S; i += blockDim.x) {
@@ -647,12 +662,16 @@ sumcheck_tail_kernel(fe* m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t,
     ld[i] = fe_load(d + i);
   }
   __syncthreads();
+  MLH_TAIL_TS(1);
   const uint32_t S0 = S;
   fe s1 = fe_zero(), s2 = fe_zero();
   tail_sums(lm, ld, S / 2, s1, s2);
+  MLH_TAIL_TS(2);
   for (uint32_t k = 0; S > 1; ++k, S /= 2) {
     const uint32_t h = S / 2;
+    MLH_TAIL_TS(51 + k);
     block_reduce2(s1, s2);
+    MLH_TAIL_TS(3 + 4 * k);
     if (threadIdx.x == 0) {
       const fe e0 = fe_sub(p, s1);
       const fe c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
@@ -661,12 +680,15 @@ sumcheck_tail_kernel(fe* m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t,
       fe_store(polys + 2 * k + 1, c2);
       const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
       dsha_absorb<8>(sh, w, stage);  // LE16(c1) || LE16(c2)
+      MLH_TAIL_TS(4 + 4 * k);
       const fe r = dsha_challenge(sh);
+      MLH_TAIL_TS(5 + 4 * k);
       fe_store(rs + k, r);
       p = fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r))));
       r_sh = r;
     }
     __syncthreads();
+    MLH_TAIL_TS(6 + 4 * k);
     const fe r = r_sh;
     s1 = fe_zero();
     s2 = fe_zero();
@@ -700,6 +722,7 @@ sumcheck_tail_kernel(fe* m, fe* __restrict__ d, uint32_t S, fe* prev, DevSha* t,
     *t = sh;
     fe_store(prev, p);
   }
+  MLH_TAIL_TS(63);
 }
 
 uint32_t sumcheck_tail_rounds(uint32_t log_height) {
