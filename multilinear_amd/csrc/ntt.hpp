@@ -18,9 +18,14 @@ constexpr int kMaxPasses = 6;
 // in TA (two modmuls).  The full table measured -6 % per transform at 2^22
 // and -11 % at 2^20 (it stays in the MALL); at 2^24 (256 MiB read at 16 B per
 // element beside the 32 B of data) pass 0 was no faster, so there the split
-// tables stay.
+// tables stay.  Re-measured with the LDS twiddle copies (MLH_FULL_TW_LOG=24):
+// pass 0 -2..6 %, the transform -1..2 %, for +48 % HBM bytes on pass 0 --
+// kept at 22 (the split tables' traffic stays at the algorithmic bytes).
 constexpr uint32_t kTwLogA = 8;
-constexpr uint32_t kFullTwLog = 22;
+#ifndef MLH_FULL_TW_LOG
+#define MLH_FULL_TW_LOG 22
+#endif
+constexpr uint32_t kFullTwLog = MLH_FULL_TW_LOG;
 
 // Device twiddle tables for one (log_n, generator, direction).
 struct NttTables {
