@@ -171,7 +171,7 @@ def main():
     ap.add_argument("--extra-reps", type=int, default=3, help="reps of the secondary timings")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
-    ap.add_argument("--extras-budget-s", type=float, default=420.0,
+    ap.add_argument("--extras-budget-s", type=float, default=240.0,
                     help="watchdog on the secondary timings (0: off)")
     ap.add_argument("--fri-log", type=int, default=28, help="config 5 codeword size (log2)")
     ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas",
