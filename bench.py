@@ -146,6 +146,40 @@ def load_valu(kernel):
     return None
 
 
+def load_valu_profile():
+    """Per-kernel VALU issue reading of every config's dominant kernels from the
+    newest committed rocprofv3 VALU pass (profile-derived, not live): lane
+    instructions/s against one wave64 instruction per 4 cycles per SIMD at
+    the clock the chip held during that kernel (GRBM_GUI_ACTIVE)."""
+    import glob
+
+    picks = {"ntt_pass_kernel<8, 0, 0, 8>": "config 2 NTT pass 0",
+             "ntt_pass_kernel<8, 1, 0, 8>": "config 2 NTT pass 1",
+             "ntt_pass_kernel<8, 2, 0, 8>": "config 2 NTT last pass",
+             "ntt_pass_kernel<9, 0, 1, 8>": "config 3 RS LDE pass 0",
+             "leaf_pairs_level2_kernel": "config 3 Merkle leaves + 2 levels",
+             "fri_fold_leaves_kernel": "FRI fold + next-tree leaves",
+             "sums_eq_kernel": "config 4 sumcheck round 0 (HBM-streaming)",
+             "fold_sums_eq_kernel": "config 4 sumcheck fold + sums (HBM-streaming)"}
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu.json")), reverse=True)
+    if not paths:
+        return None
+    try:
+        d = json.load(open(paths[0]))
+    except (OSError, ValueError):
+        return None
+    out = {"source": os.path.basename(paths[0]), "kernels": {}}
+    for name, k in d.get("kernels", {}).items():
+        for key, what in picks.items():
+            if name.endswith("mlh::" + key) and k.get("eff_clock_ghz"):
+                ceiling = 256 * 4 * 64 / 4 * k["eff_clock_ghz"] * 1e9
+                out["kernels"][key] = {"what": what, "avg_ms": k["avg_ms"],
+                                       "lane_instr_per_s": k["lane_instr_per_s"],
+                                       "clock_ghz": k["eff_clock_ghz"],
+                                       "issue_frac": k["lane_instr_per_s"] / ceiling}
+    return out
+
+
 def load_pmc(kernel, log_n):
     """HBM traffic per launch from the committed rocprofv3 PMC summary, if it
     matches this kernel/size (tools/pmc_summary.py writes it)."""
@@ -339,6 +373,9 @@ def main():
             "peak_nominal": VALU_PEAK, "frac_nominal": rate / VALU_PEAK,
             "source": "SQ_INSTS_VALU per launch (%s) x 64 lanes / live avg launch time" % valu[1],
         }
+    vp = load_valu_profile() if log_n == 24 else None
+    if vp:
+        result["valu_profile"] = vp
 
     # The extras run collectives at N > 1; if one of them stalls (a rank raising
     # inside a sharded prove leaves the others waiting in RCCL), every rank's
