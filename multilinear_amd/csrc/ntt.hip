@@ -30,6 +30,7 @@
 
 #include <type_traits>
 
+#include "bfly_asm.hpp"
 #include "field.hpp"
 #include "ntt.hpp"
 
@@ -219,46 +220,66 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   }
 
   // Generic register phase: stages [s0, s0+q) on groups of 2^q elements.
+  // Butterflies run two at a time through the generated asm (bfly_asm.hpp) in
+  // the relaxed representation; phase 1's twiddles are wave-uniform (SGPR
+  // operands), the later phases' come from the LDS copy (VGPR operands).
   auto run_phase = [&](auto S0_, auto Q_) {
     constexpr int s0 = decltype(S0_)::value;
     constexpr int q = decltype(Q_)::value;
     constexpr int G = EPT >> q;
+    constexpr int NB = EPT / 2;            // butterflies per stage
+    constexpr int BPG = 1 << (q - 1);      // per group
 #pragma unroll
     for (int s = s0; s < s0 + q; ++s) {
       const int d = 1 << (s - s0);  // element distance inside a group
+      int be0[NB], be1[NB];
+      uint32_t bj[NB];
+      bool btriv[NB];
 #pragma unroll
-      for (int gi = 0; gi < G; ++gi) {
+      for (int b = 0; b < NB; ++b) {
+        const int gi = b / BPG, m = b % BPG;
+        const int i = ((m >> (s - s0)) << (s - s0 + 1)) | (m & (d - 1));
+        be0[b] = gi * (1 << q) + i;
+        be1[b] = be0[b] + d;
         const uint32_t gamma = (uint32_t)(t * G + gi);
         const uint32_t bpos = (gamma & ((1u << s0) - 1u)) | ((gamma >> s0) << (s0 + q));
+        const uint32_t pos = bpos + ((uint32_t)i << s0);
+        bj[b] = pos & ((1u << s) - 1u);
+        // phase 1: j is a compile-time function of i (s == 0 or j == 0: w = 1)
+        btriv[b] = s0 == 0 && (s == 0 || (i & ((1 << s) - 1)) == 0);
+      }
+      if (ZT != 0 && s0 == 0 && s == 0) {  // (u, 0) -> (u, u)
 #pragma unroll
-        for (int i = 0; i < (1 << q); ++i) {
-          if (i & d) continue;
-          const int e0 = gi * (1 << q) + i;
-          const int e1 = e0 + d;
-          const uint32_t pos = bpos + ((uint32_t)i << s0);
-          const uint32_t j = pos & ((1u << s) - 1u);
-          if (ZT != 0 && s0 == 0 && s == 0) {  // (u, 0) -> (u, u)
-            x[e1] = x[e0];
-            continue;
-          }
-          fe v = x[e1];
-          if (s > 0) {
-            // phase 1 (s0 == 0): j is a compile-time function of i -> uniform load
-            if (s0 == 0) {
-              const fe* w = tw + 4 * (j << (LOGR - 1 - s));  // expanded table
-              if ((i & ((1 << s) - 1)) != 0) v = fe_mul_pre(v, w);
-            } else {
+        for (int b = 0; b < NB; ++b) x[be1[b]] = x[be0[b]];
+        continue;
+      }
+      uint64_t rare;
+#pragma unroll
+      for (int b = 0; b < NB; b += 2) {
+        fe& u0 = x[be0[b]];
+        fe& v0 = x[be1[b]];
+        fe& u1 = x[be0[b + 1]];
+        fe& v1 = x[be1[b + 1]];
+        if (s0 == 0) {
+          const fe* w0 = tw + 4 * (bj[b] << (LOGR - 1 - s));
+          const fe* w1 = tw + 4 * (bj[b + 1] << (LOGR - 1 - s));
+          if (!btriv[b] && !btriv[b + 1])
+            bfly_mm_s(u0, v0, w0[0], w0[1], w0[2], w0[3], u1, v1, w1[0], w1[1], w1[2], w1[3], rare);
+          else if (!btriv[b])
+            bfly_mt_s(u0, v0, w0[0], w0[1], w0[2], w0[3], u1, v1, rare);
+          else if (!btriv[b + 1])
+            bfly_mt_s(u1, v1, w1[0], w1[1], w1[2], w1[3], u0, v0, rare);
+          else
+            bfly_tt_v(u0, v0, u1, v1, rare);
+        } else {
 #if MLH_LDS_TW
-              const fe* w = lds_tw + 4 * (j << (LOGR - 1 - s));
+          const fe* w0 = lds_tw + 4 * (bj[b] << (LOGR - 1 - s));
+          const fe* w1 = lds_tw + 4 * (bj[b + 1] << (LOGR - 1 - s));
 #else
-              const fe* w = tw + 4 * (j << (LOGR - 1 - s));
+          const fe* w0 = tw + 4 * (bj[b] << (LOGR - 1 - s));
+          const fe* w1 = tw + 4 * (bj[b + 1] << (LOGR - 1 - s));
 #endif
-              v = fe_mul_pre(v, w);
-            }
-          }
-          const fe u = x[e0];
-          x[e0] = fe_add(u, v);
-          x[e1] = fe_sub(u, v);
+          bfly_mm_v(u0, v0, w0[0], w0[1], w0[2], w0[3], u1, v1, w1[0], w1[1], w1[2], w1[3], rare);
         }
       }
     }
@@ -344,7 +365,7 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
 #endif
       fe_store(dst + k * rstride, v);
     } else {
-      fe_store(out + kbase + (k << kshift), v);
+      fe_store(out + kbase + (k << kshift), relaxed_canon(v));
     }
   }
   (void)TPC;

@@ -713,6 +713,28 @@ def test_reed_solomon_and_fri_commit_vs_c_oracle(log_n):
     assert pd.last_element == last
 
 
+@pytest.mark.parametrize("plan", ["9,4,4", "9,5,4", "4,4,9", "9,9,4", "7,7,7", "9,8,4", "5,5,5,5"])
+def test_forced_plans_vs_c_oracle(plan, monkeypatch):
+    """Radix-2^9 first passes (the default 2^25 plan 9,8,8 starts with one) and
+    every zero-top mode against the C oracle: NTT (pass 0 <9,3,0>), INTT, RS
+    (<9,3,1>: implicit zero half) and RS of bit-reversed coefficients (<9,3,2>,
+    the PCS path), at the plan's size."""
+    monkeypatch.setenv("MLH_NTT_PLAN", plan)
+    C = _c_oracle()
+    log_n = sum(int(v) for v in plan.split(","))
+    g = F.pow_2_generator(log_n)
+    x = D.random_limbs(1 << log_n, 1700 + log_n)
+    assert (D.from_device(MN.Polynomial(D.to_device(x)).ntt(g).evals) == C.ntt(x, log_n, g)).all()
+    assert (D.from_device(MN.LagrangePolynomial(g, D.to_device(x)).intt().coeffs)
+            == C.ntt(x, log_n, g, inverse=True)).all()
+    half = np.ascontiguousarray(x[: 1 << (log_n - 1)])
+    want = C.reed_solomon(half, log_n - 1, g)
+    assert (D.from_device(MF.reed_solomon(D.to_device(half), g)) == want).all()
+    perm = np.array([int(format(i, "0%db" % (log_n - 1))[::-1], 2) for i in range(1 << (log_n - 1))])
+    brev = np.ascontiguousarray(half[perm])
+    assert (D.from_device(MF.reed_solomon_brev(D.to_device(brev), g)) == want).all()
+
+
 @pytest.mark.parametrize("log_n", [0, 1, 4, 9, 10, 11, 13, 17, 20])
 def test_reed_solomon_brev_vs_c_oracle(log_n):
     """Fused bit reversal (ZT == 2 pass-0 loads / small-kernel path) against
