@@ -128,13 +128,27 @@ mlh_status mlh_merkle_batch_commit(mlh_ctx* ctx, const void* dev_items, uint64_t
 mlh_status mlh_fri_fold(mlh_ctx* ctx, const void* dev_layer, uint32_t log_layer, uint32_t k,
                         uint32_t log_domain, const uint8_t r[16], void* dev_next);
 
-/* FriProverData (fri/mod.rs:10-175), device resident. */
+/* FriProverData (fri/mod.rs:10-175), device resident.
+ * gen_pows: the reference's FriProverData::{init,fold} and FriProof::prove
+ * take the table gen_pows and fold with twiddle gen_pows[gen_pows.len() - i 2^k]
+ * (fri/mod.rs:106-110).  The plain entry points assume the canonical table of
+ * the code's own length (pow_2_generator_powers(log_code), what every reference
+ * caller passes); the _gp variants take the table as (gen_pows[1],
+ * log2(gen_pows.len())) for any geometric table of a generator of order exactly
+ * gen_pows.len() (MLH_ERR_BAD_GENERATOR otherwise; MLH_ERR_INVALID when the
+ * table is shorter than half the code, where the reference's index underflows). */
 mlh_status mlh_fri_prover_init(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
                                mlh_transcript* tr, mlh_fri_prover** out); /* :58-76  */
+mlh_status mlh_fri_prover_init_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                                  const uint8_t gen_pows_1[16], uint32_t log_gen_pows,
+                                  mlh_transcript* tr, mlh_fri_prover** out);
 mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
                                     const uint8_t r[16], mlh_transcript* tr); /* :79-134 */
 mlh_status mlh_fri_prover_fold(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
                                mlh_transcript* tr, mlh_fri_prover** out); /* :136-145 */
+mlh_status mlh_fri_prover_fold_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                                  const uint8_t gen_pows_1[16], uint32_t log_gen_pows,
+                                  mlh_transcript* tr, mlh_fri_prover** out);
 uint32_t mlh_fri_prover_num_trees(const mlh_fri_prover* p);
 mlh_status mlh_fri_prover_roots(const mlh_fri_prover* p, uint8_t* roots_out /* [T][32] */);
 /* last_element (fri/mod.rs:13); MLH_ERR_INVALID while still None. */
@@ -160,9 +174,12 @@ typedef struct mlh_fri_proof {
   uint8_t* queries;        /* [num_queries][mlh_fri_query_bytes(L)]  */
 } mlh_fri_proof;
 uint64_t mlh_fri_query_bytes(uint32_t log_code);
-/* FriProof::prove (fri/mod.rs:261-285). */
+/* FriProof::prove (fri/mod.rs:261-285); _gp: with the caller's gen_pows (above). */
 mlh_status mlh_fri_prove(mlh_ctx* ctx, const void* dev_code, uint32_t log_code, mlh_transcript* tr,
                          mlh_fri_proof* proof);
+mlh_status mlh_fri_prove_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                            const uint8_t gen_pows_1[16], uint32_t log_gen_pows, mlh_transcript* tr,
+                            mlh_fri_proof* proof);
 /* Wire format: serde + bincode 2 standard / little-endian / fixed-int encoding
  * of FriProof<Field128> (fri/mod.rs:239-249, 367-397; field.rs:40-64) -- the
  * bytes the reference's bincode::serde::encode_to_vec produces.  encode needs

@@ -24,6 +24,7 @@ STATUS_NAMES = {
     8: "MLH_ERR_VERIFY_INDEX",
 }
 STATUS_CODES = {v: k for k, v in STATUS_NAMES.items()}
+globals().update(STATUS_CODES)  # MLH_ERR_INVALID, ... as module constants
 LOG_BLOWUP = 1
 NUM_QUERIES = 128
 
@@ -110,6 +111,8 @@ SIGNATURES = {
     "mlh_fri_prover_init": (_I, [_P, _P, _U32, _P, ctypes.POINTER(_P)]),
     "mlh_fri_prover_fold_step": (_I, [_P, _P, _U32, _P, _P]),
     "mlh_fri_prover_fold": (_I, [_P, _P, _U32, _P, ctypes.POINTER(_P)]),
+    "mlh_fri_prover_init_gp": (_I, [_P, _P, _U32, _P, _U32, _P, ctypes.POINTER(_P)]),
+    "mlh_fri_prover_fold_gp": (_I, [_P, _P, _U32, _P, _U32, _P, ctypes.POINTER(_P)]),
     "mlh_fri_prover_num_trees": (_U32, [_P]),
     "mlh_fri_prover_roots": (_I, [_P, _P]),
     "mlh_fri_prover_last_element": (_I, [_P, _P]),
@@ -118,6 +121,7 @@ SIGNATURES = {
     "mlh_fri_prover_destroy": (None, [_P]),
     "mlh_fri_query_bytes": (_U64, [_U32]),
     "mlh_fri_prove": (_I, [_P, _P, _U32, _P, ctypes.POINTER(FriProofC)]),
+    "mlh_fri_prove_gp": (_I, [_P, _P, _U32, _P, _U32, _P, ctypes.POINTER(FriProofC)]),
     "mlh_fri_verify": (_I, [ctypes.POINTER(FriProofC)]),
     "mlh_fri_proof_encoded_size": (_U64, [ctypes.POINTER(FriProofC)]),
     "mlh_fri_proof_encode": (_I, [ctypes.POINTER(FriProofC), _P, _U64]),

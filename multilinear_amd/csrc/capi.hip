@@ -582,11 +582,17 @@ mlh_status mlh_merkle_batch_commit(mlh_ctx* ctx, const void* dev_items, uint64_t
   return read_root(ctx, layers, count, root_out);
 }
 
-static mlh_status fold_tables(mlh_ctx* ctx, uint32_t log_domain, const fe** tlo, const fe** thi) {
-  const u128 ginv = h_inv(h_pow2_generator(log_domain));
+// Fold twiddles gen_pows[len - e] = g^(-e), e < len = 2^log_len (fri/mod.rs:106-110),
+// as T_lo[e mod 4096] * T_hi[e / 4096] of g^-1.
+static mlh_status fold_tables_g(mlh_ctx* ctx, u128 g, uint32_t log_len, const fe** tlo,
+                                const fe** thi) {
+  const u128 ginv = h_inv(g);
   MLH_TRY(get_table(ctx, ginv, 4096, 1, tlo));
-  MLH_TRY(get_table(ctx, h_pow(ginv, 4096), hi_count(log_domain), 1, thi));
+  MLH_TRY(get_table(ctx, h_pow(ginv, 4096), hi_count(log_len), 1, thi));
   return MLH_OK;
+}
+static mlh_status fold_tables(mlh_ctx* ctx, uint32_t log_domain, const fe** tlo, const fe** thi) {
+  return fold_tables_g(ctx, h_pow2_generator(log_domain), log_domain, tlo, thi);
 }
 
 mlh_status mlh_fri_fold(mlh_ctx* ctx, const void* dev_layer, uint32_t log_layer, uint32_t k,
@@ -618,6 +624,11 @@ struct FriLayer {
 struct mlh_fri_prover {
   mlh_ctx* ctx;
   uint32_t log_code;
+  // gen_pows of the reference's FriProverData calls (fri/mod.rs:58,79,136,261):
+  // a geometric table of 2^log_gp powers of gp_gen; fold twiddle
+  // gen_pows[len - i 2^k] = gp_gen^(-i 2^k).  Default: the code's domain.
+  u128 gp_gen = 0;
+  uint32_t log_gp = 0;
   std::vector<FriLayer> layers;
   bool has_last = false;
   uint8_t last[16];
@@ -629,16 +640,44 @@ struct mlh_fri_prover {
   }
 };
 
+// gen_pows = [g^0 .. g^(2^log_gp - 1)] (NttField::pow_2_generator_powers,
+// ntt/mod.rs:18-28, or any generator of order exactly 2^log_gp).  The
+// reference indexes gen_pows[len - i 2^k] with i 2^k < 2^(log_code - 1), so a
+// table shorter than half the code underflows its index (a panic there).
+static mlh_status set_gen_pows(mlh_ctx* ctx, mlh_fri_prover* p, const uint8_t* gen,
+                               uint32_t log_gp) {
+  if (!gen) {
+    p->gp_gen = h_pow2_generator(p->log_code);
+    p->log_gp = p->log_code;
+    return MLH_OK;
+  }
+  if (log_gp > 40 || log_gp + 1 < p->log_code)
+    return fail(ctx, MLH_ERR_INVALID, "gen_pows shorter than half the code");
+  const u128 g = h_load(gen);
+  if (!check_generator(g, log_gp))
+    return fail(ctx, MLH_ERR_BAD_GENERATOR, "gen_pows[1] must have order exactly gen_pows.len()");
+  p->gp_gen = g;
+  p->log_gp = log_gp;
+  return MLH_OK;
+}
+
 extern "C" {
 
 mlh_status mlh_fri_prover_init(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
                                mlh_transcript* tr, mlh_fri_prover** out) {
+  return mlh_fri_prover_init_gp(ctx, dev_code, log_code, nullptr, 0, tr, out);
+}
+
+mlh_status mlh_fri_prover_init_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                                  const uint8_t gen_pows_1[16], uint32_t log_gen_pows,
+                                  mlh_transcript* tr, mlh_fri_prover** out) {
   if (!ctx || !dev_code || !tr || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
   if (log_code < 1 || log_code > 40)
     return fail(ctx, MLH_ERR_NOT_POW2, "Input size must be a power of two");
   std::unique_ptr<mlh_fri_prover> p(new mlh_fri_prover());
   p->ctx = ctx;
   p->log_code = log_code;
+  MLH_TRY(set_gen_pows(ctx, p.get(), gen_pows_1, log_gen_pows));
   FriLayer l0;
   l0.values = reinterpret_cast<const fe*>(dev_code);
   l0.log_n = log_code;
@@ -664,7 +703,7 @@ mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
   const uint64_t half_n = 1ull << (log_n - 1);
   if (k + log_n != p->log_code) return fail(ctx, MLH_ERR_INVALID, "fold index k out of sequence");
   const fe *tlo, *thi;
-  MLH_TRY(fold_tables(ctx, p->log_code, &tlo, &thi));
+  MLH_TRY(fold_tables_g(ctx, p->gp_gen, p->log_gp, &tlo, &thi));
   const fe rr = to_fe(h_load(r));
   FriLayer nx;
   nx.log_n = log_n - 1;
@@ -674,7 +713,7 @@ mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
   nx.values = reinterpret_cast<const fe*>(vals);
   if (half_n == blowup) {  // fri/mod.rs:116-126
     HIP_TRY(ctx, launch_fri_fold(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), rr, tlo,
-                                 thi, k, 1ull << p->log_code, ctx->stream));
+                                 thi, k, 1ull << p->log_gp, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, vals, 32, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     pool_free(ctx, vals);
@@ -690,7 +729,7 @@ mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
   MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
   nx.tree = reinterpret_cast<uint8_t*>(tree);
   HIP_TRY(ctx, launch_fri_fold_commit(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
-                                      nx.tree, rr, tlo, thi, k, 1ull << p->log_code,
+                                      nx.tree, rr, tlo, thi, k, 1ull << p->log_gp,
                                       ctx->stream));
   MLH_TRY(read_root(ctx, nx.tree, L, nx.root));
   p->layers.push_back(nx);
@@ -743,7 +782,11 @@ struct FriDevLoop {
     off_prev = off_polys + 32 * steps;
     off_extra = off_prev + 16;
     MLH_TRY(scratch.alloc(off_extra + 16 * (n_extra ? n_extra : 1)));
-    MLH_TRY(fold_tables(ctx, log_code, &tlo, &thi));
+    if (!p->log_gp) {
+      p->gp_gen = h_pow2_generator(log_code);
+      p->log_gp = log_code;
+    }
+    MLH_TRY(fold_tables_g(ctx, p->gp_gen, p->log_gp, &tlo, &thi));
     memcpy(ctx->pinned, &tr->sha, sizeof(DevSha));
     HIP_TRY(ctx, hipMemcpyAsync(dt(), ctx->pinned, sizeof(DevSha), hipMemcpyHostToDevice,
                                 ctx->stream));
@@ -830,7 +873,7 @@ struct FriDevLoop {
     MLH_TRY(pool_alloc(ctx, half_n * sizeof(fe), &vals));
     if (half_n == (1ull << MLH_LOG_BLOWUP)) {  // fri/mod.rs:116-126
       HIP_TRY(ctx, launch_fri_fold(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), fe{},
-                                   tlo, thi, k, 1ull << p->log_code, ctx->stream, ShardMap(), rp));
+                                   tlo, thi, k, 1ull << p->log_gp, ctx->stream, ShardMap(), rp));
       HIP_TRY(ctx, launch_fri_last(reinterpret_cast<const fe*>(vals), dt(),
                                    reinterpret_cast<uint32_t*>(sb() + off_flag),
                                    reinterpret_cast<fe*>(sb() + off_last), ctx->stream));
@@ -850,7 +893,7 @@ struct FriDevLoop {
     const uint32_t t = (uint32_t)p->layers.size() - 1;
     HIP_TRY(ctx, launch_fri_fold_commit(
                      cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), nx.tree, fe{}, tlo,
-                     thi, k, 1ull << p->log_code, ctx->stream, ShardMap(), rp,
+                     thi, k, 1ull << p->log_gp, ctx->stream, ShardMap(), rp,
                      RootAbsorb{dt(), challenge_next ? r(k + 1) : nullptr, root(t)}));
     return MLH_OK;
   }
@@ -885,7 +928,8 @@ struct FriDevLoop {
 // the end; the host transcript then replays the same absorbs (root_0,
 // root_1, ..., last element) and ends in the identical state.
 static mlh_status fri_fold_device(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
-                                  mlh_transcript* tr, mlh_fri_prover** out) {
+                                  const uint8_t* gen, uint32_t log_gp, mlh_transcript* tr,
+                                  mlh_fri_prover** out) {
   if (!ctx || !dev_code || !tr || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
   if (log_code < 2 || log_code > 40)
     return fail(ctx, log_code < 2 ? MLH_ERR_INVALID : MLH_ERR_NOT_POW2,
@@ -893,6 +937,7 @@ static mlh_status fri_fold_device(mlh_ctx* ctx, const void* dev_code, uint32_t l
   std::unique_ptr<mlh_fri_prover> p(new mlh_fri_prover());
   p->ctx = ctx;
   p->log_code = log_code;
+  MLH_TRY(set_gen_pows(ctx, p.get(), gen, log_gp));
   FriDevLoop lp(ctx, p.get());
   MLH_TRY(lp.init(dev_code, log_code, tr, true));
   const uint32_t steps = log_code - MLH_LOG_BLOWUP;
@@ -908,7 +953,14 @@ extern "C" {
 
 mlh_status mlh_fri_prover_fold(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
                                mlh_transcript* tr, mlh_fri_prover** out) {
-  return fri_fold_device(ctx, dev_code, log_code, tr, out);
+  return fri_fold_device(ctx, dev_code, log_code, nullptr, 0, tr, out);
+}
+
+mlh_status mlh_fri_prover_fold_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                                  const uint8_t gen_pows_1[16], uint32_t log_gen_pows,
+                                  mlh_transcript* tr, mlh_fri_prover** out) {
+  if (!gen_pows_1) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  return fri_fold_device(ctx, dev_code, log_code, gen_pows_1, log_gen_pows, tr, out);
 }
 
 uint32_t mlh_fri_prover_num_trees(const mlh_fri_prover* p) {
@@ -1185,6 +1237,18 @@ mlh_status mlh_fri_prove(mlh_ctx* ctx, const void* dev_code, uint32_t log_code, 
   if (!ctx || !dev_code || !tr || !proof) return fail(ctx, MLH_ERR_INVALID, "null argument");
   mlh_fri_prover* p = nullptr;
   MLH_TRY(mlh_fri_prover_fold(ctx, dev_code, log_code, tr, &p));
+  mlh_status s = fri_queries(ctx, p, tr, proof);
+  mlh_fri_prover_destroy(p);
+  return s;
+}
+
+mlh_status mlh_fri_prove_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
+                            const uint8_t gen_pows_1[16], uint32_t log_gen_pows, mlh_transcript* tr,
+                            mlh_fri_proof* proof) {
+  if (!ctx || !dev_code || !tr || !proof || !gen_pows_1)
+    return fail(ctx, MLH_ERR_INVALID, "null argument");
+  mlh_fri_prover* p = nullptr;
+  MLH_TRY(mlh_fri_prover_fold_gp(ctx, dev_code, log_code, gen_pows_1, log_gen_pows, tr, &p));
   mlh_status s = fri_queries(ctx, p, tr, proof);
   mlh_fri_prover_destroy(p);
   return s;

@@ -57,11 +57,18 @@ class FriProverData:
             pass
 
     @staticmethod
-    def init(code, transcript, device=0):
+    def init(code, transcript, device=0, gen_pows=None):
+        """gen_pows: None (canonical table of the code's length) or
+        (gen_pows[1], log2(gen_pows.len())), used by the later fold steps."""
         ctx = context(device)
         h = ctypes.c_void_p()
-        check(lib().mlh_fri_prover_init(ctx, ptr(code), _log2(code.shape[0]), transcript.h,
-                                        ctypes.byref(h)), ctx)
+        if gen_pows is None:
+            check(lib().mlh_fri_prover_init(ctx, ptr(code), _log2(code.shape[0]), transcript.h,
+                                            ctypes.byref(h)), ctx)
+        else:
+            check(lib().mlh_fri_prover_init_gp(ctx, ptr(code), _log2(code.shape[0]),
+                                               fe_bytes(gen_pows[0]), gen_pows[1], transcript.h,
+                                               ctypes.byref(h)), ctx)
         return FriProverData(h.value, code)
 
     def fold_step(self, k, r, transcript, device=0):
@@ -69,11 +76,16 @@ class FriProverData:
         check(lib().mlh_fri_prover_fold_step(ctx, self.h, k, fe_bytes(r), transcript.h), ctx)
 
     @staticmethod
-    def fold(code, transcript, device=0):
+    def fold(code, transcript, device=0, gen_pows=None):
         ctx = context(device)
         h = ctypes.c_void_p()
-        check(lib().mlh_fri_prover_fold(ctx, ptr(code), _log2(code.shape[0]), transcript.h,
-                                        ctypes.byref(h)), ctx)
+        if gen_pows is None:
+            check(lib().mlh_fri_prover_fold(ctx, ptr(code), _log2(code.shape[0]), transcript.h,
+                                            ctypes.byref(h)), ctx)
+        else:
+            check(lib().mlh_fri_prover_fold_gp(ctx, ptr(code), _log2(code.shape[0]),
+                                               fe_bytes(gen_pows[0]), gen_pows[1], transcript.h,
+                                               ctypes.byref(h)), ctx)
         return FriProverData(h.value, code)
 
     def fold_roots(self):
@@ -127,12 +139,18 @@ class FriProof:
         self.c.queries = ctypes.cast(self._q, ctypes.c_void_p)
 
     @staticmethod
-    def prove(code, transcript, device=0):
-        """FriProof::prove (fri/mod.rs:261-285)."""
+    def prove(code, transcript, device=0, gen_pows=None):
+        """FriProof::prove (fri/mod.rs:261-285).  gen_pows: None for the
+        canonical table of the code's length, else (gen_pows[1], log2(len))."""
         ctx = context(device)
         lc = _log2(code.shape[0])
         p = FriProof(lc)
-        check(lib().mlh_fri_prove(ctx, ptr(code), lc, transcript.h, ctypes.byref(p.c)), ctx)
+        if gen_pows is None:
+            check(lib().mlh_fri_prove(ctx, ptr(code), lc, transcript.h, ctypes.byref(p.c)), ctx)
+        else:
+            g, lg = gen_pows
+            check(lib().mlh_fri_prove_gp(ctx, ptr(code), lc, fe_bytes(g), lg, transcript.h,
+                                         ctypes.byref(p.c)), ctx)
         return p
 
     @property

@@ -450,3 +450,236 @@ void orc_fold(uint8_t* m, uint8_t* d, uint32_t log_h, const uint8_t rb[16]) {
 void orc_mul(const uint8_t a[16], const uint8_t b[16], uint8_t out[16]) {
   st(out, fmul(ld(a), ld(b)));
 }
+
+/* ------------------------------------------------------- parallel checkers */
+/* The same arithmetic with OpenMP over independent work (butterflies of a
+ * stage, leaves/nodes of a Merkle level, entries of the eq table, pairs of a
+ * fold).  Field results are exact, so they equal the serial restatement; these
+ * exist only so the full-size parity tests (config 3 at 2^25, config 4 at 24
+ * variables, config 5 at 2^28) finish within a test's time limit on the GPU
+ * box's host cores.  Not a baseline. */
+static void pow_series_par(u128* pw, uint64_t count, u128 g, int threads) {
+#pragma omp parallel num_threads(threads)
+  {
+#ifdef _OPENMP
+    const int t = omp_get_thread_num(), T = omp_get_num_threads();
+#else
+    const int t = 0, T = 1;
+#endif
+    const uint64_t lo = count * (uint64_t)t / (uint64_t)T, hi = count * (uint64_t)(t + 1) / (uint64_t)T;
+    u128 acc = fpow(g, (u128)lo);
+    for (uint64_t j = lo; j < hi; j++) {
+      pw[j] = acc;
+      acc = fmul(acc, g);
+    }
+  }
+}
+
+int orc_ntt_par(const uint8_t* in, uint8_t* out, uint32_t log_n, const uint8_t gen[16], int inverse,
+                int threads) {
+  const uint64_t n = 1ull << log_n;
+  if (log_n < 1) return 2;
+  u128* v = (u128*)malloc(n * sizeof(u128));
+  u128* pw = (u128*)malloc((n / 2) * sizeof(u128));
+  if (!v || !pw) return 5;
+  memcpy(v, in, n * 16);
+  const long long N = (long long)n;
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (long long i = 0; i < N; i++) {
+    const uint64_t j = rev_bits((uint64_t)i, (int)log_n);
+    if ((uint64_t)i < j) {
+      u128 t = v[i];
+      v[i] = v[j];
+      v[j] = t;
+    }
+  }
+  u128 g = ld(gen);
+  if (inverse) g = finv(g);
+  pow_series_par(pw, n / 2, g, threads);  /* stage len: twiddle j = g^(j n/len) */
+  const uint64_t B = n < (1ull << 14) ? n : (1ull << 14);
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (long long b = 0; b < (long long)(n / B); b++) {
+    u128* blk = v + (uint64_t)b * B;
+    for (uint64_t len = 2; len <= B; len *= 2)
+      for (uint64_t i = 0; i < B; i += len)
+        for (uint64_t j = 0; j < len / 2; j++) {
+          const u128 w = fmul(blk[i + j + len / 2], pw[j * (n / len)]), u = blk[i + j];
+          blk[i + j] = fadd(u, w);
+          blk[i + j + len / 2] = fsub(u, w);
+        }
+  }
+  for (uint64_t len = 2 * B; len <= n; len *= 2) {
+    const long long half = (long long)(len / 2);
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (long long q = 0; q < N / 2; q++) {
+      const uint64_t i = ((uint64_t)q / half) * len, j = (uint64_t)q % half;
+      const u128 w = fmul(v[i + j + half], pw[j * (n / len)]), u = v[i + j];
+      v[i + j] = fadd(u, w);
+      v[i + j + half] = fsub(u, w);
+    }
+  }
+  if (inverse) {
+    const u128 ninv = finv((u128)n);
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (long long i = 0; i < N; i++) v[i] = fmul(v[i], ninv);
+  }
+  memcpy(out, v, n * 16);
+  free(v);
+  free(pw);
+  return 0;
+}
+
+int orc_reed_solomon_par(const uint8_t* coeffs, uint32_t log_n, const uint8_t gen[16], uint8_t* code,
+                         int threads) {
+  const uint64_t n = 1ull << log_n;
+  uint8_t* tmp = (uint8_t*)calloc(2 * n, 16);
+  if (!tmp) return 5;
+  memcpy(tmp, coeffs, n * 16);
+  const int r = orc_ntt_par(tmp, code, log_n + 1, gen, 0, threads);
+  free(tmp);
+  return r;
+}
+
+static void merkle_pairs_par(const uint8_t* code, uint32_t log_code, uint8_t* layers, int threads) {
+  const uint64_t n = 1ull << log_code, L = n / 2;
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (long long i = 0; i < (long long)L; i++) {
+    uint8_t leaf[32];
+    memcpy(leaf, code + 16 * (uint64_t)i, 16);
+    memcpy(leaf + 16, code + 16 * ((uint64_t)i + L), 16);
+    orc_sha256(leaf, 32, layers + 32 * (uint64_t)i);
+  }
+  uint64_t off = 0, cnt = L;
+  while (cnt > 1) {
+#pragma omp parallel for num_threads(threads) schedule(static) if (cnt > 4096)
+    for (long long j = 0; j < (long long)(cnt / 2); j++)
+      orc_sha256(layers + 32 * (off + 2 * (uint64_t)j), 64, layers + 32 * (off + cnt + (uint64_t)j));
+    off += cnt;
+    cnt /= 2;
+  }
+}
+
+/* orc_fri_commit with the work of each layer in parallel; gen_pows has
+ * 2^log_gp >= 2^log_code entries of the order-2^log_gp generator (the
+ * reference's fold twiddle is gen_pows[len - i 2^k], len = gen_pows.len()). */
+int orc_fri_commit_par(const uint8_t* code, uint32_t log_code, uint32_t log_gp, uint8_t* roots,
+                       uint8_t last[16], uint8_t last_random[32], int threads) {
+  const uint64_t n0 = 1ull << log_code, glen = 1ull << log_gp;
+  if (log_gp < log_code) return 2;
+  sha_t tr;
+  sha_init(&tr);
+  const u128 g = fpow(3, (MOD - 1) >> log_gp), inv2 = finv(2);
+  u128* gp = (u128*)malloc(glen * sizeof(u128));
+  u128* layer = (u128*)malloc(n0 * sizeof(u128));
+  u128* next = (u128*)malloc((n0 / 2) * sizeof(u128));
+  uint8_t* tree = (uint8_t*)malloc((n0 - 1) * 32);
+  if (!gp || !layer || !next || !tree) return 5;
+  pow_series_par(gp, glen, g, threads);
+  memcpy(layer, code, n0 * 16);
+  uint64_t n = n0;
+  uint32_t t = 0;
+  merkle_pairs_par((const uint8_t*)layer, log_code, tree, threads);
+  memcpy(roots + 32 * t, tree + 32 * (n - 2), 32);
+  sha_update(&tr, roots + 32 * t, 32);
+  t++;
+  int rc = 0;
+  for (uint32_t k = 0; k + 1 < log_code; k++) {
+    uint8_t rnd[32];
+    sha_final(&tr, rnd);
+    u128 r = ld(rnd);
+    if (r >= MOD) r -= MOD;
+    const uint64_t half = n / 2;
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (long long ii = 0; ii < (long long)half; ii++) {
+      const uint64_t i = (uint64_t)ii;
+      const u128 a = layer[i], b = layer[i + half];
+      const u128 tw = i == 0 ? 1 : gp[glen - i * (1ull << k)];
+      const u128 odd = fmul(fsub(a, b), tw);
+      next[i] = fmul(fadd(fadd(a, b), fmul(r, odd)), inv2);
+    }
+    memcpy(layer, next, half * 16);
+    n = half;
+    if (half == 2) {
+      if (layer[0] != layer[1]) rc = 6;
+      st(last, layer[0]);
+      sha_update(&tr, last, 16);
+      break;
+    }
+    merkle_pairs_par((const uint8_t*)layer, (uint32_t)__builtin_ctzll(n), tree, threads);
+    memcpy(roots + 32 * t, tree + 32 * (n - 2), 32);
+    sha_update(&tr, roots + 32 * t, 32);
+    t++;
+  }
+  if (last_random) sha_final(&tr, last_random);
+  free(layer);
+  free(next);
+  free(tree);
+  free(gp);
+  return rc;
+}
+
+void orc_eq_table_par(const uint8_t* pts, uint32_t n, uint8_t* out, int threads) {
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (long long ii = 0; ii < (long long)(1ull << n); ii++) {
+    const uint64_t idx = (uint64_t)ii;
+    u128 acc = 1;
+    for (uint32_t i = 0; i < n; i++) {
+      const u128 p = ld(pts + 16 * (n - 1 - i));
+      acc = fmul(acc, ((idx >> i) & 1) ? p : fsub(1, p));
+    }
+    st(out + 16 * idx, acc);
+  }
+}
+
+void orc_partial_sums_par(const uint8_t* m, const uint8_t* d, uint32_t log_h, uint8_t out[32],
+                          int threads) {
+  const uint64_t off = (1ull << log_h) / 2;
+  u128 s1 = 0, s2 = 0;
+  const u128 r = 2, s = fsub(1, r);
+#pragma omp parallel num_threads(threads)
+  {
+    u128 a1 = 0, a2 = 0;
+#pragma omp for schedule(static)
+    for (long long ii = 0; ii < (long long)off; ii++) {
+      const uint64_t i = (uint64_t)ii;
+      a1 = fadd(a1, fmul(ld(m + 16 * (i + off)), ld(d + 16 * (i + off))));
+      const u128 dd = fadd(fmul(s, ld(d + 16 * i)), fmul(r, ld(d + 16 * (i + off))));
+      const u128 mm = fadd(fmul(s, ld(m + 16 * i)), fmul(r, ld(m + 16 * (i + off))));
+      a2 = fadd(a2, fmul(mm, dd));
+    }
+#pragma omp critical
+    {
+      s1 = fadd(s1, a1);
+      s2 = fadd(s2, a2);
+    }
+  }
+  st(out, s1);
+  st(out + 16, s2);
+}
+
+void orc_fold_par(uint8_t* m, uint8_t* d, uint32_t log_h, const uint8_t rb[16], int threads) {
+  const uint64_t off = (1ull << log_h) / 2;
+  const u128 r = ld(rb), s = fsub(1, r);
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (long long ii = 0; ii < (long long)off; ii++) {
+    const uint64_t i = (uint64_t)ii;
+    st(d + 16 * i, fadd(fmul(s, ld(d + 16 * i)), fmul(r, ld(d + 16 * (i + off)))));
+    st(m + 16 * i, fadd(fmul(s, ld(m + 16 * i)), fmul(r, ld(m + 16 * (i + off)))));
+  }
+}
+
+/* sum_i m[i] d[i] (the claimed sum of the PCS sumcheck, polynomials.rs:165-187
+ * as an eq-table dot product) */
+void orc_dot_par(const uint8_t* m, const uint8_t* d, uint32_t log_n, uint8_t out[16], int threads) {
+  u128 tot = 0;
+#pragma omp parallel num_threads(threads)
+  {
+    u128 acc = 0;
+#pragma omp for schedule(static)
+    for (long long ii = 0; ii < (long long)(1ull << log_n); ii++)
+      acc = fadd(acc, fmul(ld(m + 16 * (uint64_t)ii), ld(d + 16 * (uint64_t)ii)));
+#pragma omp critical
+    tot = fadd(tot, acc);
+  }
+  st(out, tot);
+}

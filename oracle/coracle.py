@@ -30,6 +30,14 @@ def lib():
         L.orc_ntt_omp.argtypes = [P, P, U, P, ctypes.c_int]
         L.orc_pow_2_generator.argtypes = [U, P]
         L.orc_pow_2_generator_powers.argtypes = [U, P]
+        I = ctypes.c_int
+        L.orc_ntt_par.argtypes = [P, P, U, P, I, I]
+        L.orc_reed_solomon_par.argtypes = [P, U, P, P, I]
+        L.orc_fri_commit_par.argtypes = [P, U, U, P, P, P, I]
+        L.orc_eq_table_par.argtypes = [P, U, P, I]
+        L.orc_partial_sums_par.argtypes = [P, P, U, P, I]
+        L.orc_fold_par.argtypes = [P, P, U, P, I]
+        L.orc_dot_par.argtypes = [P, P, U, P, I]
         _lib = L
     return _lib
 
@@ -118,4 +126,65 @@ def sha256(msg: bytes) -> bytes:
 def mul(a, b):
     out = np.zeros(16, dtype=np.uint8)
     lib().orc_mul(_p(_fe(a)), _p(_fe(b)), _p(out))
+    return int.from_bytes(bytes(out), "little")
+
+
+# ---- parallel checkers (same arithmetic, OpenMP; full-size parity tests) ----
+
+def threads():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def ntt_par(limbs, log_n, gen, inverse=False):
+    a = np.ascontiguousarray(limbs, dtype=np.uint32)
+    out = np.empty_like(a)
+    rc = lib().orc_ntt_par(_p(a), _p(out), log_n, _p(_fe(gen)), 1 if inverse else 0, threads())
+    assert rc == 0
+    return out
+
+
+def reed_solomon_par(limbs, log_n, gen):
+    a = np.ascontiguousarray(limbs, dtype=np.uint32)
+    out = np.empty((2 * a.shape[0], 4), dtype=np.uint32)
+    rc = lib().orc_reed_solomon_par(_p(a), log_n, _p(_fe(gen)), _p(out), threads())
+    assert rc == 0
+    return out
+
+
+def fri_commit_par(limbs, log_code, log_gp=None):
+    """FriProverData::fold with gen_pows of 2^log_gp entries (default: the code
+    length) -> (roots, last_elem, last_random, rc)."""
+    a = np.ascontiguousarray(limbs, dtype=np.uint32)
+    roots = np.zeros((log_code - 1, 32), dtype=np.uint8)
+    last = np.zeros(16, dtype=np.uint8)
+    lr = np.zeros(32, dtype=np.uint8)
+    rc = lib().orc_fri_commit_par(_p(a), log_code, log_code if log_gp is None else log_gp, _p(roots),
+                                  _p(last), _p(lr), threads())
+    return [bytes(r) for r in roots], int.from_bytes(bytes(last), "little"), bytes(lr), rc
+
+
+def eq_table_par(points):
+    pts = np.frombuffer(b"".join(int(p).to_bytes(16, "little") for p in points) or b"\0" * 16,
+                        dtype=np.uint8).copy()
+    out = np.empty((1 << len(points), 4), dtype=np.uint32)
+    lib().orc_eq_table_par(_p(pts), len(points), _p(out), threads())
+    return out
+
+
+def partial_sums_par(m, d, log_h):
+    out = np.zeros(32, dtype=np.uint8)
+    lib().orc_partial_sums_par(_p(np.ascontiguousarray(m)), _p(np.ascontiguousarray(d)), log_h, _p(out),
+                               threads())
+    b = bytes(out)
+    return int.from_bytes(b[:16], "little"), int.from_bytes(b[16:], "little")
+
+
+def fold_par(m, d, log_h, r):
+    """In place on (contiguous uint32) m and d."""
+    lib().orc_fold_par(_p(m), _p(d), log_h, _p(_fe(r)), threads())
+
+
+def dot_par(m, d, log_n):
+    out = np.zeros(16, dtype=np.uint8)
+    lib().orc_dot_par(_p(np.ascontiguousarray(m)), _p(np.ascontiguousarray(d)), log_n, _p(out), threads())
     return int.from_bytes(bytes(out), "little")
