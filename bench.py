@@ -3,16 +3,18 @@
 Metric: "NTT 2^24 field-elems/sec + FRI commit ms; % HBM roofline".
   * N = 1: step = one forward 2^24-point NTT (config 2, src/ntt/mod.rs:69-110)
             over a device-resident synthetic vector (seeded uniform elements);
-  * N > 1 (default --mode replicas): every rank transforms its own 2^24-point
-            polynomial per step -- independent objects, no data-path
-            collective, weak scaling;
-  * N > 1, extra "sharded_ntt" (and the headline with --mode sharded): one
-            forward NTT of N * 2^24 points per step, 2^24 per GPU: local NTT,
-            one RCCL all-to-all over xGMI, cross-shard DFT kernel
-            (multilinear_amd/dist.py); the K steps stream through
-            dist.NttPipeline so the exchange of step i overlaps the local NTT
-            of step i+1 (every exchange and cross kernel completes inside the
-            timed region);
+  * N > 1 (default --mode sharded): one forward NTT of N * 2^24 points per
+            step, 2^24 per GPU: local NTT, one RCCL all-to-all over xGMI,
+            cross-shard DFT kernel (multilinear_amd/dist.py); the K steps
+            stream through dist.NttPipeline so the exchange of step i overlaps
+            the local NTT of step i+1 (every exchange and cross kernel
+            completes inside the timed region); weak scaling (2^24 per GPU);
+  * N > 1, --mode replicas: every rank transforms its own 2^24-point
+            polynomial per step (no data-path collective; reported as the
+            extra "replicas_ntt" in the default mode);
+  * strong scaling at every N (N = 1 included): "strong_ntt" = one 2^28-point
+            NTT (single GPU at N = 1, sharded over the N ranks otherwise) and
+            config 5 (RS + FRI prove of a 2^28 codeword), fixed total size;
   * value = 2^24 * N * steps / max-over-ranks(time of the K steps);
   * extras in the same JSON line: inverse NTT, FRI commit (config 3: 2^24
     coeffs -> RS LDE 2^25 -> Merkle root), full FRI prove, the 24-round
@@ -21,7 +23,12 @@ Metric: "NTT 2^24 field-elems/sec + FRI commit ms; % HBM roofline".
     N > 1 (strong scaling), each timed after the headline loop;
   * roofline: the dominant kernel (an ntt_pass) timed live with HIP events on
     its launch stream over the headline loop; algorithmic bytes per launch =
-    32 B x 2^24 (each element read once and written once);
+    that pass's share of the transform's 32 B x 2^24 (one read
+    and one write of every element for the WHOLE NTT, never the multi-pass
+    traffic), i.e. 32 B x 2^24 / passes; `bound` is the larger of that HBM
+    fraction and the pass's VALU issue fraction (SQ_INSTS_VALU of the newest
+    committed VALU pass x 64 lanes / live time, against one wave64 VALU
+    instruction per 4 cycles per SIMD at 2.4 GHz);
   * cpu_baseline: the oracle's C restatement of the reference NTT
     (oracle/liboracle.so, 1 thread) on one 2^24 NTT, rank 0 at N = 1 only.
 
@@ -43,14 +50,14 @@ sys.path.insert(0, ROOT)
 # host-staged exchanges (e.g. 2 ranks sharing one GPU).  Never used for a result.
 BACKEND = os.environ.get("MLH_BENCH_BACKEND", "nccl")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_PEAK = 7.864e13   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz full-rate lane-ops/s
-# practical issue rate of the butterfly instruction mix (fe_mul_pre + add + sub,
-# register resident, no memory): tools/bfly_peak.hip measured 5.3e11
-# butterflies/s x 301 VALU per 4 butterflies = 4.0e13 lane-instr/s; the SHA-256
-# mix peaks at the same rate (tools/sha_latency.hip: 1.65-1.75e10 node hashes/s x
-# 2272 VALU): these integer VOP3 ops issue one wave64 instruction per ~4 cycles
-# per SIMD, half the 2-cycle FP32 rate VALU_PEAK assumes
-VALU_PRACTICAL = 4.0e13
+# VALU issue ceiling of the integer VOP3 mix these kernels are made of
+# (v_mad_u64_u32, v_add/sub with carry, v_cndmask, v_alignbit, v_bitop3): one
+# wave64 instruction per 4 cycles per SIMD = 256 CU x 4 SIMD x 16 lanes x
+# 2.4 GHz.  Measured: the generated asm butterflies (tools/bfly2_bench.hip)
+# 6.45e11 butterflies/s x 60 VALU = 3.87e13 (98.5 %); SHA-256 node hashes
+# (tools/sha_latency.hip) 1.65-1.75e10/s x 2272 VALU = 3.75-4.0e13.
+VALU_PEAK = 256 * 4 * 16 * 2.4e9
+CHIP_MAX_GHZ = 2.4
 
 
 def _allreduce_max(x):
@@ -168,15 +175,20 @@ def load_valu_profile():
         d = json.load(open(paths[0]))
     except (OSError, ValueError):
         return None
-    out = {"source": os.path.basename(paths[0]), "kernels": {}}
+    out = {"source": os.path.basename(paths[0]),
+           "clock": "GRBM_GUI_ACTIVE / 8 XCDs / wall, capped at the chip's %.1f GHz; kernels "
+                    "under 50 us get the cap (the derivation breaks for short dispatches)"
+                    % CHIP_MAX_GHZ, "kernels": {}}
     for name, k in d.get("kernels", {}).items():
         for key, what in picks.items():
             if name.endswith("mlh::" + key) and k.get("eff_clock_ghz"):
-                ceiling = 256 * 4 * 64 / 4 * k["eff_clock_ghz"] * 1e9
+                clk = k["eff_clock_ghz"] if k["avg_ms"] >= 0.05 else CHIP_MAX_GHZ
+                clk = min(clk, CHIP_MAX_GHZ)
+                ceiling = 256 * 4 * 64 / 4 * clk * 1e9
                 out["kernels"][key] = {"what": what, "avg_ms": k["avg_ms"],
                                        "lane_instr_per_s": k["lane_instr_per_s"],
-                                       "clock_ghz": k["eff_clock_ghz"],
-                                       "issue_frac": k["lane_instr_per_s"] / ceiling}
+                                       "clock_ghz": clk,
+                                       "issue_frac": min(1.0, k["lane_instr_per_s"] / ceiling)}
     return out
 
 
@@ -208,9 +220,11 @@ def main():
     ap.add_argument("--extras-budget-s", type=float, default=240.0,
                     help="watchdog on the secondary timings (0: off)")
     ap.add_argument("--fri-log", type=int, default=28, help="config 5 codeword size (log2)")
-    ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas",
-                    help="N > 1 headline step: each GPU transforms its own 2^24 polynomial "
-                         "(replicas) or one N*2^24 transform is sharded with an all-to-all")
+    ap.add_argument("--mode", choices=["replicas", "sharded"], default="sharded",
+                    help="N > 1 headline step: one N*2^24 transform sharded with an all-to-all "
+                         "(default) or each GPU transforms its own 2^24 polynomial (replicas)")
+    ap.add_argument("--strong-log", type=int, default=28,
+                    help="strong-scaling NTT size (log2), fixed over N; 0: off")
     args = ap.parse_args()
 
     import torch
@@ -320,9 +334,15 @@ def main():
     dom = max(((k, v) for k, v in kernels.items() if k.startswith("ntt_pass")),
               key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
     dom_name, dom_stat = dom
-    alg_bytes = 32.0 * N  # one read + one write of every 16-B element per launch
+    # the NTT's algorithmic bytes are 2 x 16 x N for the whole
+    # transform; a pass is credited with its share (passes = NTT launches per step)
+    passes = max(1, round(sum(v["launches"] for k, v in kernels.items() if k.startswith("ntt_pass"))
+                          / dom_stat["launches"]))
+    alg_bytes = 32.0 * N / passes
     achieved_gbs = alg_bytes / (dom_stat["avg_ms"] * 1e-3) / 1e9
     traffic = load_pmc(dom_name, log_n)
+    valu = load_valu(dom_name) if log_n == 24 else None
+    valu_frac = (valu[0] * 64 / (dom_stat["avg_ms"] * 1e-3) / VALU_PEAK) if valu else None
 
     ms_per_step = elapsed / args.steps * 1e3
     value = N * args.steps * world / elapsed
@@ -352,7 +372,7 @@ def main():
         },
         "ntt_hbm_frac": (32.0 * N / (ms_per_step * 1e-3) / 1e9) / HBM_PEAK_GBS,
         "roofline": {
-            "bound": "hbm",
+            "bound": "valu" if (valu_frac or 0) > achieved_gbs / HBM_PEAK_GBS else "hbm",
             "kernel": dom_name,
             "achieved": achieved_gbs,
             "peak": HBM_PEAK_GBS,
@@ -361,16 +381,17 @@ def main():
             "traffic": traffic,
             "launch_avg_ms": dom_stat["avg_ms"],
             "alg_bytes_per_launch": alg_bytes,
+            "alg_bytes_rule": "32 B x 2^%d / %d passes (SURVEY.md 8(d))" % (log_n, passes),
+            "valu_frac": valu_frac,
         },
         "kernels": kernels,
     }
-    valu = load_valu(dom_name) if log_n == 24 else None
     if valu:
         rate = valu[0] * 64 / (dom_stat["avg_ms"] * 1e-3)
         result["valu_roofline"] = {
             "kernel": dom_name, "achieved": rate, "unit": "lane-instr/s",
-            "peak_practical": VALU_PRACTICAL, "frac_practical": rate / VALU_PRACTICAL,
-            "peak_nominal": VALU_PEAK, "frac_nominal": rate / VALU_PEAK,
+            "peak": VALU_PEAK, "frac": rate / VALU_PEAK,
+            "peak_rule": "one wave64 VALU instruction per 4 cycles per SIMD at 2.4 GHz",
             "source": "SQ_INSTS_VALU per launch (%s) x 64 lanes / live avg launch time" % valu[1],
         }
     vp = load_valu_profile() if log_n == 24 else None
@@ -523,6 +544,16 @@ def main():
                                                           log_p, lib, ctx)
             except Exception as e:
                 result["sharded_ntt_error"] = "%s: %s" % (type(e).__name__, e)
+        if world > 1 and sharded:
+            try:
+                result["replicas_ntt"] = replicas_ntt_extra(args, ntt_local, world, barrier, log_n)
+            except Exception as e:
+                result["replicas_ntt_error"] = "%s: %s" % (type(e).__name__, e)
+    if not args.no_extras and args.strong_log:
+        try:
+            result["strong_ntt"] = strong_ntt(args, lib, ctx, local, world, rank, barrier)
+        except Exception as e:
+            result["strong_ntt_error"] = "%s: %s" % (type(e).__name__, e)
         if world > 1:
             try:
                 result.update(config4_sharded(args, local, world, rank, barrier))
@@ -612,6 +643,66 @@ def sharded_ntt_extra(args, pipe, x, world, barrier, log_n, log_p, lib, ctx):
             "scaling": "weak (2^%d per GPU)" % log_n,
             "shard_dft_avg_ms": (t.value / c.value) if c.value else None,
             "layout": "cyclic shards in, block-cyclic (2^%d) out" % (log_n - log_p)}
+
+
+def replicas_ntt_extra(args, ntt_local, world, barrier, log_n):
+    """Every GPU transforms its own 2^24-point polynomial (independent objects,
+    no collective): the weak-scaling ceiling the sharded headline compares to."""
+    import torch
+
+    for _ in range(max(1, args.warmup)):
+        ntt_local()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ntt_local()
+    torch.cuda.synchronize()
+    dt = _allreduce_max(time.perf_counter() - t0)
+    return {"value": (1 << log_n) * world * args.steps / dt, "unit": "field-elems/s",
+            "ms_per_step": dt / args.steps * 1e3, "scaling": "weak (independent 2^%d per GPU)" % log_n}
+
+
+def strong_ntt(args, lib, ctx, local, world, rank, barrier):
+    """Fixed-size strong scaling: one 2^L-point forward NTT (L = --strong-log,
+    28 by default), on one GPU at N = 1 and sharded over the N ranks (cyclic
+    shards in, one all-to-all) otherwise.  hbm_frac: 32 B x 2^L algorithmic
+    bytes over the time, against N x 8 TB/s."""
+    import torch
+
+    from multilinear_amd import device as D
+
+    L = args.strong_log
+    g = int.from_bytes(bytes(_gen(lib, L)), "little")
+    reps = max(1, min(args.extra_reps, 5))
+    if world == 1:
+        xs = D.random_device(1 << L, 4242, local)
+        ys = D.empty(1 << L, local)
+        gb = D.fe_bytes(g)
+
+        def run():
+            D.check(lib.mlh_ntt(ctx, D.ptr(xs), D.ptr(ys), L, gb), ctx)
+    else:
+        from multilinear_amd import dist as DS
+
+        tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
+        log_p = world.bit_length() - 1
+        xs = D.random_device(1 << (L - log_p), 4242 + rank, local)
+
+        def run():
+            return DS.ntt(xs, L, g, tp, ops)
+
+    run()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    dt = _allreduce_max(time.perf_counter() - t0) / reps if world > 1 else \
+        (time.perf_counter() - t0) / reps
+    return {"log_n": L, "ms": dt * 1e3, "value": (1 << L) / dt, "unit": "field-elems/s",
+            "scaling": "strong (2^%d total, %s)" % (L, "single GPU" if world == 1 else
+                                                   "2^%d per GPU" % (L - world.bit_length() + 1)),
+            "hbm_frac": 32.0 * (1 << L) / dt / (world * HBM_PEAK_GBS * 1e9)}
 
 
 def config4_sharded(args, local, world, rank, barrier):

@@ -266,3 +266,52 @@ def test_ntt_pipeline_matches_sharded_ntt():
     for r in range(world):
         assert "error" not in res[r], res[r].get("error")
         assert res[r]["ok"]
+
+
+def _rccl_worker(port, q):
+    """World-1 RCCL communicator: the device-to-device collectives the sharded
+    path issues at N > 1 (Transport(host_staged=False)), on HBM tensors."""
+    import torch.distributed as tdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(0)
+    tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert tdist.get_backend() == "nccl"
+        tp = D.Transport(host_staged=False)
+        x = DV.random_device(1 << 24, 99)  # 256 MiB: the per-GPU shard the bench exchanges
+        y = tp.all_to_all(x)
+        g = tp.all_gather(x[: 1 << 12])
+        nb = tp.gather_bytes(b"\x01\x02roots")
+        torch.cuda.synchronize()
+        res = {"a2a_same": bool(torch.equal(x, y)), "a2a_dev": y.device.type,
+               "ag_same": bool(torch.equal(g, x[: 1 << 12])), "ag_dev": g.device.type,
+               "bytes": nb}
+        q.put(res)
+    except Exception:
+        import traceback
+
+        q.put({"error": traceback.format_exc()})
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_rccl_world1_device_collectives():
+    """The nccl (= RCCL) backend runs here before the driver's 8-GPU node: an
+    all_to_all_single of a 256 MiB shard, all_gather_into_tensor and the byte
+    gather, all on device tensors, through the same Transport the sharded NTT /
+    FRI / sumcheck use."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        res = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+    assert "error" not in res, res.get("error")
+    assert res["a2a_same"] and res["a2a_dev"] == "cuda"
+    assert res["ag_same"] and res["ag_dev"] == "cuda"
+    assert res["bytes"] == [b"\x01\x02roots"]
