@@ -18,7 +18,7 @@ def _gen():
     return m
 
 
-@pytest.mark.parametrize("kinds", [("m", "m"), ("m",), ("t", "t"), ("t",), ("m", "t")])
+@pytest.mark.parametrize("kinds", [("m", "m"), ("m",), ("t", "t"), ("t",), ("m", "t"), ("p", "p"), ("p",)])
 def test_variant_emulates_exactly(kinds):
     G = _gen()
     for bsrc in ("s", "v"):

@@ -80,55 +80,71 @@ class Ins:
         return [self.sdst] if self.sdst and self.sdst != "junk" else []
 
 
-def bfly_prog(b, mul):
-    """Instruction list of butterfly b.  Operand names:
-    u{b}_{i} (in, tied to a), v{b}_{i} (in, tied to d), B{b}_{k}{j} (twiddle
-    limbs), kc1 (VGPR 0x2CFF), k2d00 (SGPR 0x2D00).  Flags K{b}, C2{b}, B2{b}."""
+def product_prog(E, p, V, B, safe, kflag):
+    """t = sum_k V_k * B_k (relaxed), appended through E.  safe: count the carry
+    of every column's first mad too (any twiddle); otherwise columns 1..3 rely
+    on the stage-twiddle precondition (module docstring).  Returns the four
+    limb names of t; the wrap flag goes to SGPR kflag."""
+    r = []
+    acc = 0
+    for j in range(4):
+        cys = []
+        for k in range(4):
+            dst = ("pair", p + "P%d_%d.lo" % (j, k), p + "P%d_%d.hi" % (j, k))
+            if k == 0 and (j == 0 or not safe):
+                E("mad", dst, [V[k], B[k][j], acc], sdst="junk")
+            else:
+                cy = p + "cy%d%d" % (j, k)
+                cys.append(cy)
+                E("mad", dst, [V[k], B[k][j], acc], sdst=cy)
+            acc = dst
+        r.append(acc[1])
+        # carry count -> hi half of the next column's addend pair
+        nlo, nhi = p + "Q%d.lo" % (j + 1), p + "Q%d.hi" % (j + 1)
+        c = 0
+        for n, cy in enumerate(cys):
+            d = nhi if n == len(cys) - 1 else p + "c%d_%d" % (j, n)
+            E("addc", d, [c, 0], sdst="junk", cin=cy)
+            c = d
+        if j < 3:
+            E("mov", nlo, [acc[2]])
+            acc = ("pair", nlo, nhi)
+        else:
+            t_lo, t_hi = acc[2], nhi
+    # fold T*2^128 = T*C = T*0x2D00*2^32 - T
+    Y = ("pair", p + "Y.lo", p + "Y.hi")
+    E("mad", Y, [t_lo, "k2d00", 0], sdst="junk")
+    E("mad24", p + "Yh2", [t_hi, "k2d00", Y[2]])
+    E("sub", p + "x0", [0, t_lo], sdst=p + "bb0")
+    E("subb", p + "x1", [Y[1], t_hi], sdst=p + "bb1", cin=p + "bb0")
+    E("subb", p + "x2", [p + "Yh2", 0], sdst="junk", cin=p + "bb1")
+    return r, p
+
+
+def bfly_prog(b, kind):
+    """Instruction list of butterfly b.  kind 'm': with a stage twiddle, 't':
+    trivial (w = 1), 'p': product only v <- w v (safe first mads; any twiddle).
+    Operand names: u{b}_{i} (in, tied to a), v{b}_{i} (in, tied to d),
+    B{b}_{k}{j} (twiddle limbs), kc1 (VGPR 0x2CFF), k2d00 (SGPR 0x2D00).
+    Flags K{b}, C2{b}, B2{b}."""
     p = "b%d." % b
     U = ["u%d_%d" % (b, i) for i in range(4)]
     V = ["v%d_%d" % (b, i) for i in range(4)]
     prog = []
     E = lambda *a, **k: prog.append(Ins(*a, tag=b, **k))
-    if mul:
+    if kind in ("m", "p"):
         B = [["B%d_%d%d" % (b, k, j) for j in range(4)] for k in range(4)]
-        r = []
-        acc = 0
-        for j in range(4):
-            cys = []
-            for k in range(4):
-                dst = ("pair", p + "P%d_%d.lo" % (j, k), p + "P%d_%d.hi" % (j, k))
-                if k == 0:
-                    E("mad", dst, [V[k], B[k][j], acc], sdst="junk")
-                else:
-                    cy = p + "cy%d%d" % (j, k)
-                    cys.append(cy)
-                    E("mad", dst, [V[k], B[k][j], acc], sdst=cy)
-                acc = dst
-            r.append(acc[1])
-            # carry count -> hi half of the next column's addend pair
-            nlo, nhi = p + "Q%d.lo" % (j + 1), p + "Q%d.hi" % (j + 1)
-            c = 0
-            for n, cy in enumerate(cys):
-                d = nhi if n == len(cys) - 1 else p + "c%d_%d" % (j, n)
-                E("addc", d, [c, 0], sdst="junk", cin=cy)
-                c = d
-            if j < 3:
-                E("mov", nlo, [acc[2]])
-                acc = ("pair", nlo, nhi)
-            else:
-                t_lo, t_hi = acc[2], nhi
-        # fold T*2^128 = T*C = T*0x2D00*2^32 - T
-        Y = ("pair", p + "Y.lo", p + "Y.hi")
-        E("mad", Y, [t_lo, "k2d00", 0], sdst="junk")
-        E("mad24", p + "Yh2", [t_hi, "k2d00", Y[2]])
-        E("sub", p + "x0", [0, t_lo], sdst=p + "bb0")
-        E("subb", p + "x1", [Y[1], t_hi], sdst=p + "bb1", cin=p + "bb0")
-        E("subb", p + "x2", [p + "Yh2", 0], sdst="junk", cin=p + "bb1")
-        S = [p + "s%d" % i for i in range(4)]
+        r, _ = product_prog(E, p, V, B, kind == "p", "K%d" % b)
+        if kind == "p":  # s = r + X written straight into v (tied output d)
+            S = ["d%d_%d" % (b, i) for i in range(4)]
+        else:
+            S = [p + "s%d" % i for i in range(4)]
         E("add", S[0], [r[0], p + "x0"], sdst=p + "e0")
         E("addc", S[1], [r[1], p + "x1"], sdst=p + "e1", cin=p + "e0")
         E("addc", S[2], [r[2], p + "x2"], sdst=p + "e2", cin=p + "e1")
         E("addc", S[3], [r[3], 0], sdst="K%d" % b, cin=p + "e2")
+        if kind == "p":
+            return prog
     else:
         S = V
     A = [p + "A%d" % i for i in range(4)]
@@ -304,7 +320,7 @@ def emit(kinds, bsrc):
     """kinds: tuple of 'm' (with twiddle) / 't' (trivial, w = 1) per butterfly.
     bsrc: 's' (twiddle limbs in SGPRs) or 'v'.  Returns (asm lines, operand
     description, nvgpr, nsgpr-pairs)."""
-    progs = [bfly_prog(b, k == "m") for b, k in enumerate(kinds)]
+    progs = [bfly_prog(b, k) for b, k in enumerate(kinds)]
     ins, order = schedule(progs)
     seq, assign, nv, ns = allocate(ins, order)
     # trailing pad: the C++ code may read the flag SGPRs with a VALU right away
@@ -318,17 +334,21 @@ def emit(kinds, bsrc):
 def operand_names(kinds):
     outs, ins = [], []
     for b, k in enumerate(kinds):
-        outs += ["u%d_%d" % (b, i) for i in range(4)] + ["v%d_%d" % (b, i) for i in range(4)]
+        if k != "p":
+            outs += ["u%d_%d" % (b, i) for i in range(4)]
+        outs += ["v%d_%d" % (b, i) for i in range(4)]
     flags = []
     for b, k in enumerate(kinds):
-        if k == "m":
+        if k in ("m", "p"):
             flags.append("K%d" % b)
-        flags += ["C2%d" % b, "B2%d" % b]
+        if k != "p":
+            flags += ["C2%d" % b, "B2%d" % b]
     for b, k in enumerate(kinds):
-        if k == "m":
+        if k in ("m", "p"):
             ins += ["B%d_%d%d" % (b, kk, j) for kk in range(4) for j in range(4)]
-    ins += ["kc1"]
-    if "m" in kinds:
+    if any(k != "p" for k in kinds):
+        ins += ["kc1"]
+    if "m" in kinds or "p" in kinds:
         ins += ["k2d00"]
     return outs, flags, ins
 
@@ -502,21 +522,26 @@ def run_case(kinds, lines, opn, nv, uvals, vvals, wvals):
     env = {}
     for b in range(len(kinds)):
         for i in range(4):
-            env["%%%d" % opn["u%d_%d" % (b, i)]] = limbs(uvals[b])[i]
+            if kinds[b] != "p":
+                env["%%%d" % opn["u%d_%d" % (b, i)]] = limbs(uvals[b])[i]
             env["%%%d" % opn["v%d_%d" % (b, i)]] = limbs(vvals[b])[i]
-        if kinds[b] == "m":
+        if kinds[b] in ("m", "p"):
             Bs = [wvals[b] * (1 << (32 * k)) % M for k in range(4)]
             for k in range(4):
                 for j in range(4):
                     env["%%%d" % opn["B%d_%d%d" % (b, k, j)]] = limbs(Bs[k])[j]
-    env["%%%d" % opn["kc1"]] = KC1
+    if "kc1" in opn:
+        env["%%%d" % opn["kc1"]] = KC1
     if "k2d00" in opn:
         env["%%%d" % opn["k2d00"]] = K2D00
     regs = emulate(lines, env)
     res = []
     for b in range(len(kinds)):
-        a = value([regs["%%%d" % opn["u%d_%d" % (b, i)]] for i in range(4)])
         d = value([regs["%%%d" % opn["v%d_%d" % (b, i)]] for i in range(4)])
+        if kinds[b] == "p":  # v <- w v; flag K: true value s + C
+            res.append((None, add_c(d) if regs["%%%d" % opn["K%d" % b]] else d))
+            continue
+        a = value([regs["%%%d" % opn["u%d_%d" % (b, i)]] for i in range(4)])
         fk = regs.get("%%%d" % opn["K%d" % b], 0) if kinds[b] == "m" else 0
         fc = regs["%%%d" % opn["C2%d" % b]]
         fb = regs["%%%d" % opn["B2%d" % b]]
@@ -566,11 +591,18 @@ def selftest(kinds, lines, opn, nv, trials=3000, seed=1):
         pick = lambda: rng.choice(edge) if rng.random() < 0.3 else rng.randrange(1 << 128)
         uv = [pick() for _ in range(nb)]
         vv = [pick() for _ in range(nb)]
-        wv = [rng.choice(roots) for _ in range(nb)]
+        # products ('p') take any canonical twiddle, limbs of 0xFFFFFFFF included
+        wv = [rng.choice(roots) if k != "p" else
+              (rng.choice([M - 1, M - 2, (1 << 127) | 0xFFFFFFFF_FFFFFFFF_FFFFFFFF, 1, 2])
+               if rng.random() < 0.3 else rng.randrange(M)) for k in kinds]
         got = run_case(kinds, lines, opn, nv, uv, vv, wv)
         for b in range(nb):
-            w = wv[b] if kinds[b] == "m" else 1
+            w = wv[b] if kinds[b] in ("m", "p") else 1
             a, d = got[b]
+            if kinds[b] == "p":
+                assert 0 <= d < (1 << 128) and d % M == (w * vv[b]) % M, (kinds, b, vv[b], w)
+                checked += 1
+                continue
             assert 0 <= a < (1 << 128) and 0 <= d < (1 << 128)
             assert a % M == (uv[b] + w * vv[b]) % M, (kinds, b, uv[b], vv[b], w)
             assert d % M == (uv[b] - w * vv[b]) % M, (kinds, b, uv[b], vv[b], w)
@@ -592,7 +624,7 @@ def twiddle_precondition():
 
 # ------------------------------------------------------------ C++ header ---
 
-VARIANTS = [("m", "m"), ("m",), ("t", "t"), ("t",), ("m", "t")]
+VARIANTS = [("m", "m"), ("m",), ("t", "t"), ("t",), ("m", "t"), ("p", "p"), ("p",)]
 
 
 def cxx_function(kinds, bsrc):
@@ -601,8 +633,8 @@ def cxx_function(kinds, bsrc):
     nb = len(kinds)
     args = []
     for b in range(nb):
-        args += ["fe& u%d" % b, "fe& v%d" % b]
-        if kinds[b] == "m":
+        args += (["fe& u%d" % b] if kinds[b] != "p" else []) + ["fe& v%d" % b]
+        if kinds[b] in ("m", "p"):
             args += ["const fe& B%d_%d" % (b, k) for k in range(4)]
     args += ["uint64_t& rare"]
     body = []
@@ -611,8 +643,9 @@ def cxx_function(kinds, bsrc):
     if ns:
         body.append("  uint64_t st[%d];" % ns)
     body.append("  uint64_t junk;")
-    body.append("  const uint32_t kc1 = 0x2CFFu;")
-    if "m" in kinds:
+    if "kc1" in ins:
+        body.append("  const uint32_t kc1 = 0x2CFFu;")
+    if "k2d00" in ins:
         body.append("  const uint32_t k2d00 = 0x2D00u;")
     asm = "\\n\\t".join(lines)
     ol = []
@@ -639,6 +672,9 @@ def cxx_function(kinds, bsrc):
     body.append("  rare = %s;" % " | ".join(flags))
     body.append("  if (__builtin_expect(rare != 0, 0)) {")
     for b in range(nb):
+        if kinds[b] == "p":
+            body.append("    if ((K%d >> __lane_id()) & 1u) v%d = relaxed_add_c(v%d);" % (b, b, b))
+            continue
         fk = "K%d" % b if kinds[b] == "m" else "0ull"
         body.append("    bfly_fix(u%d, v%d, %s, C2%d, B2%d);" % (b, b, fk, b, b))
     body.append("  }")
@@ -713,7 +749,7 @@ def main():
     total = 0
     for kinds in VARIANTS:
         for bsrc in ("s", "v"):
-            if "m" not in kinds and bsrc == "s":
+            if "m" not in kinds and "p" not in kinds and bsrc == "s":
                 continue
             fname, code, lines = cxx_function(kinds, bsrc)
             _, _, _, _, _, nv, opn = render(kinds, bsrc)
