@@ -55,6 +55,17 @@ typedef struct mlh_fri_prover mlh_fri_prover; /* fri/mod.rs FriProverData       
 const char* mlh_version(void);
 mlh_status mlh_context_create(int device, void* hip_stream, mlh_ctx** out);
 void mlh_context_destroy(mlh_ctx* ctx);
+/* Twiddle / fold tables are cached per context (built on the first use of a
+ * size and generator) in a bounded LRU cache: default limit 1 GiB; tables the
+ * running operation uses are never evicted, so the cache may exceed a very
+ * small limit by that operation's tables.  limit 0 frees every table not in
+ * use at the next opportunity. */
+mlh_status mlh_set_table_cache_limit(mlh_ctx* ctx, uint64_t bytes);
+uint64_t mlh_table_cache_bytes(const mlh_ctx* ctx);
+/* Test/tuning hook: force the NTT radix plan of this context (count digits
+ * 4..9; a plan applies to the transforms whose log size equals its digit sum;
+ * count = 0 restores the default plan). */
+mlh_status mlh_set_ntt_plan(mlh_ctx* ctx, const uint32_t* logr, uint32_t count);
 mlh_status mlh_set_stream(mlh_ctx* ctx, void* hip_stream);
 mlh_status mlh_synchronize(mlh_ctx* ctx);
 const char* mlh_last_error(const mlh_ctx* ctx);

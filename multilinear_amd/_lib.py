@@ -83,6 +83,9 @@ SIGNATURES = {
     "mlh_context_create": (_I, [_I, _P, ctypes.POINTER(_P)]),
     "mlh_context_destroy": (None, [_P]),
     "mlh_set_stream": (_I, [_P, _P]),
+    "mlh_set_ntt_plan": (_I, [_P, ctypes.POINTER(ctypes.c_uint32), _U32]),
+    "mlh_set_table_cache_limit": (_I, [_P, ctypes.c_uint64]),
+    "mlh_table_cache_bytes": (ctypes.c_uint64, [_P]),
     "mlh_synchronize": (_I, [_P]),
     "mlh_last_error": (ctypes.c_char_p, [_P]),
     "mlh_malloc": (_I, [_P, _S, ctypes.POINTER(_P)]),

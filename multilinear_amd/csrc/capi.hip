@@ -54,11 +54,22 @@ struct TableKey {
   }
 };
 
+// A cached twiddle table: device buffer, size, LRU stamp.
+struct CachedTable {
+  fe* d = nullptr;
+  size_t bytes = 0;
+  uint64_t stamp = 0;
+};
+
 struct mlh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  std::map<TableKey, fe*> tables;
+  // twiddle / fold tables, bounded LRU (mlh_set_table_cache_limit)
+  std::map<TableKey, CachedTable> tables;
+  size_t table_bytes = 0;
+  size_t table_limit = (size_t)1 << 30;
+  uint64_t table_stamp = 0;
   std::multimap<size_t, void*> pool;  // cached free device blocks
   std::map<void*, size_t> live;       // pool-owned live blocks
   fe* partials = nullptr;             // 2 * kMaxRedBlocks
@@ -68,6 +79,11 @@ struct mlh_ctx {
   size_t qstage_bytes = 0;
   fe* ntt_scratch = nullptr;          // NTT ping-pong buffer (grow-only)
   size_t ntt_scratch_bytes = 0;
+  // debug / test hooks, fixed at creation (MLH_DEBUG_SYNC) or set through the
+  // API (mlh_set_ntt_plan): never read from the environment on a hot path
+  bool debug_sync = false;
+  uint32_t forced_plan[kMaxPasses] = {0};
+  uint32_t forced_plan_len = 0;
   // kernel timer (mlh_profile_*): HIP events on the launch stream
   bool prof_on = false;
   std::vector<hipEvent_t> ev_free;
@@ -205,20 +221,64 @@ struct PoolBuf {
   }
 };
 
+// Table cache bound: when a new table would take the cache past its limit,
+// least-recently-used tables are freed (after the stream drains, since queued
+// kernels may still read them).  The tables one operation fetches are stamped
+// consecutively and fewer than kTablePin (an NTT of 2^40: 5 stage + 4 + 4
+// inter-pass tables; a PCS prove: those + 2 fold tables), so the newest
+// kTablePin stamps -- every table the running operation holds a pointer to --
+// are never evicted.
+constexpr uint64_t kTablePin = 24;
+
+static mlh_status table_make_room(mlh_ctx* ctx, size_t need) {
+  if (ctx->table_bytes + need <= ctx->table_limit) return MLH_OK;
+  std::vector<std::pair<uint64_t, TableKey>> order;
+  for (auto& kv : ctx->tables)
+    if (kv.second.stamp + kTablePin <= ctx->table_stamp) order.push_back({kv.second.stamp, kv.first});
+  std::sort(order.begin(), order.end(),
+            [](const std::pair<uint64_t, TableKey>& a, const std::pair<uint64_t, TableKey>& b) {
+              return a.first < b.first;
+            });
+  bool synced = false;
+  for (auto& o : order) {
+    if (ctx->table_bytes + need <= ctx->table_limit) break;
+    if (!synced) {
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+      synced = true;
+    }
+    auto it = ctx->tables.find(o.second);
+    HIP_TRY(ctx, hipFree(it->second.d));
+    ctx->table_bytes -= it->second.bytes;
+    ctx->tables.erase(it);
+  }
+  return MLH_OK;
+}
+
+static bool table_hit(mlh_ctx* ctx, const TableKey& k, const fe** out) {
+  auto it = ctx->tables.find(k);
+  if (it == ctx->tables.end()) return false;
+  it->second.stamp = ++ctx->table_stamp;
+  *out = it->second.d;
+  return true;
+}
+
+static mlh_status table_alloc(mlh_ctx* ctx, const TableKey& k, size_t bytes, fe** d) {
+  MLH_TRY(table_make_room(ctx, bytes));
+  HIP_TRY(ctx, hipMalloc(d, bytes));
+  ctx->tables[k] = CachedTable{*d, bytes, ++ctx->table_stamp};
+  ctx->table_bytes += bytes;
+  return MLH_OK;
+}
+
 // table[t] = base^t * scale, t < count, cached per context.  expand: 4 fe per
 // entry (t * 2^(32k), k < 4) for fe_mul_pre.
 static mlh_status get_table(mlh_ctx* ctx, u128 base, uint64_t count, u128 scale, const fe** out,
                             bool expand = false) {
   TableKey k{base, count, scale, expand ? 1 : 0};
-  auto it = ctx->tables.find(k);
-  if (it != ctx->tables.end()) {
-    *out = it->second;
-    return MLH_OK;
-  }
+  if (table_hit(ctx, k, out)) return MLH_OK;
   fe* d = nullptr;
-  HIP_TRY(ctx, hipMalloc(&d, count * sizeof(fe) * (expand ? 4 : 1)));
+  MLH_TRY(table_alloc(ctx, k, count * sizeof(fe) * (expand ? 4 : 1), &d));
   HIP_TRY(ctx, launch_pow_table(d, to_fe(base), to_fe(scale), count, ctx->stream, expand));
-  ctx->tables[k] = d;
   *out = d;
   return MLH_OK;
 }
@@ -227,16 +287,11 @@ static mlh_status get_table(mlh_ctx* ctx, u128 base, uint64_t count, u128 scale,
 static mlh_status get_table2d(mlh_ctx* ctx, u128 base, uint64_t rows, uint64_t cols,
                               uint64_t mult, u128 scale, const fe** out, bool expand = false) {
   TableKey k{base, rows, scale, expand ? 1 : 0, cols, mult};
-  auto it = ctx->tables.find(k);
-  if (it != ctx->tables.end()) {
-    *out = it->second;
-    return MLH_OK;
-  }
+  if (table_hit(ctx, k, out)) return MLH_OK;
   fe* d = nullptr;
-  HIP_TRY(ctx, hipMalloc(&d, rows * cols * sizeof(fe) * (expand ? 4 : 1)));
+  MLH_TRY(table_alloc(ctx, k, rows * cols * sizeof(fe) * (expand ? 4 : 1), &d));
   HIP_TRY(ctx, launch_pow_table2d(d, to_fe(base), to_fe(scale), rows, cols, mult, ctx->stream,
                                   expand));
-  ctx->tables[k] = d;
   *out = d;
   return MLH_OK;
 }
@@ -258,7 +313,8 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
     MLH_TRY(get_table(ctx, w, N / 2 ? N / 2 : 1, 1, &tb->tw_small));
     return MLH_OK;
   }
-  ntt_plan_radices(log_n, &tb->nradix, tb->logr);
+  tb->debug_sync = ctx->debug_sync;
+  ntt_plan_radices(log_n, &tb->nradix, tb->logr, ctx->forced_plan, ctx->forced_plan_len);
   for (uint32_t p = 0; p < tb->nradix; ++p) {
     const uint64_t R = 1ull << tb->logr[p];
     MLH_TRY(get_table(ctx, h_pow(w, N / R), R / 2, 1, &tb->tw[p], true));
@@ -271,12 +327,10 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
         tb->logr[p] + logw <= kFullTwLog ? logw : (logw < kTwLogA ? logw : kTwLogA);
     const u128 ws = h_pow(w, S);
     tb->loga[p] = loga;
-    MLH_TRY(get_table2d(ctx, ws, R, 1ull << loga, 1, p == 0 ? scale : (u128)1, &tb->ta[p],
-                        MLH_XTW));
+    MLH_TRY(get_table2d(ctx, ws, R, 1ull << loga, 1, p == 0 ? scale : (u128)1, &tb->ta[p]));
     tb->tb[p] = nullptr;
     if (logw > loga)
-      MLH_TRY(get_table2d(ctx, ws, R, 1ull << (logw - loga), 1ull << loga, 1, &tb->tb[p],
-                          MLH_XTW == 1));
+      MLH_TRY(get_table2d(ctx, ws, R, 1ull << (logw - loga), 1ull << loga, 1, &tb->tb[p]));
     S <<= tb->logr[p];
   }
   return MLH_OK;
@@ -348,6 +402,8 @@ mlh_status mlh_context_create(int device, void* hip_stream, mlh_ctx** out) {
   std::unique_ptr<mlh_ctx> c(new mlh_ctx());
   c->device = device;
   c->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  const char* dbg = getenv("MLH_DEBUG_SYNC");
+  c->debug_sync = dbg && *dbg && strcmp(dbg, "0") != 0;
   if (hipMalloc(&c->partials, 2 * kMaxRedBlocks * sizeof(fe)) != hipSuccess) return MLH_ERR_OOM;
   if (hipMalloc(&c->small, 64 * sizeof(fe)) != hipSuccess) return MLH_ERR_OOM;
   if (hipHostMalloc(&c->pinned, 4096, 0) != hipSuccess) return MLH_ERR_OOM;
@@ -361,7 +417,7 @@ void mlh_context_destroy(mlh_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   resolve_profile(ctx);
   for (auto e : ctx->ev_free) (void)hipEventDestroy(e);
-  for (auto& kv : ctx->tables) (void)hipFree(kv.second);
+  for (auto& kv : ctx->tables) (void)hipFree(kv.second.d);
   for (auto& kv : ctx->pool) (void)hipFree(kv.second);
   for (auto& kv : ctx->live) (void)hipFree(kv.first);
   (void)hipFree(ctx->ntt_scratch);
@@ -370,6 +426,24 @@ void mlh_context_destroy(mlh_ctx* ctx) {
   (void)hipHostFree(ctx->pinned);
   if (ctx->qstage) (void)hipHostFree(ctx->qstage);
   delete ctx;
+}
+
+mlh_status mlh_set_table_cache_limit(mlh_ctx* ctx, uint64_t bytes) {
+  if (!ctx) return MLH_ERR_INVALID;
+  ctx->table_limit = (size_t)bytes;
+  return table_make_room(ctx, 0);
+}
+
+uint64_t mlh_table_cache_bytes(const mlh_ctx* ctx) { return ctx ? ctx->table_bytes : 0; }
+
+mlh_status mlh_set_ntt_plan(mlh_ctx* ctx, const uint32_t* logr, uint32_t count) {
+  if (!ctx || (count && !logr) || count > (uint32_t)kMaxPasses)
+    return fail(ctx, MLH_ERR_INVALID, "plan: at most kMaxPasses digits");
+  for (uint32_t i = 0; i < count; ++i)
+    if (logr[i] < 4 || logr[i] > 9) return fail(ctx, MLH_ERR_INVALID, "plan digits must be 4..9");
+  ctx->forced_plan_len = count;
+  for (uint32_t i = 0; i < count; ++i) ctx->forced_plan[i] = logr[i];
+  return MLH_OK;
 }
 
 mlh_status mlh_set_stream(mlh_ctx* ctx, void* hip_stream) {

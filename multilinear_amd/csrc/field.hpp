@@ -237,8 +237,12 @@ __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
 // a * w for a twiddle w supplied as its limb-shifted multiples
 // B_k = w * 2^(32k) mod M (k = 0..3, canonical; "expanded" tables):
 //   a * w = sum_k a_k * B_k   (< 2^162: four 32x128 rows summed column-wise)
-// then one fold of the top T < 2^34: T * 2^128 = T * 0x2D00 * 2^32 - T.
-// 17 v_mad_u64_u32 instead of 16 + 8 for the 256-bit product + two folds.
+// then one fold of the top T < 2^35: T * 2^128 = T * 0x2D00 * 2^32 - T.
+// Every MAC after a column's first product counts its carry; the first MAC
+// of columns 1..3 adds to {hi(prev), carries} < 2^35, which can exceed 2^64
+// together with a product of two limbs >= 2^32 - 8, so it counts too.  (The
+// NTT's hot path uses the generated asm of bfly_asm.hpp instead; this is the
+// C reference it was checked against, tools/bfly2_bench.hip.)
 __device__ __forceinline__ fe fe_mul_pre_r(const fe& a, const fe& B0, const fe& B1, const fe& B2,
                                            const fe& B3) {
   uint64_t acc;
@@ -249,29 +253,29 @@ __device__ __forceinline__ fe fe_mul_pre_r(const fe& a, const fe& B0, const fe& 
   mac_carry(acc, a.w[2], B2.w[0], c2);
   mac_carry(acc, a.w[3], B3.w[0], c2);
   r0 = (uint32_t)acc;
-  acc = (acc >> 32) | ((uint64_t)c2 << 32);  // < 2^34: the next first MAC cannot overflow
-  acc = (uint64_t)a.w[0] * B0.w[1] + acc;
+  acc = (acc >> 32) | ((uint64_t)c2 << 32);
   c2 = 0;
+  mac_carry(acc, a.w[0], B0.w[1], c2);
   mac_carry(acc, a.w[1], B1.w[1], c2);
   mac_carry(acc, a.w[2], B2.w[1], c2);
   mac_carry(acc, a.w[3], B3.w[1], c2);
   r1 = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)c2 << 32);
-  acc = (uint64_t)a.w[0] * B0.w[2] + acc;
   c2 = 0;
+  mac_carry(acc, a.w[0], B0.w[2], c2);
   mac_carry(acc, a.w[1], B1.w[2], c2);
   mac_carry(acc, a.w[2], B2.w[2], c2);
   mac_carry(acc, a.w[3], B3.w[2], c2);
   r2 = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)c2 << 32);
-  acc = (uint64_t)a.w[0] * B0.w[3] + acc;
   c2 = 0;
+  mac_carry(acc, a.w[0], B0.w[3], c2);
   mac_carry(acc, a.w[1], B1.w[3], c2);
   mac_carry(acc, a.w[2], B2.w[3], c2);
   mac_carry(acc, a.w[3], B3.w[3], c2);
   r3 = (uint32_t)acc;
-  const uint32_t t_lo = (uint32_t)(acc >> 32), t_hi = c2;  // T = t_lo + t_hi 2^32 < 2^34
-  // X = T*C = T*0x2D00*2^32 - T (>= 0, < 2^80: three limbs), value = r + X < 2^128 + 2^80
+  const uint32_t t_lo = (uint32_t)(acc >> 32), t_hi = c2;  // T = t_lo + t_hi 2^32 < 2^35
+  // X = T*C = T*0x2D00*2^32 - T (>= 0, < 2^81: three limbs), value = r + X < 2^128 + 2^81
   const uint64_t v = (uint64_t)t_lo * kCmul;
   const uint32_t vh = (uint32_t)(v >> 32) + __umul24(t_hi, kCmul);
   uint32_t b, k;

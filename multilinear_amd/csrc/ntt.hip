@@ -90,9 +90,6 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 #ifndef MLH_LDS_TB
 #define MLH_LDS_TB 1  // two-table passes: the tile's TB column staged through LDS
 #endif
-#if MLH_LDS_TB && MLH_XTW
-#error "MLH_LDS_TB assumes plain (non-expanded) inter-pass tables"
-#endif
 constexpr int pass_waves_per_simd(int logr, int ept) {
   return ept == 16 ? 2 : (logr == 8 ? MLH_WPS8 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2)));
 }
@@ -348,20 +345,11 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
       // w_S^(jrest k) = TA[k][jl] * TB[k][jh]: the 8 columns of a tile are
       // 8 consecutive jl, so a wave's lanes read 8 runs of 128 B per table
       const uint64_t jl = jrest & ((1ull << g.loga) - 1);
-#if MLH_XTW
-      v = fe_mul_pre(v, ta + 4 * ((k << g.loga) + jl));
-#if MLH_XTW == 1
-      if (TW == 0) v = fe_mul_pre(v, tb + 4 * (k * (g.stride >> g.loga) + (jrest >> g.loga)));
-#else
-      if (TW == 0) v = fe_mul(v, tb[k * (g.stride >> g.loga) + (jrest >> g.loga)]);
-#endif
-#else
       v = fe_mul(v, ta[(k << g.loga) + jl]);
 #if MLH_LDS_TB
       if (TW == 0) v = fe_mul(v, lds[k]);
 #else
       if (TW == 0) v = fe_mul(v, tb[k * (g.stride >> g.loga) + (jrest >> g.loga)]);
-#endif
 #endif
       fe_store(dst + k * rstride, v);
     } else {
@@ -501,22 +489,20 @@ static hipError_t launch_pass(bool last, int zero_top, const fe* in, fe* out, co
   return launch_pass_ept<LOGR, kEPT>(last, zero_top, in, out, tw, ta, tb, g, tiles, st);
 }
 
-void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr) {
-  // Test hook: MLH_NTT_PLAN="4,8,4" forces a radix plan (digits 4..9 summing
-  // to log_n) so every pass shape can be checked at oracle-sized N.
-  if (const char* env = getenv("MLH_NTT_PLAN")) {
-    uint32_t tmp[kMaxPasses], cnt = 0, sum = 0;
-    const char* q = env;
-    while (*q && cnt < (uint32_t)kMaxPasses) {
-      const uint32_t v = (uint32_t)strtoul(q, (char**)&q, 10);
-      if (v < 4 || v > 9) { cnt = 0; break; }
-      tmp[cnt++] = v;
-      sum += v;
-      if (*q == ',') ++q; else break;
+void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr, const uint32_t* forced,
+                      uint32_t nforced) {
+  // A forced plan (mlh_set_ntt_plan: digits 4..9 summing to log_n) lets the
+  // tests check every pass shape at oracle-sized N; otherwise the default.
+  if (forced && nforced >= 2 && nforced <= (uint32_t)kMaxPasses) {
+    uint32_t sum = 0;
+    bool ok = true;
+    for (uint32_t i = 0; i < nforced; ++i) {
+      ok = ok && forced[i] >= 4 && forced[i] <= 9;
+      sum += forced[i];
     }
-    if (cnt >= 2 && sum == log_n) {
-      *nradix = cnt;
-      for (uint32_t i = 0; i < cnt; ++i) logr[i] = tmp[i];
+    if (ok && sum == log_n) {
+      *nradix = nforced;
+      for (uint32_t i = 0; i < nforced; ++i) logr[i] = forced[i];
       return;
     }
   }
@@ -588,7 +574,7 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
       default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;
-    if (getenv("MLH_DEBUG_SYNC")) {
+    if (tb.debug_sync) {
       e = hipStreamSynchronize(st);
       if (e != hipSuccess) return e;
     }

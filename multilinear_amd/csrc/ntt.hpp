@@ -8,10 +8,6 @@
 namespace mlh {
 
 constexpr int kMaxPasses = 6;
-#ifndef MLH_XTW
-#define MLH_XTW 0  // inter-pass twiddles as expanded tables (fe_mul_pre): 1 = TA and TB, 2 = TA only
-
-#endif
 // Inter-pass twiddles w_S^(jrest k) of a pass with W columns, R rows: one
 // table TA[k][jrest] (one modmul per element) while R * W <= 2^kFullTwLog
 // entries (64 MiB), else split TA[k][jl] * TB[k][jh] with 2^kTwLogA columns
@@ -21,6 +17,10 @@ constexpr int kMaxPasses = 6;
 // tables stay.  Re-measured with the LDS twiddle copies (MLH_FULL_TW_LOG=24):
 // pass 0 -2..6 %, the transform -1..2 %, for +48 % HBM bytes on pass 0 --
 // kept at 22 (the split tables' traffic stays at the algorithmic bytes).
+// Expanded inter-pass tables through the generated asm product (round 2:
+// 43 instead of ~66 VALU per multiply) measured slower -- pass 0 0.201 ->
+// 0.211-0.223 ms: the 4 expanded loads per twiddle cannot be hoisted across
+// the asm statements, so every pair of elements waits on its L2 loads.
 constexpr uint32_t kTwLogA = 8;
 #ifndef MLH_FULL_TW_LOG
 #define MLH_FULL_TW_LOG 22
@@ -44,9 +44,13 @@ struct NttTables {
   const fe* tw_small = nullptr;          // N <= 2^10: w^t, t < N/2
   fe scale;                              // n^-1 (inverse) or 1
   bool inverse = false;
+  bool debug_sync = false;               // sync after every pass (MLH_DEBUG_SYNC at context creation)
 };
 
-void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr);
+// Radix plan of a 2^log_n transform: the default, or `forced` (nforced
+// digits 4..9 summing to log_n; ignored otherwise).
+void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr,
+                      const uint32_t* forced = nullptr, uint32_t nforced = 0);
 
 // batch: vectors of in_len inputs / N outputs, contiguous
 hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n, uint64_t in_len,

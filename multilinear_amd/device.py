@@ -108,3 +108,25 @@ def random_device(n, seed, device=0):
 
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
+
+
+class ntt_plan:
+    """Context manager forcing the NTT radix plan of this device's context
+    (mlh_set_ntt_plan), e.g. ``with ntt_plan("9,4,4"): ...`` -- test/tuning hook."""
+
+    def __init__(self, plan, device=0):
+        self.digits = [int(v) for v in plan.split(",")] if isinstance(plan, str) else list(plan)
+        self.device = device
+
+    def __enter__(self):
+        import ctypes
+
+        ctx = context(self.device)
+        arr = (ctypes.c_uint32 * len(self.digits))(*self.digits)
+        check(lib().mlh_set_ntt_plan(ctx, arr, len(self.digits)), ctx)
+        return self
+
+    def __exit__(self, *exc):
+        ctx = context(self.device)
+        check(lib().mlh_set_ntt_plan(ctx, None, 0), ctx)
+        return False

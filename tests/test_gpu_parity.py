@@ -651,10 +651,14 @@ def test_fri_commit_2_24_verifies():
 
 @pytest.mark.parametrize("plan", ["4,4,4", "4,8,4", "8,4,4", "4,4,8", "5,5,5", "4,9,4",
                                   "4,4,4,4", "6,5,4"])
-def test_ntt_forced_radix_plans(plan, monkeypatch):
+def test_ntt_forced_radix_plans(plan):
     """Every pass shape (first / middle / last, radix 2^4..2^9, 3-4 passes) at
-    oracle-sized N via the MLH_NTT_PLAN test hook."""
-    monkeypatch.setenv("MLH_NTT_PLAN", plan)
+    oracle-sized N via the mlh_set_ntt_plan test hook."""
+    with D.ntt_plan(plan):
+        _forced_plan_vs_python_oracle(plan)
+
+
+def _forced_plan_vs_python_oracle(plan):
     log_n = sum(int(v) for v in plan.split(","))
     n = 1 << log_n
     g = F.pow_2_generator(log_n)
@@ -714,12 +718,16 @@ def test_reed_solomon_and_fri_commit_vs_c_oracle(log_n):
 
 
 @pytest.mark.parametrize("plan", ["9,4,4", "9,5,4", "4,4,9", "9,9,4", "7,7,7", "9,8,4", "5,5,5,5"])
-def test_forced_plans_vs_c_oracle(plan, monkeypatch):
+def test_forced_plans_vs_c_oracle(plan):
     """Radix-2^9 first passes (the default 2^25 plan 9,8,8 starts with one) and
     every zero-top mode against the C oracle: NTT (pass 0 <9,3,0>), INTT, RS
     (<9,3,1>: implicit zero half) and RS of bit-reversed coefficients (<9,3,2>,
     the PCS path), at the plan's size."""
-    monkeypatch.setenv("MLH_NTT_PLAN", plan)
+    with D.ntt_plan(plan):
+        _forced_plan_vs_c_oracle(plan)
+
+
+def _forced_plan_vs_c_oracle(plan):
     C = _c_oracle()
     log_n = sum(int(v) for v in plan.split(","))
     g = F.pow_2_generator(log_n)
@@ -926,3 +934,31 @@ def test_batched_pcs_prove_matches_oracle(m, n):
     assert got.verify(Transcript())
     got.outputs = [outs[0] + 1] + outs[1:]
     assert not got.verify(Transcript())
+
+
+def test_table_cache_is_bounded_and_results_stay_exact():
+    """The per-context twiddle cache is an LRU bounded by
+    mlh_set_table_cache_limit: with a 2 MiB limit, transforms of many sizes
+    (each needing its own tables, the 2^22 ones several MiB) still match the C
+    oracle, and afterwards the cache holds no more than the last operation's
+    tables."""
+    C = _c_oracle()
+    lib, ctx = D.lib(), D.context()
+    D.check(lib.mlh_set_table_cache_limit(ctx, 2 << 20), ctx)
+    try:
+        for log_n in (12, 16, 20, 22, 13, 21, 22, 15):
+            g = F.pow_2_generator(log_n)
+            x = D.random_limbs(1 << log_n, 4000 + log_n)
+            got = D.from_device(MN.Polynomial(D.to_device(x)).ntt(g).evals)
+            assert (got == C.ntt(x, log_n, g)).all(), log_n
+        # small transforms with distinct generators: their tables push the big
+        # ones out of the pinned window; the cache then fits the limit
+        x = D.random_limbs(1 << 12, 77)
+        g12 = F.pow_2_generator(12)
+        for e in range(1, 40, 2):
+            g = pow(g12, e, F.M)
+            got = D.from_device(MN.Polynomial(D.to_device(x)).ntt(g).evals)
+            assert (got == C.ntt(x, 12, g)).all(), e
+        assert lib.mlh_table_cache_bytes(ctx) <= 2 << 20
+    finally:
+        D.check(lib.mlh_set_table_cache_limit(ctx, 1 << 30), ctx)

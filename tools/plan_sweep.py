@@ -1,5 +1,5 @@
 """Time the 2^24 NTT and the 2^24 -> 2^25 RS LDE under forced radix plans
-(MLH_NTT_PLAN, the ntt_plan_radices test hook) -- dev tool for choosing the
+(mlh_set_ntt_plan, the radix-plan test hook) -- dev tool for choosing the
 default plan.  Outputs are checked equal to the default plan's."""
 import ctypes
 import os
@@ -44,10 +44,9 @@ def main():
     for kind, ln, plans in cases:
         ref = None
         for plan in plans:
-            if plan:
-                os.environ["MLH_NTT_PLAN"] = plan
-            else:
-                os.environ.pop("MLH_NTT_PLAN", None)
+            digits = [int(v) for v in plan.split(",")] if plan else []
+            arr = (ctypes.c_uint32 * max(1, len(digits)))(*digits)
+            D.check(lib.mlh_set_ntt_plan(ctx, arr, len(digits)), ctx)
             if kind == "ntt":
                 fn = lambda: D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(out), 24, g24), ctx)
                 res = out
@@ -59,7 +58,7 @@ def main():
                 ref = res.clone()
             print("%-3s 2^%d plan %-7s %.4f ms  same %s" % (kind, ln, plan or "default", ms,
                                                          bool(torch.equal(res, ref))), flush=True)
-        os.environ.pop("MLH_NTT_PLAN", None)
+        D.check(lib.mlh_set_ntt_plan(ctx, None, 0), ctx)
 
 
 if __name__ == "__main__":
