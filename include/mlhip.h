@@ -41,7 +41,8 @@ typedef enum mlh_status {
   MLH_ERR_OOM = 5,           /* device allocation failed                           */
   MLH_ERR_NOT_RS_CODE = 6,   /* fri/mod.rs:119-122 "not an RS code"                */
   MLH_ERR_VERIFY = 7,        /* verifier rejected (Merkle: IncompatibleHash)       */
-  MLH_ERR_VERIFY_INDEX = 8   /* Merkle path directions != index (IncompatibleIndex) */
+  MLH_ERR_VERIFY_INDEX = 8,  /* Merkle path directions != index (IncompatibleIndex) */
+  MLH_ERR_COMM = 9           /* a collective of the multi-GPU transport failed      */
 } mlh_status;
 
 typedef struct mlh_ctx mlh_ctx;               /* device + stream + twiddle caches */
@@ -423,6 +424,66 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
 /* PCSProof::verify (multilinear_pcs.rs:138-190), host side. */
 mlh_status mlh_pcs_verify(const mlh_pcs_proof* proof, uint32_t n_vars, const uint8_t* host_inputs,
                           const uint8_t output[16], mlh_transcript* tr);
+
+/* ---- multi-GPU: one process per GPU -------
+ * The reference has no distributed API; these run its NTT / reed_solomon /
+ * FriProof::prove / sumcheck on P = 2^p ranks.  Exchanges go through a
+ * transport: the built-in one is RCCL over xGMI (mlh_comm: rank 0 calls
+ * mlh_comm_unique_id and sends the 128 bytes to the other ranks out of band,
+ * every rank calls mlh_comm_create); a caller may supply its own (e.g. over
+ * host memory; host_side = 1 makes the library drain its stream before each
+ * call).  Every rank calls the same entry point with its shard; collectives
+ * are enqueued on the context stream.
+ * Layout of a sharded 2^log_n vector: block-cyclic with block 2^log_s, local
+ * index l of rank r = global ((l >> log_s) << (log_s + p)) | (r << log_s) |
+ * (l mod 2^log_s); "cyclic" = log_s 0. */
+typedef int (*mlh_all_to_all_fn)(void* user, const void* dev_send, void* dev_recv,
+                                 uint64_t bytes_per_rank, void* hip_stream);
+typedef int (*mlh_all_gather_fn)(void* user, const void* dev_send, void* dev_recv, uint64_t bytes,
+                                 void* hip_stream);
+typedef struct mlh_transport {
+  uint32_t world;     /* P, a power of two <= 16                                */
+  uint32_t rank;      /* this process                                           */
+  uint32_t host_side; /* 1: callbacks complete on the host (stream drained first) */
+  void* user;
+  /* chunk i (bytes_per_rank) of dev_send goes to rank i; chunk i of dev_recv came from rank i */
+  mlh_all_to_all_fn all_to_all;
+  /* dev_recv = every rank's dev_send (bytes each), in rank order */
+  mlh_all_gather_fn all_gather;
+} mlh_transport;
+typedef struct mlh_comm mlh_comm;
+mlh_status mlh_comm_unique_id(uint8_t out[128]);
+mlh_status mlh_comm_create(mlh_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t id[128],
+                           mlh_comm** out);
+void mlh_comm_destroy(mlh_comm* comm);
+mlh_status mlh_comm_transport(mlh_comm* comm, mlh_transport* out);
+/* Polynomial::ntt / LagrangePolynomial::intt (ntt/mod.rs:69-173) of a 2^log_n
+ * vector: forward takes the cyclic layout (2^log_n / P local elements) and
+ * returns block 2^log_n / P^2; inverse != 0 the reverse.  One all-to-all. */
+mlh_status mlh_sharded_ntt(mlh_ctx* ctx, const mlh_transport* tp, const void* dev_in, void* dev_out,
+                           uint32_t log_n, const uint8_t gen[16], int inverse);
+/* reed_solomon (fri/mod.rs:19-28): 2^log_n coefficients in the cyclic layout,
+ * gen of order 2^(log_n + 1) -> the codeword in block 2^(log_n + 1) / P^2. */
+mlh_status mlh_sharded_reed_solomon(mlh_ctx* ctx, const mlh_transport* tp, const void* dev_coeffs,
+                                    uint32_t log_n, const uint8_t gen[16], void* dev_code);
+/* FriProof::prove (fri/mod.rs:261-285) of a 2^log_code codeword in the block
+ * 2^log_code / P^2 layout (mlh_sharded_reed_solomon's output); layers below
+ * 2^gather_log entries are gathered and finished replicated (16 is a good
+ * value).  Every rank returns the same proof: byte-identical to mlh_fri_prove
+ * of the natural-order codeword. */
+mlh_status mlh_sharded_fri_prove(mlh_ctx* ctx, const mlh_transport* tp, const void* dev_code,
+                                 uint32_t log_code, uint32_t gather_log, mlh_transcript* tr,
+                                 mlh_fri_proof* proof);
+/* build_tables_for_pcs's delta (sumcheck.rs:128-145) in the cyclic layout:
+ * rank r gets delta[l P + r], l < 2^(n - p). */
+mlh_status mlh_sharded_eq_table(mlh_ctx* ctx, const mlh_transport* tp, const uint8_t* points,
+                                uint32_t n, void* dev_out);
+/* compute_sumcheck_polynomials (sumcheck.rs:77-102), composition x[0], of
+ * tables in the cyclic layout (folded in place); polys_out [n][2][16],
+ * rs_out [n][16] as mlh_sumcheck_prove. */
+mlh_status mlh_sharded_sumcheck_prove(mlh_ctx* ctx, const mlh_transport* tp, void* dev_m, void* dev_d,
+                                      uint32_t n, const uint8_t sum[16], mlh_transcript* tr,
+                                      uint8_t* polys_out, uint8_t* rs_out);
 
 /* ---- device timing helpers (bench / profiling) --------------------------- */
 /* Kernel timer: while enabled, every NTT pass launch is bracketed by HIP

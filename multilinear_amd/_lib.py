@@ -22,6 +22,7 @@ STATUS_NAMES = {
     6: "MLH_ERR_NOT_RS_CODE",
     7: "MLH_ERR_VERIFY",
     8: "MLH_ERR_VERIFY_INDEX",
+    9: "MLH_ERR_COMM",
 }
 STATUS_CODES = {v: k for k, v in STATUS_NAMES.items()}
 globals().update(STATUS_CODES)  # MLH_ERR_INVALID, ... as module constants
@@ -69,6 +70,24 @@ class BatchedFriProofC(ctypes.Structure):
 
 class BatchedPcsProofC(ctypes.Structure):
     _fields_ = [("fri", BatchedFriProofC), ("sumcheck_polys", ctypes.c_void_p)]
+
+
+# mlh_transport (include/mlhip.h): collectives as C callbacks
+ALL_TO_ALL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_uint64, ctypes.c_void_p)
+ALL_GATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_uint64, ctypes.c_void_p)
+
+
+class TransportC(ctypes.Structure):
+    _fields_ = [
+        ("world", ctypes.c_uint32),
+        ("rank", ctypes.c_uint32),
+        ("host_side", ctypes.c_uint32),
+        ("user", ctypes.c_void_p),
+        ("all_to_all", ALL_TO_ALL_FN),
+        ("all_gather", ALL_GATHER_FN),
+    ]
 
 
 _P = ctypes.c_void_p
@@ -178,6 +197,16 @@ SIGNATURES = {
     "mlh_profile_enable": (_I, [_P, _I]),
     "mlh_profile_reset": (_I, [_P]),
     "mlh_profile_get": (_I, [_P, ctypes.c_char_p, ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_double)]),
+    "mlh_comm_unique_id": (_I, [_P]),
+    "mlh_comm_create": (_I, [_P, _U32, _U32, _P, ctypes.POINTER(_P)]),
+    "mlh_comm_destroy": (None, [_P]),
+    "mlh_comm_transport": (_I, [_P, ctypes.POINTER(TransportC)]),
+    "mlh_sharded_ntt": (_I, [_P, ctypes.POINTER(TransportC), _P, _P, _U32, _P, _I]),
+    "mlh_sharded_reed_solomon": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _P, _P]),
+    "mlh_sharded_fri_prove": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _U32, _P,
+                                   ctypes.POINTER(FriProofC)]),
+    "mlh_sharded_eq_table": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _P]),
+    "mlh_sharded_sumcheck_prove": (_I, [_P, ctypes.POINTER(TransportC), _P, _P, _U32, _P, _P, _P, _P]),
 }
 
 _lib = None

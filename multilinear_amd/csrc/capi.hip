@@ -29,6 +29,7 @@
 #include "host_field.hpp"
 #include "host_sha256.hpp"
 #include "host_transcript.hpp"
+#include "context.hpp"
 #include "merkle.hpp"
 #include "ntt.hpp"
 #include "sha256.hpp"
@@ -37,189 +38,6 @@
 
 using namespace mlh;
 
-
-// ---------------------------------------------------------------------------
-// context
-// ---------------------------------------------------------------------------
-struct TableKey {
-  u128 base;
-  uint64_t count;
-  u128 scale;
-  int expand;
-  uint64_t cols = 0;  // 2D tables: count = rows, entry (k, j) = base^(k j mult)
-  uint64_t mult = 0;
-  bool operator<(const TableKey& o) const {
-    return std::tie(base, count, scale, expand, cols, mult) <
-           std::tie(o.base, o.count, o.scale, o.expand, o.cols, o.mult);
-  }
-};
-
-// A cached twiddle table: device buffer, size, LRU stamp.
-struct CachedTable {
-  fe* d = nullptr;
-  size_t bytes = 0;
-  uint64_t stamp = 0;
-};
-
-struct mlh_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::string err;
-  // twiddle / fold tables, bounded LRU (mlh_set_table_cache_limit)
-  std::map<TableKey, CachedTable> tables;
-  size_t table_bytes = 0;
-  size_t table_limit = (size_t)1 << 30;
-  uint64_t table_stamp = 0;
-  std::multimap<size_t, void*> pool;  // cached free device blocks
-  std::map<void*, size_t> live;       // pool-owned live blocks
-  fe* partials = nullptr;             // 2 * kMaxRedBlocks
-  fe* small = nullptr;                // 64 elements scratch (sums, points)
-  uint8_t* pinned = nullptr;          // 4 KiB pinned host staging
-  uint8_t* qstage = nullptr;          // pinned staging of query phases (grow-only)
-  size_t qstage_bytes = 0;
-  fe* ntt_scratch = nullptr;          // NTT ping-pong buffer (grow-only)
-  size_t ntt_scratch_bytes = 0;
-  // debug / test hooks, fixed at creation (MLH_DEBUG_SYNC) or set through the
-  // API (mlh_set_ntt_plan): never read from the environment on a hot path
-  bool debug_sync = false;
-  uint32_t forced_plan[kMaxPasses] = {0};
-  uint32_t forced_plan_len = 0;
-  // kernel timer (mlh_profile_*): HIP events on the launch stream
-  bool prof_on = false;
-  std::vector<hipEvent_t> ev_free;
-  struct Pending {
-    std::string label;
-    hipEvent_t a, b;
-  };
-  std::vector<Pending> pending;
-  std::map<std::string, std::pair<uint64_t, double>> prof;  // label -> (count, total ms)
-};
-
-static hipEvent_t take_event(mlh_ctx* ctx) {
-  if (!ctx->ev_free.empty()) {
-    hipEvent_t e = ctx->ev_free.back();
-    ctx->ev_free.pop_back();
-    return e;
-  }
-  hipEvent_t e = nullptr;
-  (void)hipEventCreate(&e);
-  return e;
-}
-
-static void resolve_profile(mlh_ctx* ctx) {
-  for (auto& p : ctx->pending) {
-    (void)hipEventSynchronize(p.b);
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, p.a, p.b);
-    auto& slot = ctx->prof[p.label];
-    slot.first += 1;
-    slot.second += ms;
-  }
-  // events are shared between consecutive pairs: collect unique ones
-  std::vector<hipEvent_t> evs;
-  for (auto& p : ctx->pending) {
-    evs.push_back(p.a);
-    evs.push_back(p.b);
-  }
-  std::sort(evs.begin(), evs.end());
-  evs.erase(std::unique(evs.begin(), evs.end()), evs.end());
-  for (auto e : evs) ctx->ev_free.push_back(e);
-  ctx->pending.clear();
-}
-
-// Kernel-timer bracket around one launch (no-op unless mlh_profile_enable).
-struct ProfScope {
-  mlh_ctx* ctx;
-  const char* label;
-  hipEvent_t a = nullptr;
-  ProfScope(mlh_ctx* c, const char* lab) : ctx(c), label(lab) {
-    if (ctx->prof_on) {
-      a = take_event(ctx);
-      (void)hipEventRecord(a, ctx->stream);
-    }
-  }
-  void end() {
-    if (!a) return;
-    hipEvent_t b = take_event(ctx);
-    (void)hipEventRecord(b, ctx->stream);
-    ctx->pending.push_back(mlh_ctx::Pending{label, a, b});
-    a = nullptr;
-  }
-};
-
-
-static mlh_status fail(mlh_ctx* ctx, mlh_status st, const std::string& msg) {
-  if (ctx) ctx->err = msg;
-  return st;
-}
-
-#define HIP_TRY(ctx, expr)                                                                \
-  do {                                                                                    \
-    hipError_t e_ = (expr);                                                               \
-    if (e_ != hipSuccess)                                                                 \
-      return fail((ctx), MLH_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_));  \
-  } while (0)
-
-#define MLH_TRY(expr)              \
-  do {                             \
-    mlh_status s_ = (expr);        \
-    if (s_ != MLH_OK) return s_;   \
-  } while (0)
-
-static fe to_fe(u128 v) {
-  fe r;
-  memcpy(r.w, &v, 16);
-  return r;
-}
-static u128 from_fe(const fe& x) {
-  u128 v;
-  memcpy(&v, x.w, 16);
-  return v;
-}
-
-// pooled device allocation: large per-call buffers are reused across calls
-static mlh_status pool_alloc(mlh_ctx* ctx, size_t bytes, void** out) {
-  bytes = (bytes + 255) & ~(size_t)255;
-  auto it = ctx->pool.lower_bound(bytes);
-  if (it != ctx->pool.end() && it->first <= bytes + bytes / 4) {
-    *out = it->second;
-    ctx->live[it->second] = it->first;
-    ctx->pool.erase(it);
-    return MLH_OK;
-  }
-  void* p = nullptr;
-  hipError_t e = hipMalloc(&p, bytes);
-  if (e != hipSuccess) {
-    // release cached blocks and retry once
-    for (auto& kv : ctx->pool) (void)hipFree(kv.second);
-    ctx->pool.clear();
-    e = hipMalloc(&p, bytes);
-    if (e != hipSuccess) return fail(ctx, MLH_ERR_OOM, "hipMalloc failed");
-  }
-  ctx->live[p] = bytes;
-  *out = p;
-  return MLH_OK;
-}
-static void pool_free(mlh_ctx* ctx, void* p) {
-  if (!p) return;
-  auto it = ctx->live.find(p);
-  if (it == ctx->live.end()) return;
-  ctx->pool.emplace(it->second, p);
-  ctx->live.erase(it);
-}
-
-// RAII helper for pooled buffers
-struct PoolBuf {
-  mlh_ctx* ctx;
-  void* p = nullptr;
-  explicit PoolBuf(mlh_ctx* c) : ctx(c) {}
-  ~PoolBuf() { pool_free(ctx, p); }
-  mlh_status alloc(size_t bytes) { return pool_alloc(ctx, bytes, &p); }
-  template <class T>
-  T* as() const {
-    return reinterpret_cast<T*>(p);
-  }
-};
 
 // Table cache bound: when a new table would take the cache past its limit,
 // least-recently-used tables are freed (after the stream drains, since queued

@@ -1,0 +1,573 @@
+// Multi-GPU orchestration behind the C ABI: one process per GPU, the exchange
+// steps through a pluggable transport (mlh_transport) whose built-in
+// implementation is RCCL over xGMI (mlh_comm, librccl).  The reference has no
+// distributed API (its prover is single-threaded: src/ntt/mod.rs:69-173,
+// src/fri/mod.rs:19-145 and :261-285, sumcheck.rs:77-247); SURVEY.md 8(e)
+// prescribes the sharding, DESIGN.md §6 describes the layouts.  These are the
+// schedules of multilinear_amd/dist.py (the executable spec the CPU gloo tests
+// run with oracle rank-local ops), in C++ so a Rust caller binds them directly.
+//
+// Layout: a sharded vector of 2^log_n elements over P = 2^log_p ranks is
+// block-cyclic with block S = 2^log_s: local l of rank r is global
+// ((l >> log_s) << (log_s + log_p)) | (r << log_s) | (l mod S).
+//   * NTT / RS: cyclic in (S = 1), block 2^log_n / P^2 out, ONE all-to-all.
+//   * FRI prove: block layout; every pair (i, i + n/2) and every aligned run of
+//     S leaves is local; per layer one all-gather of the subtree roots; a layer
+//     whose local part becomes one block is re-dealt by one all-to-all (or
+//     gathered below gather_log and finished replicated); transcript
+//     replicated in HBM; queries opened by the owner, combined by one gather.
+//   * Sumcheck: cyclic (rank r holds index l P + r); folds are local while the
+//     local table has >= 2 entries; the per-rank round sums are all-gathered
+//     and a device kernel adds them; the last log P rounds run replicated.
+#include <rccl/rccl.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "context.hpp"
+#include "host_sha256.hpp"
+#include "host_transcript.hpp"
+
+using namespace mlh;
+
+// ---------------------------------------------------------------------------
+// RCCL communicator and the transport wrapper
+// ---------------------------------------------------------------------------
+struct mlh_comm {
+  ncclComm_t comm = nullptr;
+  int device = 0;
+  uint32_t world = 1, rank = 0;
+};
+
+static int rccl_all_to_all(void* user, const void* send, void* recv, uint64_t bytes_per_rank,
+                           void* stream) {
+  mlh_comm* c = static_cast<mlh_comm*>(user);
+  return ncclAllToAll(send, recv, (size_t)bytes_per_rank, ncclUint8, c->comm,
+                      static_cast<hipStream_t>(stream)) == ncclSuccess
+             ? 0
+             : 1;
+}
+
+static int rccl_all_gather(void* user, const void* send, void* recv, uint64_t bytes, void* stream) {
+  mlh_comm* c = static_cast<mlh_comm*>(user);
+  return ncclAllGather(send, recv, (size_t)bytes, ncclUint8, c->comm,
+                       static_cast<hipStream_t>(stream)) == ncclSuccess
+             ? 0
+             : 1;
+}
+
+namespace {
+
+uint32_t log2u(uint64_t v) { return 63 - __builtin_clzll(v); }
+
+// Collectives of one sharded call on the context's stream.
+struct Tp {
+  mlh_ctx* ctx;
+  const mlh_transport* t;
+  uint32_t P, p, rank;
+  Tp(mlh_ctx* c, const mlh_transport* tr)
+      : ctx(c), t(tr), P(tr->world), p(log2u(tr->world)), rank(tr->rank) {}
+  mlh_status prep() {
+    if (t->host_side) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return MLH_OK;
+  }
+  // chunk i (bytes_per_rank) of send goes to rank i; chunk i of recv came from rank i
+  mlh_status all_to_all(const void* send, void* recv, uint64_t bytes_per_rank) {
+    MLH_TRY(prep());
+    if (t->all_to_all(t->user, send, recv, bytes_per_rank, ctx->stream) != 0)
+      return fail(ctx, MLH_ERR_COMM, "transport all_to_all failed");
+    return MLH_OK;
+  }
+  // recv = concatenation over ranks (rank order) of every rank's `bytes`
+  mlh_status all_gather(const void* send, void* recv, uint64_t bytes) {
+    MLH_TRY(prep());
+    if (t->all_gather(t->user, send, recv, bytes, ctx->stream) != 0)
+      return fail(ctx, MLH_ERR_COMM, "transport all_gather failed");
+    return MLH_OK;
+  }
+};
+
+mlh_status check_transport(mlh_ctx* ctx, const mlh_transport* t) {
+  if (!t || !t->all_to_all || !t->all_gather) return fail(ctx, MLH_ERR_INVALID, "null transport");
+  if (t->world == 0 || t->world > 16 || (t->world & (t->world - 1)) || t->rank >= t->world)
+    return fail(ctx, MLH_ERR_INVALID, "world must be a power of two <= 16, rank < world");
+  return MLH_OK;
+}
+
+// Device buffers owned by one sharded call, released to the context pool.
+struct Bufs {
+  mlh_ctx* ctx;
+  std::vector<void*> held;
+  explicit Bufs(mlh_ctx* c) : ctx(c) {}
+  ~Bufs() {
+    for (void* p : held) pool_free(ctx, p);
+  }
+  template <class T>
+  mlh_status get(size_t bytes, T** out) {
+    void* p = nullptr;
+    MLH_TRY(pool_alloc(ctx, bytes ? bytes : 16, &p));
+    held.push_back(p);
+    *out = static_cast<T*>(p);
+    return MLH_OK;
+  }
+};
+
+void store_fe(uint8_t out[16], u128 v) { h_store(out, v); }
+
+}  // namespace
+
+extern "C" {
+
+mlh_status mlh_comm_unique_id(uint8_t out[128]) {
+  if (!out) return MLH_ERR_INVALID;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return MLH_ERR_COMM;
+  static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+  memcpy(out, &id, 128);
+  return MLH_OK;
+}
+
+mlh_status mlh_comm_create(mlh_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t id[128],
+                           mlh_comm** out) {
+  if (!ctx || !id || !out || world == 0 || rank >= world) return MLH_ERR_INVALID;
+  *out = nullptr;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, 128);
+  std::unique_ptr<mlh_comm> c(new mlh_comm());
+  c->device = ctx->device;
+  c->world = world;
+  c->rank = rank;
+  const ncclResult_t r = ncclCommInitRank(&c->comm, (int)world, uid, (int)rank);
+  if (r != ncclSuccess) return fail(ctx, MLH_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  *out = c.release();
+  return MLH_OK;
+}
+
+void mlh_comm_destroy(mlh_comm* c) {
+  if (!c) return;
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  delete c;
+}
+
+mlh_status mlh_comm_transport(mlh_comm* c, mlh_transport* out) {
+  if (!c || !out) return MLH_ERR_INVALID;
+  out->world = c->world;
+  out->rank = c->rank;
+  out->host_side = 0;
+  out->user = c;
+  out->all_to_all = rccl_all_to_all;
+  out->all_gather = rccl_all_gather;
+  return MLH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// NTT / INTT / Reed-Solomon (ntt/mod.rs:69-173, fri/mod.rs:19-28)
+// ---------------------------------------------------------------------------
+// X[j + M t] = sum_g wP^(g t) w^(g j) Z_g[j], Z_g = NTT_M(x[g + P .]) with
+// generator w^P, M = N / P: local NTT, all-to-all of the M/P-element chunks,
+// cross-shard DFT (mlh_shard_ntt_cross).
+mlh_status mlh_sharded_ntt(mlh_ctx* ctx, const mlh_transport* t, const void* dev_in, void* dev_out,
+                           uint32_t log_n, const uint8_t gen[16], int inverse) {
+  if (!ctx || !dev_in || !dev_out || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  MLH_TRY(check_transport(ctx, t));
+  Tp tp(ctx, t);
+  if (tp.P == 1)
+    return inverse ? mlh_intt(ctx, dev_in, dev_out, log_n, gen) : mlh_ntt(ctx, dev_in, dev_out, log_n, gen);
+  if (log_n < 2 * tp.p + 1 || log_n > 40)
+    return fail(ctx, MLH_ERR_INVALID, "sharded NTT needs 2^log_n >= 2 P^2");
+  const uint64_t M = 1ull << (log_n - tp.p);
+  uint8_t gp[16];
+  store_fe(gp, h_pow(h_load(gen), (u128)tp.P));
+  Bufs b(ctx);
+  fe *z, *recv;
+  MLH_TRY(b.get(M * 16, &z));
+  MLH_TRY(b.get(M * 16, &recv));
+  if (!inverse) {
+    MLH_TRY(mlh_ntt(ctx, dev_in, z, log_n - tp.p, gp));
+    MLH_TRY(tp.all_to_all(z, recv, M / tp.P * 16));
+    MLH_TRY(mlh_shard_ntt_cross(ctx, recv, dev_out, log_n, tp.p, tp.rank, gen, 0));
+  } else {
+    MLH_TRY(mlh_shard_ntt_cross(ctx, dev_in, z, log_n, tp.p, tp.rank, gen, 1));
+    MLH_TRY(tp.all_to_all(z, recv, M / tp.P * 16));
+    MLH_TRY(mlh_intt(ctx, recv, dev_out, log_n - tp.p, gp));
+  }
+  return MLH_OK;
+}
+
+mlh_status mlh_sharded_reed_solomon(mlh_ctx* ctx, const mlh_transport* t, const void* dev_coeffs,
+                                    uint32_t log_n, const uint8_t gen[16], void* dev_code) {
+  if (!ctx || !dev_coeffs || !dev_code || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  MLH_TRY(check_transport(ctx, t));
+  Tp tp(ctx, t);
+  if (tp.P == 1) return mlh_reed_solomon(ctx, dev_coeffs, log_n, gen, dev_code);
+  const uint32_t log_c = log_n + MLH_LOG_BLOWUP;
+  if (log_c < 2 * tp.p + 1 || log_c > 40)
+    return fail(ctx, MLH_ERR_INVALID, "sharded RS needs 2^(log_n+1) >= 2 P^2");
+  const uint64_t M2 = 1ull << (log_c - tp.p);  // local code length
+  uint8_t gp[16];
+  store_fe(gp, h_pow(h_load(gen), (u128)tp.P));
+  Bufs b(ctx);
+  fe *z, *recv;
+  MLH_TRY(b.get(M2 * 16, &z));
+  MLH_TRY(b.get(M2 * 16, &recv));
+  MLH_TRY(mlh_reed_solomon(ctx, dev_coeffs, log_n - tp.p, gp, z));
+  MLH_TRY(tp.all_to_all(z, recv, M2 / tp.P * 16));
+  return mlh_shard_ntt_cross(ctx, recv, dev_code, log_c, tp.p, tp.rank, gen, 0);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// FRI prove (fri/mod.rs:57-175, 261-285) of a block-layout codeword
+// ---------------------------------------------------------------------------
+namespace {
+
+struct SLayer {
+  const fe* values = nullptr;
+  uint8_t* tree = nullptr;
+  uint32_t log_n = 0, log_p = 0, log_s = 0;
+  uint32_t sub_levels = 0;        // tree levels held locally
+  uint8_t* top = nullptr;         // device tree over the gathered level-log_s nodes
+  const uint8_t* root = nullptr;  // 32-byte device view of the root
+  std::vector<uint8_t> top_host;  // host copy of `top` (query phase)
+  uint64_t local_leaves() const { return 1ull << (log_n - 1 - log_p); }
+};
+
+uint64_t level_offset(uint64_t leaves, uint32_t level) {
+  uint64_t off = 0;
+  for (uint32_t i = 0; i < level; ++i) off += leaves >> i;
+  return off;
+}
+
+struct ShardedFri {
+  mlh_ctx* ctx;
+  Tp& tp;
+  Bufs& b;
+  std::vector<SLayer> layers;
+  ShardedFri(mlh_ctx* c, Tp& t, Bufs& bb) : ctx(c), tp(t), b(bb) {}
+
+  mlh_status make_layer(const fe* values, uint32_t log_n, bool sharded, SLayer* out) {
+    SLayer L;
+    L.values = values;
+    L.log_n = log_n;
+    L.log_p = sharded ? tp.p : 0;
+    L.log_s = sharded ? log_n - 2 * tp.p : 0;
+    L.sub_levels = sharded ? L.log_s : log_n - 1;
+    *out = L;
+    return MLH_OK;
+  }
+  mlh_status commit(SLayer& L) {  // local tree, then the top over all ranks
+    MLH_TRY(b.get(mlh_merkle_layers_bytes(L.local_leaves()), &L.tree));
+    MLH_TRY(mlh_merkle_commit_pairs(ctx, L.values, L.log_n - L.log_p, L.tree, nullptr));
+    return commit_top(L);
+  }
+  mlh_status commit_top(SLayer& L) {
+    const uint64_t tree_bytes = mlh_merkle_layers_bytes(L.local_leaves());
+    if (L.log_p == 0) {
+      L.root = L.tree + tree_bytes - 32;
+      return MLH_OK;
+    }
+    const uint64_t half_t = L.local_leaves() >> L.sub_levels;
+    const uint8_t* nodes = L.tree + 32 * level_offset(L.local_leaves(), L.sub_levels);
+    uint8_t* gathered;
+    MLH_TRY(b.get(32 * half_t * tp.P, &gathered));
+    MLH_TRY(tp.all_gather(nodes, gathered, 32 * half_t));
+    MLH_TRY(b.get(mlh_merkle_layers_bytes(half_t * tp.P), &L.top));
+    MLH_TRY(mlh_merkle_top(ctx, gathered, tp.P, half_t, L.top));
+    L.root = L.top + mlh_merkle_layers_bytes(half_t * tp.P) - 32;
+    return MLH_OK;
+  }
+  // block layout -> natural order on every rank (all-gather + one 2D copy per rank)
+  mlh_status to_natural(const fe* values, uint32_t log_n, fe** out) {
+    const uint64_t local = 1ull << (log_n - tp.p), S = 1ull << (log_n - 2 * tp.p), T = local / S;
+    fe *g, *nat;
+    MLH_TRY(b.get(local * tp.P * 16, &g));
+    MLH_TRY(b.get(local * tp.P * 16, &nat));
+    MLH_TRY(tp.all_gather(values, g, local * 16));
+    for (uint32_t r = 0; r < tp.P; ++r)
+      HIP_TRY(ctx, hipMemcpy2DAsync(nat + r * S, tp.P * S * 16, g + r * local, S * 16, S * 16, T,
+                                    hipMemcpyDeviceToDevice, ctx->stream));
+    *out = nat;
+    return MLH_OK;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+mlh_status mlh_sharded_fri_prove(mlh_ctx* ctx, const mlh_transport* t, const void* dev_code,
+                                 uint32_t log_code, uint32_t gather_log, mlh_transcript* tr,
+                                 mlh_fri_proof* proof) {
+  if (!ctx || !dev_code || !tr || !proof || !proof->commitments || !proof->queries)
+    return fail(ctx, MLH_ERR_INVALID, "null argument");
+  MLH_TRY(check_transport(ctx, t));
+  Tp tp(ctx, t);
+  if (log_code < 2 || log_code > 40) return fail(ctx, MLH_ERR_INVALID, "log_code out of range");
+  if (tp.p && log_code < 2 * tp.p) return fail(ctx, MLH_ERR_INVALID, "codeword too small for the world");
+  if (tp.P == 1) return mlh_fri_prove(ctx, dev_code, log_code, tr, proof);
+  if (gather_log < 2 * tp.p + 2) gather_log = 2 * tp.p + 2;
+  const uint32_t n0 = log_code, steps = log_code - MLH_LOG_BLOWUP;
+  Bufs b(ctx);
+  ShardedFri F(ctx, tp, b);
+  uint8_t* state;
+  fe *rbuf, *lastbuf;
+  uint32_t* flagbuf;
+  MLH_TRY(b.get(mlh_device_transcript_bytes(), &state));
+  MLH_TRY(b.get(16 * (steps + 1), &rbuf));
+  MLH_TRY(b.get(16, &lastbuf));
+  MLH_TRY(b.get(16, &flagbuf));
+  HIP_TRY(ctx, hipMemsetAsync(flagbuf, 0, 16, ctx->stream));
+  MLH_TRY(mlh_transcript_to_device(ctx, tr, state));
+  SLayer L0;
+  if (log_code > gather_log) {
+    MLH_TRY(F.make_layer(static_cast<const fe*>(dev_code), log_code, true, &L0));
+  } else {
+    fe* nat;
+    MLH_TRY(F.to_natural(static_cast<const fe*>(dev_code), log_code, &nat));
+    MLH_TRY(F.make_layer(nat, log_code, false, &L0));
+  }
+  MLH_TRY(F.commit(L0));
+  F.layers.push_back(L0);
+  MLH_TRY(mlh_device_transcript_absorb(ctx, state, F.layers.back().root, 32, rbuf));
+  bool done = false;
+  for (uint32_t k = 0; k < steps; ++k) {
+    const SLayer cur = F.layers.back();
+    if ((1ull << cur.log_n) <= (1ull << MLH_LOG_BLOWUP)) break;
+    const fe* r = rbuf + k;
+    const uint32_t log_next = cur.log_n - 1;
+    const uint64_t next_local = 1ull << (log_next - cur.log_p);
+    fe* nv;
+    MLH_TRY(b.get(next_local * 16, &nv));
+    if ((1ull << log_next) == (1ull << MLH_LOG_BLOWUP)) {  // fri/mod.rs:116-126
+      MLH_TRY(mlh_shard_fri_fold_dr(ctx, cur.values, cur.log_n, k, n0, r, nv, 40, 0, 0));
+      MLH_TRY(mlh_device_fri_last(ctx, nv, state, flagbuf, lastbuf));
+      done = true;
+      break;
+    }
+    SLayer nx;
+    if (cur.log_p == 0) {
+      MLH_TRY(F.make_layer(nv, log_next, false, &nx));
+      MLH_TRY(b.get(mlh_merkle_layers_bytes(nx.local_leaves()), &nx.tree));
+      MLH_TRY(mlh_shard_fri_fold_commit_dr(ctx, cur.values, cur.log_n, k, n0, r, nv, nx.tree, 40, 0, 0));
+    } else if (log_next >= cur.log_p + cur.log_s + 1) {  // >= 2 local blocks: pairs stay local
+      nx.values = nv;
+      nx.log_n = log_next;
+      nx.log_p = cur.log_p;
+      nx.log_s = cur.log_s;
+      nx.sub_levels = cur.log_s;
+      MLH_TRY(b.get(mlh_merkle_layers_bytes(nx.local_leaves()), &nx.tree));
+      MLH_TRY(mlh_shard_fri_fold_commit_dr(ctx, cur.values, cur.log_n - cur.log_p, k, n0, r, nv,
+                                           nx.tree, cur.log_s, cur.log_p, tp.rank));
+    } else {  // the folded layer is in natural block order: re-deal or gather
+      MLH_TRY(mlh_shard_fri_fold_dr(ctx, cur.values, cur.log_n - cur.log_p, k, n0, r, nv, cur.log_s,
+                                    cur.log_p, tp.rank));
+      fe* dealt;
+      if (log_next > gather_log) {
+        MLH_TRY(b.get(next_local * 16, &dealt));
+        MLH_TRY(tp.all_to_all(nv, dealt, next_local / tp.P * 16));
+        MLH_TRY(F.make_layer(dealt, log_next, true, &nx));
+      } else {
+        MLH_TRY(b.get(next_local * tp.P * 16, &dealt));
+        MLH_TRY(tp.all_gather(nv, dealt, next_local * 16));
+        MLH_TRY(F.make_layer(dealt, log_next, false, &nx));
+      }
+      MLH_TRY(b.get(mlh_merkle_layers_bytes(nx.local_leaves()), &nx.tree));
+      MLH_TRY(mlh_merkle_commit_pairs(ctx, nx.values, nx.log_n - nx.log_p, nx.tree, nullptr));
+    }
+    MLH_TRY(F.commit_top(nx));
+    F.layers.push_back(nx);
+    MLH_TRY(mlh_device_transcript_absorb(ctx, state, F.layers.back().root, 32, rbuf + k + 1));
+  }
+  if (!done) return fail(ctx, MLH_ERR_INVALID, "fold produced no last element");
+
+  // one wait: roots, last element, RS flag; the host transcript replays them
+  const size_t nt = F.layers.size();
+  std::vector<uint8_t> roots(32 * nt);
+  for (size_t i = 0; i < nt; ++i)
+    HIP_TRY(ctx, hipMemcpyAsync(roots.data() + 32 * i, F.layers[i].root, 32, hipMemcpyDeviceToHost,
+                                ctx->stream));
+  uint8_t last[16];
+  uint32_t flag = 0;
+  HIP_TRY(ctx, hipMemcpyAsync(last, lastbuf, 16, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(&flag, flagbuf, 4, hipMemcpyDeviceToHost, ctx->stream));
+  for (auto& L : F.layers)
+    if (L.top) {
+      const uint64_t nb = mlh_merkle_layers_bytes(L.local_leaves() >> L.sub_levels << tp.p);
+      L.top_host.resize(nb);
+      HIP_TRY(ctx, hipMemcpyAsync(L.top_host.data(), L.top, nb, hipMemcpyDeviceToHost, ctx->stream));
+    }
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (flag) return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
+  for (size_t i = 0; i < nt; ++i) mlh_transcript_absorb(tr, roots.data() + 32 * i, 32);
+  mlh_transcript_absorb(tr, last, 16);
+
+  // queries (fri/mod.rs:266-277): the owner opens, records combined by a gather
+  const uint64_t half = 1ull << (log_code - 1);
+  std::vector<uint64_t> idx(MLH_NUM_QUERIES);
+  for (uint32_t q = 0; q < MLH_NUM_QUERIES; ++q) {
+    idx[q] = transcript_query_index(tr, half);
+    uint8_t le[8];
+    memcpy(le, &idx[q], 8);
+    mlh_transcript_absorb(tr, le, 8);
+  }
+  const uint64_t qbytes = mlh_fri_query_bytes(log_code);
+  std::vector<uint8_t> mine(qbytes * MLH_NUM_QUERIES, 0);
+  uint64_t layer_off = 0;
+  for (const SLayer& L : F.layers) {
+    const uint64_t leaves = 1ull << (L.log_n - 1);
+    const uint64_t rec_len = 32ull * L.log_n;  // pair + (log_n - 1) siblings
+    std::vector<uint32_t> who;
+    std::vector<uint64_t> loc;
+    for (uint32_t q = 0; q < MLH_NUM_QUERIES; ++q) {
+      const uint64_t i = idx[q] % leaves;
+      if (L.log_p) {
+        const uint64_t r = (i >> L.log_s) & ((1ull << L.log_p) - 1);
+        if (r != tp.rank) continue;
+        loc.push_back(((i >> (L.log_s + L.log_p)) << L.log_s) | (i & ((1ull << L.log_s) - 1)));
+      } else {
+        loc.push_back(i);
+      }
+      who.push_back(q);
+    }
+    const uint64_t sub_rec = 32ull * (1 + L.sub_levels);
+    std::vector<uint8_t> recs(sub_rec * (loc.size() ? loc.size() : 1));
+    if (!loc.empty())
+      MLH_TRY(mlh_merkle_open_pairs(ctx, L.values, L.log_n - L.log_p, L.tree, L.sub_levels, loc.data(),
+                                    (uint32_t)loc.size(), recs.data()));
+    // host top levels of a sharded layer: leaves = P * half_t nodes
+    const uint64_t top_leaves = L.top ? (L.local_leaves() >> L.sub_levels) << tp.p : 0;
+    for (size_t w = 0; w < who.size(); ++w) {
+      const uint32_t q = who[w];
+      const uint64_t i = idx[q] % leaves;
+      uint8_t* dst = mine.data() + q * qbytes + layer_off;
+      memcpy(dst, recs.data() + w * sub_rec, sub_rec);
+      uint64_t off = 0, cnt = top_leaves;
+      for (uint32_t lv = 0; L.top && cnt > 1; ++lv, off += cnt, cnt >>= 1) {
+        const uint64_t node = (i >> (L.sub_levels + lv)) ^ 1;
+        memcpy(dst + sub_rec + 32 * lv, L.top_host.data() + 32 * (off + node), 32);
+      }
+    }
+    layer_off += rec_len;
+  }
+  // every record is written by exactly one rank: OR of the gathered copies
+  uint8_t *dmine, *dall;
+  MLH_TRY(b.get(mine.size(), &dmine));
+  MLH_TRY(b.get(mine.size() * tp.P, &dall));
+  HIP_TRY(ctx, hipMemcpyAsync(dmine, mine.data(), mine.size(), hipMemcpyHostToDevice, ctx->stream));
+  MLH_TRY(tp.all_gather(dmine, dall, mine.size()));
+  std::vector<uint8_t> all(mine.size() * tp.P);
+  HIP_TRY(ctx, hipMemcpyAsync(all.data(), dall, all.size(), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (uint32_t r = 1; r < tp.P; ++r)
+    for (size_t i = 0; i < mine.size(); ++i) all[i] |= all[r * mine.size() + i];
+  proof->log_code = log_code;
+  proof->num_trees = (uint32_t)nt;
+  proof->num_queries = MLH_NUM_QUERIES;
+  memcpy(proof->commitments, roots.data(), 32 * nt);
+  memcpy(proof->queries, all.data(), mine.size());
+  if (proof->query_indices) memcpy(proof->query_indices, idx.data(), 8 * MLH_NUM_QUERIES);
+  memcpy(proof->last_elem, last, 16);
+  mlh_transcript_random(tr, proof->last_random);
+  return MLH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Sumcheck (sumcheck.rs:77-247) of cyclic-layout tables
+// ---------------------------------------------------------------------------
+// delta of build_tables_for_pcs (sumcheck.rs:128-145) in the cyclic layout:
+// rank r holds delta[l P + r] = eq(points[:n-p], l) * c_r, where
+// c_r = prod_{b<p} (bit_b(r) ? points[n-1-b] : 1 - points[n-1-b]).
+mlh_status mlh_sharded_eq_table(mlh_ctx* ctx, const mlh_transport* t, const uint8_t* points,
+                                uint32_t n, void* dev_out) {
+  if (!ctx || !dev_out || (n && !points)) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  MLH_TRY(check_transport(ctx, t));
+  Tp tp(ctx, t);
+  if (n < tp.p) return fail(ctx, MLH_ERR_INVALID, "fewer variables than log2(world)");
+  u128 c = 1;
+  for (uint32_t bit = 0; bit < tp.p; ++bit) {
+    const u128 pt = h_load(points + 16 * (n - 1 - bit));
+    c = h_mul(c, ((tp.rank >> bit) & 1) ? pt : h_sub(1, pt));
+  }
+  MLH_TRY(mlh_eq_table(ctx, points, n - tp.p, dev_out));
+  if (c == 1) return MLH_OK;
+  uint8_t cb[16];
+  store_fe(cb, c);
+  return mlh_field_scale(ctx, dev_out, cb, dev_out, 1ull << (n - tp.p));
+}
+
+mlh_status mlh_sharded_sumcheck_prove(mlh_ctx* ctx, const mlh_transport* t, void* dev_m, void* dev_d,
+                                      uint32_t n, const uint8_t sum[16], mlh_transcript* tr,
+                                      uint8_t* polys_out, uint8_t* rs_out) {
+  if (!ctx || !dev_m || !dev_d || !sum || !tr || n < 1 || n > 40)
+    return fail(ctx, MLH_ERR_INVALID, "bad argument");
+  MLH_TRY(check_transport(ctx, t));
+  Tp tp(ctx, t);
+  if (n < tp.p) return fail(ctx, MLH_ERR_INVALID, "fewer variables than log2(world)");
+  if (tp.P == 1) return mlh_sumcheck_prove(ctx, dev_m, dev_d, n, sum, tr, polys_out, rs_out);
+  Bufs b(ctx);
+  uint8_t* state;
+  fe *prev, *polys, *rs, *sums, *pairs;
+  MLH_TRY(b.get(mlh_device_transcript_bytes(), &state));
+  MLH_TRY(b.get(16, &prev));
+  MLH_TRY(b.get(32ull * n, &polys));
+  MLH_TRY(b.get(16ull * n, &rs));
+  MLH_TRY(b.get(32, &sums));
+  MLH_TRY(b.get(32ull * tp.P, &pairs));
+  MLH_TRY(mlh_transcript_to_device(ctx, tr, state));
+  memcpy(ctx->pinned + 3072, sum, 16);
+  HIP_TRY(ctx, hipMemcpyAsync(prev, ctx->pinned + 3072, 16, hipMemcpyHostToDevice, ctx->stream));
+  fe* m = static_cast<fe*>(dev_m);
+  fe* d = static_cast<fe*>(dev_d);
+  bool sharded = true;
+  uint32_t log_local = n - tp.p;
+  auto go_replicated = [&](uint64_t cnt) -> mlh_status {  // gather cnt entries per rank
+    fe *gm, *gd;
+    MLH_TRY(b.get(16 * cnt * tp.P, &gm));
+    MLH_TRY(b.get(16 * cnt * tp.P, &gd));
+    MLH_TRY(tp.all_gather(m, gm, 16 * cnt));
+    MLH_TRY(tp.all_gather(d, gd, 16 * cnt));
+    m = gm;
+    d = gd;
+    sharded = false;
+    return MLH_OK;
+  };
+  if (log_local == 0) {
+    MLH_TRY(go_replicated(1));
+    log_local = n;
+  }
+  MLH_TRY(mlh_sumcheck_sums_dev(ctx, m, d, log_local, sums));
+  for (uint32_t k = 0; k < n; ++k) {
+    const fe* pr = sums;
+    if (sharded) {
+      MLH_TRY(tp.all_gather(sums, pairs, 32));
+      pr = pairs;
+    }
+    MLH_TRY(mlh_device_sumcheck_round(ctx, pr, sharded ? tp.P : 1, prev, state, polys + 2 * k, rs + k));
+    if (k + 1 == n) {
+      MLH_TRY(mlh_sumcheck_fold_dr(ctx, m, d, log_local, rs + k));
+      break;
+    }
+    if (log_local >= 2) {
+      MLH_TRY(mlh_sumcheck_fold_sums_dr(ctx, m, d, log_local, rs + k, sums));
+      --log_local;
+    } else {  // sharded, local 2 -> 1 entries: gather the P-entry tables, go replicated
+      MLH_TRY(mlh_sumcheck_fold_dr(ctx, m, d, log_local, rs + k));
+      MLH_TRY(go_replicated(1));
+      log_local = tp.p;
+      MLH_TRY(mlh_sumcheck_sums_dev(ctx, m, d, log_local, sums));
+    }
+  }
+  std::vector<uint8_t> host(48ull * n);
+  HIP_TRY(ctx, hipMemcpyAsync(host.data(), polys, 32ull * n, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(host.data() + 32ull * n, rs, 16ull * n, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (uint32_t k = 0; k < n; ++k) mlh_transcript_absorb(tr, host.data() + 32 * k, 32);
+  if (polys_out) memcpy(polys_out, host.data(), 32ull * n);
+  if (rs_out) memcpy(rs_out, host.data() + 32ull * n, 16ull * n);
+  return MLH_OK;
+}
+
+}  // extern "C"

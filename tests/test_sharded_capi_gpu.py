@@ -1,0 +1,182 @@
+"""The multi-GPU C ABI (csrc/sharded.hip: mlh_sharded_*, mlh_comm_*).
+
+* 2 and 4 real processes sharing the one GPU, exchanges through
+  sharded.HostTransport (torch.distributed gloo as C callbacks): the sharded
+  NTT / INTT / RS outputs reassemble to the single-GPU transforms, the sharded
+  FRI proof equals the single-GPU mlh_fri_prove proof byte for byte (and
+  verifies), the sharded eq table + sumcheck give the single-GPU round
+  polynomials and challenges.
+* RCCL at world 1: an mlh_comm is created from a unique id and its transport
+  callbacks (ncclAllToAll / ncclAllGather) move device buffers.
+The schedules are those of multilinear_amd/dist.py, whose Python version the
+CPU tests (tests/test_dist_cpu.py) check against the oracle over gloo.
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+from multilinear_amd import device as DV  # noqa: E402
+from multilinear_amd import dist as D  # noqa: E402
+from multilinear_amd import sharded as S  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, q):
+    import random
+
+    import torch.distributed as tdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from multilinear_amd import fri as MF
+        from multilinear_amd import ntt as MN
+        from multilinear_amd import polynomials as MPL
+        from multilinear_amd import sumcheck as MS
+        from multilinear_amd.fri import FriProof
+        from multilinear_amd.transcript import Transcript
+
+        torch.cuda.set_device(0)
+        ht = S.HostTransport(D.Transport(host_staged=True))
+        res = {}
+        # NTT / INTT
+        ln = cfg["log_ntt"]
+        x = DV.random_limbs(1 << ln, seed=31)
+        g = MN.pow_2_generator(ln)
+        xl = DV.to_device(D.shard_cyclic(x, world, rank))
+        X = S.ntt(xl, ln, g, ht)
+        res["ntt"] = DV.from_device(X).tobytes()
+        res["intt_ok"] = bool(torch.equal(S.ntt(X, ln, g, ht, inverse=True), xl))
+        # RS + FRI prove
+        lc = cfg["log_code"]
+        coeffs = DV.random_limbs(1 << (lc - 1), seed=11)
+        gc = MN.pow_2_generator(lc)
+        code = S.reed_solomon(DV.to_device(D.shard_cyclic(coeffs, world, rank)), lc - 1, gc, ht)
+        res["code"] = DV.from_device(code).tobytes()
+        pf = S.fri_prove(code, lc, Transcript(), ht, gather_log=cfg["gather_log"])
+        res["proof"] = (bytes(pf._commit), bytes(pf._q), list(pf._idx), bytes(pf.c.last_elem),
+                        bytes(pf.c.last_random), pf.verify())
+        # sumcheck
+        n = cfg["n_sc"]
+        ev = DV.random_limbs(1 << n, seed=21)
+        rr = random.Random(4)
+        pts = [rr.randrange(D.M) for _ in range(n)]
+        d = S.eq_table(pts, ht)
+        tr = Transcript()
+        polys, rs = S.sumcheck_prove(DV.to_device(D.shard_cyclic(ev, world, rank)), d, n, 777, tr, ht)
+        res["sc"] = (polys, rs, tr.random())
+        if rank == 0:  # single-GPU references
+            ref = {"ntt": DV.from_device(MN.Polynomial(DV.to_device(x)).ntt(g).evals),
+                   "code": DV.from_device(MF.reed_solomon(DV.to_device(coeffs), gc))}
+            rp = FriProof.prove(MF.reed_solomon(DV.to_device(coeffs), gc), Transcript())
+            ref["proof"] = (bytes(rp._commit), bytes(rp._q), list(rp._idx), bytes(rp.c.last_elem),
+                            bytes(rp.c.last_random))
+            tab = MS.SumcheckTables(DV.to_device(ev), MPL.eq_table(pts))
+            t2 = Transcript()
+            p2, r2 = tab.compute_sumcheck_polynomials(777, t2)
+            ref["sc"] = (p2, r2, t2.random())
+            res["ref"] = ref
+        torch.cuda.synchronize()
+        q.put((rank, res))
+    except Exception:
+        import traceback
+
+        q.put((rank, {"error": traceback.format_exc()}))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cfg", [
+    (2, dict(log_ntt=14, log_code=16, gather_log=8, n_sc=10)),
+    (4, dict(log_ntt=16, log_code=20, gather_log=12, n_sc=12)),
+    (4, dict(log_ntt=12, log_code=12, gather_log=16, n_sc=3)),
+])
+def test_sharded_capi_multiprocess(world, cfg):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=300) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+    ref = res[0].pop("ref")
+    ln, lc = cfg["log_ntt"], cfg["log_code"]
+    parts = [np.frombuffer(res[r]["ntt"], dtype=np.uint32).reshape(-1, 4) for r in range(world)]
+    assert (D.unshard_blocks(parts, ln - 2 * (world.bit_length() - 1)) == ref["ntt"]).all()
+    parts = [np.frombuffer(res[r]["code"], dtype=np.uint32).reshape(-1, 4) for r in range(world)]
+    assert (D.unshard_blocks(parts, lc - 2 * (world.bit_length() - 1)) == ref["code"]).all()
+    for r in range(world):
+        assert res[r]["intt_ok"], "rank %d: INTT(NTT(x)) != x" % r
+        assert res[r]["proof"][5], "rank %d proof rejected" % r
+        assert res[r]["proof"][:5] == ref["proof"], "rank %d: proof differs from single GPU" % r
+        assert res[r]["sc"] == ref["sc"], "rank %d: sumcheck differs from single GPU" % r
+
+
+def _rccl_worker(port, q):
+    import torch.distributed as tdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        from multilinear_amd import ntt as MN
+
+        comm = S.RcclComm.from_torch()
+        t = comm.transport
+        assert (t.world, t.rank) == (1, 0)
+        x = DV.random_device(1 << 20, 5)
+        y = torch.empty_like(x)
+        st = torch.cuda.current_stream().cuda_stream
+        ok_a2a = t.all_to_all(t.user, DV.ptr(x), DV.ptr(y), x.numel() * 4, st) == 0
+        torch.cuda.synchronize()
+        same_a2a = bool(torch.equal(x, y))
+        z = torch.empty_like(x[:4096])
+        ok_ag = t.all_gather(t.user, DV.ptr(x), DV.ptr(z), z.numel() * 4, st) == 0
+        torch.cuda.synchronize()
+        same_ag = bool(torch.equal(z, x[:4096]))
+        g = MN.pow_2_generator(16)
+        xs = DV.random_device(1 << 16, 6)
+        same_ntt = bool(torch.equal(S.ntt(xs, 16, g, comm), MN.Polynomial(xs).ntt(g).evals))
+        comm.close()
+        q.put(dict(ok_a2a=ok_a2a, same_a2a=same_a2a, ok_ag=ok_ag, same_ag=same_ag, same_ntt=same_ntt))
+    except Exception:
+        import traceback
+
+        q.put({"error": traceback.format_exc()})
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_rccl_comm_world1_transport():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        res = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+    assert "error" not in res, res.get("error")
+    assert all(res.values()), res
