@@ -681,15 +681,15 @@ def strong_ntt(args, lib, ctx, local, world, rank, barrier):
 
         def run():
             D.check(lib.mlh_ntt(ctx, D.ptr(xs), D.ptr(ys), L, gb), ctx)
-    else:
-        from multilinear_amd import dist as DS
+    else:  # mlh_sharded_ntt over libmlhip's RCCL communicator
+        from multilinear_amd import sharded as SH
 
-        tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
+        tr = _transport(local)
         log_p = world.bit_length() - 1
         xs = D.random_device(1 << (L - log_p), 4242 + rank, local)
 
         def run():
-            return DS.ntt(xs, L, g, tp, ops)
+            return SH.ntt(xs, L, g, tr, device=local)
 
     run()
     barrier()
@@ -716,16 +716,19 @@ def config4_sharded(args, local, world, rank, barrier):
     from multilinear_amd import dist as DS
     from multilinear_amd.transcript import Transcript
 
+    from multilinear_amd import sharded as SH
+
     n = args.log_n
     tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
+    tr = _transport(local)
     rr = random.Random(5)
     pts = [rr.randrange(D.M) for _ in range(n)]
     base = D.random_device(1 << (n - tp.world.bit_length() + 1), 500 + rank, local)
 
-    def run():
+    def run():  # the C-ABI schedule over libmlhip's RCCL communicator
         m = base.clone()
-        d = DS.eq_table(pts, tp, ops)
-        return DS.sumcheck_prove(m, d, n, 0, Transcript(), tp, ops)
+        d = SH.eq_table(pts, tr, local)
+        return SH.sumcheck_prove(m, d, n, 0, Transcript(), tr, local)
 
     # config 3 sharded: RS LDE of 2^n coefficients + Merkle root over the ranks
     coeffs = D.random_device(1 << (n - tp.world.bit_length() + 1), 700 + rank, local)
@@ -776,15 +779,15 @@ def config5(args, lib, ctx, local, world, rank, barrier):
         def run():
             code = MF.reed_solomon(coeffs, g, local)
             return MF.FriProof.prove(code, Transcript(), local)
-    else:
-        from multilinear_amd import dist as DS
+    else:  # the C-ABI schedule (csrc/sharded.hip) over libmlhip's RCCL communicator
+        from multilinear_amd import sharded as SH
 
-        tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
-        coeffs = D.random_device(1 << (L - 1 - tp.world.bit_length() + 1), 77 + rank, local)
+        tr = _transport(local)
+        coeffs = D.random_device(1 << (L - 1 - world.bit_length() + 1), 77 + rank, local)
 
         def run():
-            code = DS.reed_solomon(coeffs, L - 1, g, tp, ops)
-            return DS.fri_prove(code, L, Transcript(), tp, ops)
+            code = SH.reed_solomon(coeffs, L - 1, g, tr, local)
+            return SH.fri_prove(code, L, Transcript(), tr, device=local)
 
     p = run()  # warm-up (tables, allocator)
     barrier()
@@ -799,7 +802,26 @@ def config5(args, lib, ctx, local, world, rank, barrier):
         dt = _allreduce_max(dt)
     return {"config5_log_code": L, "config5_rs_fri_prove_ms": dt * 1e3,
             "config5_verified": bool(p.verify()),
-            "config5_layout": "single GPU" if world == 1 else "sharded x%d" % world}
+            "config5_layout": "single GPU" if world == 1 else
+                              "sharded x%d (mlh_sharded_reed_solomon + mlh_sharded_fri_prove)" % world}
+
+
+_TRANSPORT = []
+
+
+def _transport(local):
+    """The multi-GPU transport of the C-ABI schedules: libmlhip's own RCCL
+    communicator (unique id broadcast over the torch.distributed group); in a
+    gloo rehearsal, torch collectives as host callbacks."""
+    if not _TRANSPORT:
+        from multilinear_amd import dist as DS
+        from multilinear_amd import sharded as SH
+
+        if BACKEND == "nccl":
+            _TRANSPORT.append(SH.RcclComm.from_torch(device=local))
+        else:
+            _TRANSPORT.append(SH.HostTransport(DS.Transport(host_staged=True), local))
+    return _TRANSPORT[0]
 
 
 def _gen(lib, log_n):
