@@ -337,24 +337,38 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     kbase = k1 + (reverse_mid_digits(g, mid) << g.logr[0]);
     kshift = g.log_n - LOGR;
   }
+  if constexpr (!LAST) {
+    // w_S^(jrest k) = TA[k][jl] * TB[k][jh]: the 8 columns of a tile are 8
+    // consecutive jl, so a wave's lanes read 8 runs of 128 B per table.  The
+    // products run two elements per generated asm statement (relaxed result;
+    // bfly_asm.hpp), and the next pass takes relaxed input.
+    const uint64_t jl = jrest & ((1ull << g.loga) - 1);
 #pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    const uint64_t k = pos[e];
-    fe v = x[e];
-    if (!LAST) {
-      // w_S^(jrest k) = TA[k][jl] * TB[k][jh]: the 8 columns of a tile are
-      // 8 consecutive jl, so a wave's lanes read 8 runs of 128 B per table
-      const uint64_t jl = jrest & ((1ull << g.loga) - 1);
-      v = fe_mul(v, ta[(k << g.loga) + jl]);
+    for (int e = 0; e < EPT; e += 2) {
+      uint64_t rare;
+      const fe a0 = fe_load(ta + ((uint64_t)pos[e] << g.loga) + jl);
+      const fe a1 = fe_load(ta + ((uint64_t)pos[e + 1] << g.loga) + jl);
+      bfly_ff_v(x[e], a0, x[e + 1], a1, rare);
+      if constexpr (TW == 0) {
 #if MLH_LDS_TB
-      if (TW == 0) v = fe_mul(v, lds[k]);
+        const fe b0 = lds[pos[e]], b1 = lds[pos[e + 1]];
 #else
-      if (TW == 0) v = fe_mul(v, tb[k * (g.stride >> g.loga) + (jrest >> g.loga)]);
+        const uint64_t tcols = g.stride >> g.loga, jh = jrest >> g.loga;
+        const fe b0 = fe_load(tb + (uint64_t)pos[e] * tcols + jh);
+        const fe b1 = fe_load(tb + (uint64_t)pos[e + 1] * tcols + jh);
 #endif
-      fe_store(dst + k * rstride, v);
-    } else {
-      fe_store(out + kbase + (k << kshift), relaxed_canon(v));
+        bfly_ff_v(x[e], b0, x[e + 1], b1, rare);
+      }
+      fe_store(dst + (uint64_t)pos[e] * rstride, x[e]);
+      fe_store(dst + (uint64_t)pos[e + 1] * rstride, x[e + 1]);
     }
+  } else {
+    // canonical output, four elements per asm statement
+    static_assert(EPT % 4 == 0, "canonicalisation in fours");
+#pragma unroll
+    for (int e = 0; e < EPT; e += 4) bfly_cccc_v(x[e], x[e + 1], x[e + 2], x[e + 3]);
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) fe_store(out + kbase + ((uint64_t)pos[e] << kshift), x[e]);
   }
   (void)TPC;
 }

@@ -18,10 +18,11 @@ def _gen():
     return m
 
 
-@pytest.mark.parametrize("kinds", [("m", "m"), ("m",), ("t", "t"), ("t",), ("m", "t"), ("p", "p"), ("p",)])
+@pytest.mark.parametrize("kinds", [("m", "m"), ("m",), ("t", "t"), ("t",), ("m", "t"), ("p", "p"), ("p",),
+                                   ("f", "f"), ("f",), ("c", "c", "c", "c"), ("c",)])
 def test_variant_emulates_exactly(kinds):
     G = _gen()
-    for bsrc in ("s", "v"):
+    for bsrc in (("s", "v") if any(k in ("m", "p") for k in kinds) else ("v",)):
         lines, outs, flags, ins, ns, nv, opn = G.render(kinds, bsrc)
         G.check_hazards(lines)
         assert G.selftest(kinds, lines, opn, nv, trials=1500, seed=7) == 1500 * len(kinds)
@@ -40,6 +41,25 @@ def test_rare_paths_are_reachable_and_fixed():
     lines, _, _, _, _, nv, opn = G.render(("m",), "v")
     (a, d), = G.run_case(("m",), lines, opn, nv, [5], [top], [2])
     assert a % G.M == (5 + 2 * top) % G.M and d % G.M == (5 - 2 * top) % G.M
+
+
+def test_full_product_wrap_flag():
+    """v * w whose folded sum carries out of 2^128 (flag K, fixed by + C):
+    found by search over structured operands, e.g. (2^127 - 2) * (2^128 - 1)."""
+    G = _gen()
+    lines, _, _, _, _, nv, opn = G.render(("f",), "v")
+    for v, w in [((1 << 127) - 2, (1 << 128) - 1), ((1 << 127) + 1, (1 << 128) - 1), (G.M - 1, G.M - 1),
+                 ((1 << 128) - 1, (1 << 128) - 1), (0, G.M - 1)]:
+        (_, d), = G.run_case(("f",), lines, opn, nv, [0], [v], [w])
+        assert 0 <= d < (1 << 128) and d % G.M == (v * w) % G.M
+
+
+def test_canonicalise_edges():
+    G = _gen()
+    lines, _, _, _, _, nv, opn = G.render(("c",), "v")
+    for v in [0, 1, G.M - 1, G.M, G.M + 1, (1 << 128) - 1, G.C]:
+        (_, d), = G.run_case(("c",), lines, opn, nv, [0], [v], [1])
+        assert d == v % G.M
 
 
 def test_stage_twiddle_precondition():

@@ -56,8 +56,11 @@ class Ins:
     """One instruction.  dst/src name virtual registers (str) or immediates (int).
     A pair is ('pair', lo, hi).  sdst/cin name SGPR-pair virtual registers."""
 
-    def __init__(self, op, dst, src, sdst=None, cin=None, tag=0):
+    def __init__(self, op, dst, src, sdst=None, cin=None, tag=0, after=()):
         self.op, self.dst, self.src, self.sdst, self.cin, self.tag = op, dst, src, sdst, cin, tag
+        # names whose every read must precede this instruction (it reuses
+        # their register: the second hi partner of a pair's lo, see allocate)
+        self.after = tuple(after)
 
     def vreads(self):
         out = []
@@ -121,6 +124,91 @@ def product_prog(E, p, V, B, safe, kflag):
     return r, p
 
 
+def fmul_prog(E, p, V, W):
+    """Full product v * w of two plain 128-bit values (w: a table entry, any
+    value < 2^128), relaxed result written to the tied output d.  Product
+    scan over 7 columns (16 mads; the first mad of columns 0, 1 and the single
+    mad of column 6 cannot overflow, every other carry is counted), then
+    H*2^128 = H*C = H*0x2D00*2^32 - H: Z = L + (H*0x2D00 << 32) by 4 mads,
+    Z - H, and the top T < 2^47 folded once more (T*0x2D00*2^32 - T).  A
+    carry out of the last add (value >= 2^128, probability ~2^-35) is flagged
+    in K: the true value is s + C."""
+    acc = 0
+    r = []
+    col_hi = {}
+    for j in range(7):
+        terms = [(i, j - i) for i in range(4) if 0 <= j - i <= 3]
+        cys = []
+        for n, (i, jj) in enumerate(terms):
+            dst = ("pair", p + "P%d_%d.lo" % (j, n), p + "P%d_%d.hi" % (j, n))
+            if (n == 0 and j <= 1) or j == 6:
+                E("mad", dst, [V[i], W[jj], acc], sdst="junk")
+            else:
+                cy = p + "cy%d%d" % (j, n)
+                cys.append(cy)
+                E("mad", dst, [V[i], W[jj], acc], sdst=cy)
+            acc = dst
+        r.append(acc[1])
+        col_hi[j] = acc[2]
+        if j == 6:
+            r.append(acc[2])
+            break
+        nlo, nhi = p + "Q%d.lo" % (j + 1), p + "Q%d.hi" % (j + 1)
+        if cys:
+            c = 0
+            for n, cy in enumerate(cys):
+                d = nhi if n == len(cys) - 1 else p + "c%d_%d" % (j, n)
+                E("addc", d, [c, 0], sdst="junk", cin=cy)
+                c = d
+        else:
+            E("mov", nhi, [0])
+        E("mov", nlo, [acc[2]])
+        acc = ("pair", nlo, nhi)
+    # Z = L + (H * 0x2D00) << 32.  Z_j = r_j + r_{j+3}*0x2D00 (j = 1..3) by a
+    # mad onto the pair {r_j, 0}: r_j's own register pair, whose hi half
+    # (the column's carry word, already moved on) is re-zeroed; Z_4 = r_7*0x2D00.
+    Z = {}
+    for j in (1, 2, 3):
+        zr = p + "Zr%d" % j
+        E("mov", zr, [0], after=[col_hi[j]])
+        Z[j] = ("pair", p + "Z%d.lo" % j, p + "Z%d.hi" % j)
+        E("mad", Z[j], [r[j + 3], "k2d00", ("pair", r[j], zr)], sdst="junk")
+    Z[4] = ("pair", p + "Z4.lo", p + "Z4.hi")
+    E("mad", Z[4], [r[7], "k2d00", 0], sdst="junk")
+    # carry words (< 2^15) into the next limb
+    E("add", p + "a2", [Z[2][1], Z[1][2]], sdst=p + "e3")
+    E("addc", p + "a3", [Z[3][1], Z[2][2]], sdst=p + "e4", cin=p + "e3")
+    E("addc", p + "a4", [Z[4][1], Z[3][2]], sdst=p + "e5", cin=p + "e4")
+    E("addc", p + "a5", [Z[4][2], 0], sdst="junk", cin=p + "e5")
+    # X = Z - H (>= 0): x0..x3, top T = (tl, th) < 2^47
+    E("sub", p + "x0", [r[0], r[4]], sdst=p + "bb0")
+    E("subb", p + "x1", [Z[1][1], r[5]], sdst=p + "bb1", cin=p + "bb0")
+    E("subb", p + "x2", [p + "a2", r[6]], sdst=p + "bb2", cin=p + "bb1")
+    E("subb", p + "x3", [p + "a3", r[7]], sdst=p + "bb3", cin=p + "bb2")
+    E("subb", p + "tl", [p + "a4", 0], sdst=p + "bb4", cin=p + "bb3")
+    E("subb", p + "th", [p + "a5", 0], sdst="junk", cin=p + "bb4")
+    # fold T: T*C = (T*0x2D00) << 32 - T  (three limbs y0..y2, >= 0)
+    Y = ("pair", p + "Y.lo", p + "Y.hi")
+    E("mad", Y, [p + "tl", "k2d00", 0], sdst="junk")
+    E("mad24", p + "Yh2", [p + "th", "k2d00", Y[2]])
+    E("sub", p + "y0", [0, p + "tl"], sdst=p + "bb5")
+    E("subb", p + "y1", [Y[1], p + "th"], sdst=p + "bb6", cin=p + "bb5")
+    E("subb", p + "y2", [p + "Yh2", 0], sdst="junk", cin=p + "bb6")
+    return [p + "x0", p + "x1", p + "x2", p + "x3"], [p + "y0", p + "y1", p + "y2"]
+
+
+def canon_prog(E, p, b):
+    """Relaxed -> canonical: x >= M iff x + C carries out of 2^128."""
+    V = ["v%d_%d" % (b, i) for i in range(4)]
+    T = [p + "T%d" % i for i in range(4)]
+    E("add", T[0], [V[0], -1], sdst=p + "e0")
+    E("addc", T[1], [V[1], "kc1"], sdst=p + "e1", cin=p + "e0")
+    E("addc", T[2], [V[2], 0], sdst=p + "e2", cin=p + "e1")
+    E("addc", T[3], [V[3], 0], sdst=p + "e3", cin=p + "e2")
+    for i in range(4):
+        E("cnd", "d%d_%d" % (b, i), [V[i], T[i]], cin=p + "e3")
+
+
 def bfly_prog(b, kind):
     """Instruction list of butterfly b.  kind 'm': with a stage twiddle, 't':
     trivial (w = 1), 'p': product only v <- w v (safe first mads; any twiddle).
@@ -132,6 +220,18 @@ def bfly_prog(b, kind):
     V = ["v%d_%d" % (b, i) for i in range(4)]
     prog = []
     E = lambda *a, **k: prog.append(Ins(*a, tag=b, **k))
+    if kind == "c":
+        canon_prog(E, p, b)
+        return prog
+    if kind == "f":
+        W = ["W%d_%d" % (b, j) for j in range(4)]
+        X, Yl = fmul_prog(E, p, V, W)
+        S = ["d%d_%d" % (b, i) for i in range(4)]
+        E("add", S[0], [X[0], Yl[0]], sdst=p + "e0")
+        E("addc", S[1], [X[1], Yl[1]], sdst=p + "e1", cin=p + "e0")
+        E("addc", S[2], [X[2], Yl[2]], sdst=p + "e2", cin=p + "e1")
+        E("addc", S[3], [X[3], 0], sdst="K%d" % b, cin=p + "e2")
+        return prog
     if kind in ("m", "p"):
         B = [["B%d_%d%d" % (b, k, j) for j in range(4)] for k in range(4)]
         r, _ = product_prog(E, p, V, B, kind == "p", "K%d" % b)
@@ -203,6 +303,12 @@ def schedule(progs):
                 for rd in readers.get(src, []):
                     if rd != idx:
                         deps[idx].append((rd, 0))
+    for idx, it in enumerate(ins):
+        for nm in it.after:
+            for rd in readers.get(nm, []):
+                deps[idx].append((rd, 0))
+            if nm in writer:
+                deps[idx].append((writer[nm], 0))
     succ = [[] for _ in range(n)]
     for i in range(n):
         for (p, g) in deps[i]:
@@ -252,11 +358,15 @@ def allocate(ins, order):
             if isinstance(s, tuple):
                 pairs.append((s[1], s[2]))
     is_temp = lambda r: r.startswith("b") and "." in r
-    # pair groups (halves may be defined by different instructions)
-    partner = {}
+    # pair groups (halves may be defined by different instructions); a lo may
+    # have several hi partners with disjoint lifetimes (one odd register)
+    lo_his, hi_lo = {}, {}
     for lo, hi in pairs:
-        partner[lo] = ("lo", hi)
-        partner[hi] = ("hi", lo)
+        lo_his.setdefault(lo, [])
+        if hi not in lo_his[lo]:
+            lo_his[lo].append(hi)
+        assert hi_lo.get(hi, lo) == lo, ("hi with two lo partners", hi)
+        hi_lo[hi] = lo
     vtemps = [r for r in first if is_temp(r) and not is_sgpr_name(r)]
     stemps = [r for r in first if is_temp(r) and is_sgpr_name(r)]
     # half-step intervals: defined by instruction t -> occupied from 2t+1, last
@@ -277,17 +387,23 @@ def allocate(ins, order):
     for r in sorted(vtemps, key=lambda r: first[r]):
         if r in assign:
             continue
-        if r in partner:
-            role, other = partner[r]
-            lo, hi = (r, other) if role == "lo" else (other, r)
+        if r in lo_his or r in hi_lo:
+            lo = r if r in lo_his else hi_lo[r]
+            his = lo_his[lo]
+            ivs = [span(h) for h in his]
+            for i in range(len(ivs)):
+                for j in range(i):
+                    a, b = ivs[i], ivs[j]
+                    assert a[1] < b[0] or b[1] < a[0], ("hi partners overlap", lo, his)
             ia = span(lo)
-            ib = span(hi)
             m = 0
-            while not (free(VBASE + 2 * m, *ia) and free(VBASE + 2 * m + 1, *ib)):
+            while not (free(VBASE + 2 * m, *ia) and all(free(VBASE + 2 * m + 1, *iv) for iv in ivs)):
                 m += 1
-            for reg, iv, nm in ((VBASE + 2 * m, ia, lo), (VBASE + 2 * m + 1, ib, hi)):
-                busy.setdefault(reg, []).append(iv)
-                assign[nm] = "v%d" % reg
+            busy.setdefault(VBASE + 2 * m, []).append(ia)
+            assign[lo] = "v%d" % (VBASE + 2 * m)
+            for h, iv in zip(his, ivs):
+                busy.setdefault(VBASE + 2 * m + 1, []).append(iv)
+                assign[h] = "v%d" % (VBASE + 2 * m + 1)
         else:
             iv = span(r)
             m = VBASE
@@ -331,24 +447,30 @@ def emit(kinds, bsrc):
     return seq, assign, nv, ns, max(tail, 0)
 
 
+def has_u(k):
+    return k in ("m", "t")
+
+
 def operand_names(kinds):
     outs, ins = [], []
     for b, k in enumerate(kinds):
-        if k != "p":
+        if has_u(k):
             outs += ["u%d_%d" % (b, i) for i in range(4)]
         outs += ["v%d_%d" % (b, i) for i in range(4)]
     flags = []
     for b, k in enumerate(kinds):
-        if k in ("m", "p"):
+        if k in ("m", "p", "f"):
             flags.append("K%d" % b)
-        if k != "p":
+        if has_u(k):
             flags += ["C2%d" % b, "B2%d" % b]
     for b, k in enumerate(kinds):
         if k in ("m", "p"):
             ins += ["B%d_%d%d" % (b, kk, j) for kk in range(4) for j in range(4)]
-    if any(k != "p" for k in kinds):
+        if k == "f":
+            ins += ["W%d_%d" % (b, j) for j in range(4)]
+    if any(k in ("m", "t", "c") for k in kinds):
         ins += ["kc1"]
-    if "m" in kinds or "p" in kinds:
+    if any(k in ("m", "p", "f") for k in kinds):
         ins += ["k2d00"]
     return outs, flags, ins
 
@@ -518,11 +640,11 @@ def value(l):
 
 def run_case(kinds, lines, opn, nv, uvals, vvals, wvals):
     """Emulate one lane; apply the flag fixes as the C++ cold path does;
-    return [(a, d)] as integers."""
+    return [(a, d)] as integers (a = None for the one-operand kinds)."""
     env = {}
     for b in range(len(kinds)):
         for i in range(4):
-            if kinds[b] != "p":
+            if has_u(kinds[b]):
                 env["%%%d" % opn["u%d_%d" % (b, i)]] = limbs(uvals[b])[i]
             env["%%%d" % opn["v%d_%d" % (b, i)]] = limbs(vvals[b])[i]
         if kinds[b] in ("m", "p"):
@@ -530,6 +652,9 @@ def run_case(kinds, lines, opn, nv, uvals, vvals, wvals):
             for k in range(4):
                 for j in range(4):
                     env["%%%d" % opn["B%d_%d%d" % (b, k, j)]] = limbs(Bs[k])[j]
+        if kinds[b] == "f":
+            for j in range(4):
+                env["%%%d" % opn["W%d_%d" % (b, j)]] = limbs(wvals[b])[j]
     if "kc1" in opn:
         env["%%%d" % opn["kc1"]] = KC1
     if "k2d00" in opn:
@@ -538,8 +663,11 @@ def run_case(kinds, lines, opn, nv, uvals, vvals, wvals):
     res = []
     for b in range(len(kinds)):
         d = value([regs["%%%d" % opn["v%d_%d" % (b, i)]] for i in range(4)])
-        if kinds[b] == "p":  # v <- w v; flag K: true value s + C
+        if kinds[b] in ("p", "f"):  # v <- w v; flag K: true value s + C
             res.append((None, add_c(d) if regs["%%%d" % opn["K%d" % b]] else d))
+            continue
+        if kinds[b] == "c":
+            res.append((None, d))
             continue
         a = value([regs["%%%d" % opn["u%d_%d" % (b, i)]] for i in range(4)])
         fk = regs.get("%%%d" % opn["K%d" % b], 0) if kinds[b] == "m" else 0
@@ -592,15 +720,19 @@ def selftest(kinds, lines, opn, nv, trials=3000, seed=1):
         uv = [pick() for _ in range(nb)]
         vv = [pick() for _ in range(nb)]
         # products ('p') take any canonical twiddle, limbs of 0xFFFFFFFF included
-        wv = [rng.choice(roots) if k != "p" else
+        wv = [rng.choice(roots) if k not in ("p", "f") else
               (rng.choice([M - 1, M - 2, (1 << 127) | 0xFFFFFFFF_FFFFFFFF_FFFFFFFF, 1, 2])
                if rng.random() < 0.3 else rng.randrange(M)) for k in kinds]
         got = run_case(kinds, lines, opn, nv, uv, vv, wv)
         for b in range(nb):
-            w = wv[b] if kinds[b] in ("m", "p") else 1
+            w = wv[b] if kinds[b] in ("m", "p", "f") else 1
             a, d = got[b]
-            if kinds[b] == "p":
+            if kinds[b] in ("p", "f"):
                 assert 0 <= d < (1 << 128) and d % M == (w * vv[b]) % M, (kinds, b, vv[b], w)
+                checked += 1
+                continue
+            if kinds[b] == "c":
+                assert d == vv[b] % M, (kinds, b, vv[b])
                 checked += 1
                 continue
             assert 0 <= a < (1 << 128) and 0 <= d < (1 << 128)
@@ -624,7 +756,8 @@ def twiddle_precondition():
 
 # ------------------------------------------------------------ C++ header ---
 
-VARIANTS = [("m", "m"), ("m",), ("t", "t"), ("t",), ("m", "t"), ("p", "p"), ("p",)]
+VARIANTS = [("m", "m"), ("m",), ("t", "t"), ("t",), ("m", "t"), ("p", "p"), ("p",), ("f", "f"), ("f",),
+            ("c", "c", "c", "c"), ("c",)]
 
 
 def cxx_function(kinds, bsrc):
@@ -633,10 +766,13 @@ def cxx_function(kinds, bsrc):
     nb = len(kinds)
     args = []
     for b in range(nb):
-        args += (["fe& u%d" % b] if kinds[b] != "p" else []) + ["fe& v%d" % b]
+        args += (["fe& u%d" % b] if has_u(kinds[b]) else []) + ["fe& v%d" % b]
         if kinds[b] in ("m", "p"):
             args += ["const fe& B%d_%d" % (b, k) for k in range(4)]
-    args += ["uint64_t& rare"]
+        if kinds[b] == "f":
+            args.append("const fe& W%d" % b)
+    if flags:
+        args += ["uint64_t& rare"]
     body = []
     for f in flags:
         body.append("  uint64_t %s;" % f)
@@ -663,21 +799,26 @@ def cxx_function(kinds, bsrc):
             il.append('"v"(kc1)')
         elif i == "k2d00":
             il.append('"s"(k2d00)')
+        elif i[0] == "W":
+            b, j = i[1:].split("_")
+            il.append('"v"(W%s.w[%s])' % (b, j))
         else:
             b, kj = i[1:].split("_")
             il.append('"%s"(B%s_%s.w[%s])' % (bsrc, b, kj[0], kj[1]))
     clob = ", ".join('"v%d"' % (VBASE + r) for r in range(nv))
     body.append('  asm volatile(\n      "%s"\n      : %s\n      : %s\n      : %s);' % (
         asm, ",\n        ".join(ol), ",\n        ".join(il), clob))
-    body.append("  rare = %s;" % " | ".join(flags))
-    body.append("  if (__builtin_expect(rare != 0, 0)) {")
+    if flags:
+        body.append("  rare = %s;" % " | ".join(flags))
+        body.append("  if (__builtin_expect(rare != 0, 0)) {")
     for b in range(nb):
-        if kinds[b] == "p":
+        if kinds[b] in ("p", "f"):
             body.append("    if ((K%d >> __lane_id()) & 1u) v%d = relaxed_add_c(v%d);" % (b, b, b))
-            continue
-        fk = "K%d" % b if kinds[b] == "m" else "0ull"
-        body.append("    bfly_fix(u%d, v%d, %s, C2%d, B2%d);" % (b, b, fk, b, b))
-    body.append("  }")
+        elif kinds[b] != "c":
+            fk = "K%d" % b if kinds[b] == "m" else "0ull"
+            body.append("    bfly_fix(u%d, v%d, %s, C2%d, B2%d);" % (b, b, fk, b, b))
+    if flags:
+        body.append("  }")
     stats = "%d VALU, %d s_nop, %d VGPR temps, %d SGPR-pair temps" % (
         sum(1 for l in lines if l.startswith("v_")), sum(1 for l in lines if l.startswith("s_nop")), nv, ns)
     return fname, "// %s\n__device__ __forceinline__ void %s(%s) {\n%s\n}\n" % (
@@ -749,7 +890,7 @@ def main():
     total = 0
     for kinds in VARIANTS:
         for bsrc in ("s", "v"):
-            if "m" not in kinds and "p" not in kinds and bsrc == "s":
+            if not any(k in ("m", "p") for k in kinds) and bsrc == "s":
                 continue
             fname, code, lines = cxx_function(kinds, bsrc)
             _, _, _, _, _, nv, opn = render(kinds, bsrc)
