@@ -1369,26 +1369,29 @@ struct EqSumcheck {
   uint32_t L = 0, a = 0, B = 0;
   PoolBuf buf;
   fe *pts = nullptr, *c = nullptr, *lo = nullptr, *d = nullptr, *H = nullptr, *scratch = nullptr;
+  fe* Hs = nullptr;  // eq suffix tables of the last a points (sumcheck_eq_tail_kernel)
   explicit EqSumcheck(mlh_ctx* c_) : ctx(c_), buf(c_) {}
 
   // matrix: round 0's table; work (2^(L-1) entries, optional) receives the
   // folded table -- the first fold reads `matrix` and writes `work`, so the
   // caller's evaluations are never copied (build_tables_for_pcs's clone)
-  mlh_status init(const fe* matrix, fe* work, uint32_t L_, const uint8_t* host_points) {
+  mlh_status init(const fe* matrix, fe* work, uint32_t L_, const uint8_t* host_points,
+                  bool want_tail = false) {
     src = matrix;
     m = work ? work : const_cast<fe*>(matrix);
     L = L_;
     a = L < kEqLo ? L : kEqLo;
     B = L - a;
-    // pts[L] | c | scratch[2^(a/2) + 2^(a - a/2)] | lo[2^a] | d[2^a] | H[2^B - 1]
+    // pts[L] | c | scratch[2^(a/2) + 2^(a - a/2)] | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1]
     const uint64_t ns = (1ull << (a / 2)) + (1ull << (a - a / 2));
-    MLH_TRY(buf.alloc(16 * (L + 1 + ns + 2 * (1ull << a) + (1ull << B))));
+    MLH_TRY(buf.alloc(16 * (L + 1 + ns + 3 * (1ull << a) + (1ull << B))));
     pts = buf.as<fe>();
     c = pts + L;
     scratch = c + 1;
     lo = scratch + ns;
     d = B ? lo + (1ull << a) : lo;  // B == 0: delta is the whole eq table
     H = lo + 2 * (1ull << a);
+    Hs = H + (1ull << B);
     // points and c_0 = 1 through the pinned staging area (pinned + 1024, at
     // most 41 x 16 B; callers use [0, 144) and [3072, 3088) for other uploads
     // and download into [0, ...) only after these kernels, on the same stream)
@@ -1399,38 +1402,72 @@ struct EqSumcheck {
     HIP_TRY(ctx, hipMemcpyAsync(pts, hp, 16ull * (L + 1), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, launch_eq_table(pts + B, a, scratch, lo, ctx->stream));
     if (B) HIP_TRY(ctx, launch_eq_suffix(pts, B, H, ctx->stream));
+    if (want_tail) HIP_TRY(ctx, launch_eq_suffix(pts + B, a, Hs, ctx->stream));
     return MLH_OK;
   }
   const fe* Hk(uint32_t k) const { return H + ((1ull << B) - (1ull << (B - k))); }
 
-  // round 0's sums into ctx->partials
+  // Head rounds k < B go in groups of up to kGroup (sumcheck.hip, "grouped
+  // eq-factored rounds"): one HBM pass yields the corner sums of a whole
+  // group, the group's rounds run from them, and one pass folds the group's
+  // variables and yields the next group's corner sums.  gk / gJ / gnb: the
+  // current group's first round, size and partial block count.
+  static constexpr uint32_t kGroup = 3;
+  uint32_t gk = 0, gJ = 0, gnb = 0;
+  uint32_t group_len(uint32_t k) const { return B - k < kGroup ? B - k : kGroup; }
+
+  // round 0's sums (B > 0: the first group's corner sums) into ctx->partials
   mlh_status first_sums(uint32_t* np) {
-    if (B)
-      HIP_TRY(ctx, launch_sums_eq(src, 1ull << (L - 1), Hk(0), lo, a, ctx->partials, ctx->stream,
-                                  np));
-    else
+    if (B) {
+      gk = 0;
+      gJ = group_len(0);
+      HIP_TRY(ctx, launch_group_sums_eq(src, 1ull << L, gJ, Hk(gJ - 1), lo, a, ctx->partials,
+                                        ctx->stream, &gnb));
+      *np = gnb;
+    } else {
       HIP_TRY(ctx, launch_sums(src, d, 1ull << (L - 1), ctx->partials, ctx->small, ctx->stream, np));
+    }
     return MLH_OK;
   }
+  // round k (r: its challenge slot; the slots of one group are contiguous)
   mlh_status round(uint32_t k, uint32_t np, fe* prev, DevSha* dt, fe* poly, fe* r) {
-    HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, prev, dt, poly, r, ctx->stream,
-                                       k < B ? pts + k : nullptr, k < B ? c : nullptr));
+    if (k < B) {
+      const uint32_t t = k - gk;
+      HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, gnb, gJ, t, t + 1, prev, dt, poly, r - t,
+                                         pts + gk, c, ctx->stream));
+    } else {
+      HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, prev, dt, poly, r, ctx->stream));
+    }
     return MLH_OK;
   }
-  // fold round k's tables with r (HBM); want_sums: also round k+1's sums
+  // all rounds of the current head group in one launch (no work between them)
+  mlh_status round_group(fe* prev, DevSha* dt, fe* polys_gk, fe* rs_gk) {
+    HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, gnb, gJ, 0, gJ, prev, dt, polys_gk, rs_gk,
+                                       pts + gk, c, ctx->stream));
+    return MLH_OK;
+  }
+  // after round k's challenge (r_dev): fold what is due (HBM); want_sums: also
+  // round k+1's sums.  A head group folds once, after its last round.
   mlh_status fold(uint32_t k, const fe* r_dev, uint32_t* np, bool want_sums = true) {
     const uint64_t S = 1ull << (L - k);
-    const fe* in = k == 0 ? src : m;
-    if (k + 1 < B) {
-      HIP_TRY(ctx, launch_fold_sums_eq(m, S, r_dev, Hk(k + 1), lo, a, ctx->partials, ctx->stream,
-                                       np, in));
-    } else if (k + 1 == B) {
-      HIP_TRY(ctx, launch_fold(m, nullptr, S, fe{}, ctx->stream, r_dev, in));
+    if (k < B) {
+      if (k + 1 < gk + gJ) return MLH_OK;  // mid-group: nothing to fold yet
+      const fe* in = gk == 0 ? src : m;
+      const uint32_t JN = group_len(k + 1);
+      HIP_TRY(ctx, launch_fold_group_eq(in, 1ull << (L - gk), gJ, JN, r_dev - (gJ - 1), m,
+                                        JN ? Hk(k + JN) : nullptr, lo, a, ctx->partials,
+                                        ctx->stream, &gnb));
+      if (JN) {
+        gk = k + 1;
+        gJ = JN;
+        *np = gnb;
+        return MLH_OK;
+      }
       HIP_TRY(ctx, launch_scale_dev(lo, c, 1ull << a, d, ctx->stream));
       if (want_sums)
         HIP_TRY(ctx, launch_sums(m, d, 1ull << (a - 1), ctx->partials, ctx->small, ctx->stream, np));
     } else {
-      MLH_TRY(sumcheck_fold_dr(ctx, m, d, S, r_dev, np, in));
+      MLH_TRY(sumcheck_fold_dr(ctx, m, d, S, r_dev, np, k == 0 ? src : m));
     }
     return MLH_OK;
   }
@@ -1455,17 +1492,28 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
   HIP_TRY(ctx, hipMemcpyAsync(sb, ctx->pinned, 144, hipMemcpyHostToDevice, ctx->stream));
   EqSumcheck es(ctx);
   MLH_TRY(es.init(reinterpret_cast<const fe*>(dev_evals), reinterpret_cast<fe*>(dev_work), L,
-                  host_points));
+                  host_points, true));
   // head rounds stream only the matrix; the last a rounds (delta materialised,
   // 2^a entries) run in the LDS-resident tail launch
+  // head groups: one launch for a group's rounds, one HBM pass folding it and
+  // summing the next group; the last group's fold is fused into the tail's load
   uint32_t np = 0;
   if (es.B) MLH_TRY(es.first_sums(&np));
-  for (uint32_t k = 0; k < es.B; ++k) {
-    MLH_TRY(es.round(k, np, prev, dt, polys + 2 * k, rs + k));
-    MLH_TRY(es.fold(k, rs + k, &np, false));
+  for (uint32_t k = 0; k < es.B;) {
+    const uint32_t J = es.gJ;
+    MLH_TRY(es.round_group(prev, dt, polys + 2 * k, rs + k));
+    k += J;
+    if (k < es.B) MLH_TRY(es.fold(k - 1, rs + k - 1, &np, false));
   }
-  HIP_TRY(ctx, launch_sumcheck_tail(es.m, es.d, es.a, prev, dt, polys + 2 * es.B, rs + es.B,
-                                    ctx->stream, es.B ? es.m : es.src));
+  if (es.B) {  // the last group's fold: a wide launch (the tail's 256 threads are latency-bound on it)
+    uint32_t nb = 0;
+    HIP_TRY(ctx, launch_fold_group_eq(es.gk == 0 ? es.src : es.m, 1ull << (L - es.gk), es.gJ, 0,
+                                      rs + es.gk, es.m, nullptr, nullptr, es.a, ctx->partials,
+                                      ctx->stream, &nb));
+  }
+  HIP_TRY(ctx, launch_sumcheck_eq_tail(es.B ? es.m : es.src, 0, nullptr, es.a, es.Hs,
+                                       es.pts + es.B, es.c, prev, dt, polys + 2 * es.B, rs + es.B,
+                                       es.m, es.d, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 48ull * L, es.d, 16, hipMemcpyDeviceToHost,
                               ctx->stream));

@@ -32,10 +32,13 @@ constexpr uint32_t kTailLogMax = 12;  // sumcheck_tail_kernel: 2 x 2^12 x 16 B =
 // Phase timestamps of sumcheck_tail_kernel (tools/tail_bench.hip builds this
 // file with -DMLH_TAIL_PROF; compiled out otherwise).
 #ifdef MLH_TAIL_PROF
-__device__ uint64_t g_tail_ts[64];
-#define MLH_TAIL_TS(i)                                        \
-  do {                                                        \
-    if (threadIdx.x == 0 && (i) < 64) g_tail_ts[i] = wall_clock64(); \
+__device__ uint64_t g_tail_ts[64], g_tail_cyc[64];
+#define MLH_TAIL_TS(i)                                \
+  do {                                                \
+    if (threadIdx.x == 0 && (i) < 64) {               \
+      g_tail_ts[i] = wall_clock64();                  \
+      g_tail_cyc[i] = __builtin_amdgcn_s_memtime();   \
+    }                                                 \
   } while (0)
 #else
 #define MLH_TAIL_TS(i) \
@@ -222,6 +225,91 @@ fold_sums_eq_kernel(fe* m, uint64_t S, const fe* __restrict__ rp, const fe* __re
   if (threadIdx.x == 0) {
     fe_store(partials + 2 * blockIdx.x, e0);
     fe_store(partials + 2 * blockIdx.x + 1, e1);
+  }
+}
+
+// ---- grouped eq-factored rounds ------------------------------------------------
+// A group of J <= 3 consecutive head rounds k..k+J-1 is served by ONE read of
+// its table T (S entries): with Q = S / 2^J and the corner sums
+//   X_c = sum_{i<Q} T[c Q + i] e(i),  e = eq(p_{k+J}, ..., p_{L-1}) = H_{k+J-1}[i >> a] lo[..],
+// round k+t's eq-factored sums are the contraction
+//   E_b = sum_{c: c_t = b} prod_{u<t} (c_u ? r_{k+u} : 1 - r_{k+u})
+//                          prod_{t<u<J} (c_u ? p_{k+u} : 1 - p_{k+u}) X_c
+// (c_u = bit J-1-u of c: the group's first variable is the table's MSB).  The
+// weights fold the t variables already challenged with their r's (the tables
+// the per-round kernels would have folded) and expand eq over the rest, so the
+// E0/E1 equal the per-round kernels' exactly.  One 16-B read and one modmul per
+// element serve J rounds; the J folds are applied in one pass afterwards
+// (fold_group_eq_kernel), which also emits the next group's corner sums.
+
+// corner sums X_c of a group of J rounds over T (S entries).  The grid is
+// 2^J corners x nbc blocks (block = c * nbc + bb, so partials[block] is
+// corner-major); a corner's nbc * 256 threads (a power of two >= 2^a) stride
+// over its Q entries, so a thread's i mod 2^a is fixed and lo is applied once.
+template <int J>
+__global__ void __launch_bounds__(kRedThreads)
+group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, const fe* __restrict__ H,
+                     const fe* __restrict__ lo, uint32_t a, uint32_t nbc,
+                     fe* __restrict__ partials) {
+  const uint64_t Q = S >> J;
+  const uint32_t c = blockIdx.x / nbc, bb = blockIdx.x % nbc;
+  const fe* Tc = T + (uint64_t)c * Q;
+  fe acc = fe_zero(), acc2 = fe_zero();
+  const uint64_t stride = (uint64_t)nbc * blockDim.x;
+  const uint64_t i0 = (uint64_t)bb * blockDim.x + threadIdx.x;
+  uint64_t i = i0;
+  for (; i + stride < Q; i += 2 * stride) {  // two entries in flight per thread
+    const fe h0 = fe_load(H + (i >> a)), h1 = fe_load(H + ((i + stride) >> a));
+    const fe v0 = fe_load(Tc + i), v1 = fe_load(Tc + i + stride);
+    acc = fe_add(acc, fe_mul(v0, h0));
+    acc2 = fe_add(acc2, fe_mul(v1, h1));
+  }
+  if (i < Q) acc = fe_add(acc, fe_mul(fe_load(Tc + i), fe_load(H + (i >> a))));
+  acc = fe_add(acc, acc2);
+  if (i0 < Q) acc = fe_mul(acc, fe_load(lo + (i0 & ((1ull << a) - 1))));
+  fe z = fe_zero();
+  block_reduce2(acc, z);
+  if (threadIdx.x == 0) fe_store(partials + blockIdx.x, acc);
+}
+
+// Fold T (S entries) over its J top variables with rs[0..J-1] into Tout
+// (S / 2^J entries; Tout == T allowed: each output slot is read, as corner 0,
+// only by the thread that writes it), and (JN > 0) the corner sums of the next
+// group of JN rounds over the folded table (grid: 2^JN corners x nbc blocks,
+// as group_sums_eq_kernel).
+template <int J, int JN>
+__global__ void __launch_bounds__(kRedThreads)
+fold_group_eq_kernel(const fe* Tin, uint64_t S, const fe* __restrict__ rs, fe* Tout,
+                     const fe* __restrict__ H, const fe* __restrict__ lo, uint32_t a,
+                     uint32_t nbc, fe* __restrict__ partials) {
+  constexpr int NI = 1 << J;
+  const uint64_t Sp = S >> J, Qp = Sp >> JN;
+  const uint32_t co = blockIdx.x / nbc, bb = blockIdx.x % nbc;
+  fe r[J];
+#pragma unroll
+  for (int u = 0; u < J; ++u) r[u] = fe_load(rs + u);
+  fe acc = fe_zero();
+  const uint64_t stride = (uint64_t)nbc * blockDim.x;
+  const uint64_t i0 = (uint64_t)bb * blockDim.x + threadIdx.x;
+  for (uint64_t i = i0; i < Qp; i += stride) {
+    const uint64_t x = (uint64_t)co * Qp + i;
+    fe v[NI];
+#pragma unroll
+    for (int c = 0; c < NI; ++c) v[c] = fe_load(Tin + (uint64_t)c * Sp + x);
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+      const int half = NI >> (u + 1);
+#pragma unroll
+      for (int c = 0; c < half; ++c) v[c] = lerp(v[c], v[c + half], r[u]);
+    }
+    fe_store(Tout + x, v[0]);
+    if (JN) acc = fe_add(acc, fe_mul(v[0], fe_load(H + (i >> a))));
+  }
+  if (JN) {
+    if (i0 < Qp) acc = fe_mul(acc, fe_load(lo + (i0 & ((1ull << a) - 1))));
+    fe z = fe_zero();
+    block_reduce2(acc, z);
+    if (threadIdx.x == 0) fe_store(partials + blockIdx.x, acc);
   }
 }
 
@@ -463,6 +551,62 @@ hipError_t launch_fold_sums_eq(fe* m, uint64_t S, const fe* r_dev, const fe* H, 
   return hipGetLastError();
 }
 
+// grouped kernels: per corner nbc blocks (a power of two), the corners x nbc
+// partials within the 2 * kMaxRedBlocks buffer; work >= 2^a keeps a corner's
+// stride a multiple of 2^a
+static inline unsigned group_blocks(uint64_t work, uint32_t corners) {
+  uint64_t b = work / (4 * kRedThreads);  // >= 4 entries per thread
+  const uint64_t cap = 2ull * kMaxRedBlocks / corners;
+  if (b > cap) b = cap;
+  return (unsigned)(b ? b : 1);
+}
+
+hipError_t launch_group_sums_eq(const fe* T, uint64_t S, uint32_t J, const fe* H, const fe* lo,
+                                uint32_t a, fe* partials, hipStream_t st, uint32_t* nb) {
+  if (J < 1 || J > 3 || a < 8 || (S >> J) < (1ull << a)) return hipErrorInvalidValue;
+  uint32_t nbc = group_blocks(S >> J, 1u << J);
+  while ((uint64_t)nbc * kRedThreads < (1ull << a)) nbc *= 2;  // stride >= 2^a
+  *nb = nbc;
+  const dim3 g(nbc << J), b(kRedThreads);
+  if (J == 1) hipLaunchKernelGGL(group_sums_eq_kernel<1>, g, b, 0, st, T, S, H, lo, a, nbc, partials);
+  if (J == 2) hipLaunchKernelGGL(group_sums_eq_kernel<2>, g, b, 0, st, T, S, H, lo, a, nbc, partials);
+  if (J == 3) hipLaunchKernelGGL(group_sums_eq_kernel<3>, g, b, 0, st, T, S, H, lo, a, nbc, partials);
+  return hipGetLastError();
+}
+
+template <int J>
+static void launch_fold_group_j(uint32_t JN, uint32_t nbc, hipStream_t st, const fe* Tin,
+                                uint64_t S, const fe* rs, fe* Tout, const fe* H, const fe* lo,
+                                uint32_t a, fe* partials) {
+  const dim3 g(nbc << JN), b(kRedThreads);
+  if (JN == 0)
+    hipLaunchKernelGGL((fold_group_eq_kernel<J, 0>), g, b, 0, st, Tin, S, rs, Tout, H, lo, a, nbc, partials);
+  if (JN == 1)
+    hipLaunchKernelGGL((fold_group_eq_kernel<J, 1>), g, b, 0, st, Tin, S, rs, Tout, H, lo, a, nbc, partials);
+  if (JN == 2)
+    hipLaunchKernelGGL((fold_group_eq_kernel<J, 2>), g, b, 0, st, Tin, S, rs, Tout, H, lo, a, nbc, partials);
+  if (JN == 3)
+    hipLaunchKernelGGL((fold_group_eq_kernel<J, 3>), g, b, 0, st, Tin, S, rs, Tout, H, lo, a, nbc, partials);
+}
+
+hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t JN, const fe* rs,
+                                fe* Tout, const fe* H, const fe* lo, uint32_t a, fe* partials,
+                                hipStream_t st, uint32_t* nb) {
+  if (J < 1 || J > 3 || JN > 3 || a < 8 || (S >> (J + JN)) < (1ull << a))
+    return hipErrorInvalidValue;
+  const uint64_t work = S >> (J + JN);  // per output corner
+  uint32_t nbc = (uint32_t)(work / kRedThreads < 1 ? 1 : work / kRedThreads);  // one output per thread
+  const uint32_t cap = (2 * kMaxRedBlocks) >> JN;
+  if (nbc > cap) nbc = cap;
+  if (JN)
+    while ((uint64_t)nbc * kRedThreads < (1ull << a)) nbc *= 2;
+  *nb = nbc;
+  if (J == 1) launch_fold_group_j<1>(JN, nbc, st, Tin, S, rs, Tout, H, lo, a, partials);
+  if (J == 2) launch_fold_group_j<2>(JN, nbc, st, Tin, S, rs, Tout, H, lo, a, partials);
+  if (J == 3) launch_fold_group_j<3>(JN, nbc, st, Tin, S, rs, Tout, H, lo, a, partials);
+  return hipGetLastError();
+}
+
 hipError_t launch_scale_dev(const fe* src, const fe* c, uint64_t n, fe* out, hipStream_t st) {
   hipLaunchKernelGGL(scale_dev_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, c,
                      n, out);
@@ -567,6 +711,36 @@ hipError_t launch_bitrev(const fe* in, fe* out, uint32_t log_n, hipStream_t st) 
 // ---- one sumcheck round with the transcript on the device -------------------
 namespace mlh {
 
+// Lane-0 round step: (s1, s2) = p(1), p(2) and the claim p(0) + p(1) ->
+// interpolate (closed form on x = 0,1,2), store (c1, c2), absorb them, draw
+// r (stored to r_out) and advance the claim to p(r).
+__device__ __forceinline__ fe round_step(const fe& s1, const fe& s2, fe& claim, DevSha& s,
+                                         uint32_t* stage, fe* poly_out, fe* r_out) {
+  const fe e0 = fe_sub(claim, s1);
+  const fe c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
+  const fe c1 = fe_sub(fe_sub(s1, e0), c2);
+  fe_store(poly_out, c1);
+  fe_store(poly_out + 1, c2);
+  const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
+  dsha_absorb<8>(s, w, stage);  // LE16(c1) || LE16(c2)
+  const fe r = dsha_challenge(s);
+  fe_store(r_out, r);
+  claim = fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r))));
+  return r;
+}
+// eq-factored round: (E0, E1) -> (s1, s2) = (c p E1, c (3p - 1)(2 E1 - E0))
+__device__ __forceinline__ void eq_round_sums(fe& s1, fe& s2, const fe& c, const fe& pv) {
+  const fe E0 = s1, E1 = s2;
+  const fe three_p_1 = fe_sub(fe_add(fe_dbl(pv), pv), fe_one());
+  s1 = fe_mul(fe_mul(c, pv), E1);
+  s2 = fe_mul(fe_mul(c, three_p_1), fe_sub(fe_dbl(E1), E0));
+}
+// c <- c ((1 - r)(1 - p) + r p) = c (1 - p - r + 2 r p)
+__device__ __forceinline__ fe eq_scale_next(const fe& c, const fe& pv, const fe& r) {
+  const fe f = fe_add(fe_sub(fe_sub(fe_one(), pv), r), fe_dbl(fe_mul(r, pv)));
+  return fe_mul(c, f);
+}
+
 // sums = (s1, s2) = p(1), p(2); prev = claimed sum = p(0) + p(1).  Closed-form
 // interpolation on x = 0,1,2 (polynomials.rs:51-87): e0 = prev - s1,
 // c2 = (s2 - 2 s1 + e0) / 2, c1 = s1 - e0 - c2; absorb LE16(c1), LE16(c2)
@@ -601,26 +775,306 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
   }
   block_reduce2(s1, s2);  // (its barriers also publish the staged state)
   if (threadIdx.x != 0) return;
-  if (pk) {
-    const fe E0 = s1, E1 = s2;
-    const fe three_p_1 = fe_sub(fe_add(fe_dbl(pv), pv), fe_one());
-    s1 = fe_mul(fe_mul(c, pv), E1);
-    s2 = fe_mul(fe_mul(c, three_p_1), fe_sub(fe_dbl(E1), E0));
-  }
-  const fe e0 = fe_sub(p, s1);
-  const fe c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
-  const fe c1 = fe_sub(fe_sub(s1, e0), c2);
-  fe_store(poly_out, c1);
-  fe_store(poly_out + 1, c2);
-  const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
-  dsha_absorb<8>(s, w, stage);  // LE16(c1) || LE16(c2)
+  if (pk) eq_round_sums(s1, s2, c, pv);
+  const fe r = round_step(s1, s2, p, s, stage, poly_out, r_out);
   *t = s;
-  const fe r = dsha_challenge(s);
-  fe_store(r_out, r);
-  fe_store(prev, fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r)))));
-  if (pk) {  // (1 - r)(1 - p) + r p = 1 - p - r + 2 r p
-    const fe f = fe_add(fe_sub(fe_sub(fe_one(), pv), r), fe_dbl(fe_mul(r, pv)));
-    fe_store(cdev, fe_mul(c, f));
+  fe_store(prev, p);
+  if (pk) fe_store(cdev, eq_scale_next(c, pv, r));
+}
+
+// out = P + Q (R + S T): the one two-modmul form every lane-parallel step of
+// sumcheck_group_kernel is cast in, so independent chains (corner weights,
+// the claim p(r), the eq scale) run side by side on different lanes.
+__device__ __forceinline__ fe pqrst(const fe& P, const fe& Q, const fe& R, const fe& S,
+                                    const fe& T) {
+  return fe_add(P, fe_mul(Q, fe_add(R, fe_mul(S, T))));
+}
+__device__ __forceinline__ fe shfl_fe(const fe& x, int src) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.w[i] = (uint32_t)__shfl((int)x.w[i], src, 64);
+  return r;
+}
+
+// Wave 0 (all 64 lanes) runs rounds t0..t1-1 of a group of J eq-factored
+// rounds from its corner sums, lanes split by role: lanes 8..15 hold the
+// corner sums (lane 8 + c: X_c), lane 0 the claim and the round's
+// interpolation / transcript, lane 1 the eq scale c (v: lane 0 the claim,
+// lane 1 c, on entry and on exit).  Per round: step A (pqrst on every lane) =
+// corner weights + the previous round's claim p(r) (lane 0) and scale
+// c <- c (1 - p - r + 2 r p) (lane 1); a 3-level shuffle sum gives E0/E1;
+// step B (pqrst) = s1 = (c p) E1 on lane 0 and s2 = (c (3p - 1)) (2 E1 - E0) on
+// lane 1; lane 0 interpolates, absorbs and draws r.  p / r: the group's
+// points / challenges (r[u] for u < t0 known on entry; the rest filled in);
+// polys: round t0's slot; rs: round 0's r slot (lane 0 stores r_t at rs + t).
+__device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_t t0, uint32_t t1,
+                                                const fe (&p)[3], fe (&r)[3], fe& v, DevSha& s,
+                                                uint32_t* stage, fe* polys, fe* rs) {
+  const uint32_t NC = 1u << J;
+  const uint32_t lane = threadIdx.x & 63;
+  const bool wl = lane >= 8 && lane < 8 + NC;  // corner-weight lane
+  const uint32_t cl = lane - 8;                // its corner
+  fe e0 = fe_zero(), c1 = fe_zero(), c2 = fe_zero(), rp = fe_zero(), pp = fe_zero();
+  const fe one = fe_one();
+  for (uint32_t tt = t0; tt <= t1; ++tt) {
+    const int tb = 3 + 8 * (int)tt;
+    (void)tb;
+    // step A: lane 0 claim = e0 + r (c1 + c2 r), lane 1 c (0 + c (1-p + r (2p-1))),
+    // weight lanes X_c prod(factors); first round of the launch: v as loaded
+    {
+      fe P = fe_zero(), Q = fe_zero(), R = fe_zero(), S = fe_zero(), T = fe_zero();
+      if (tt > t0) {
+        if (lane == 0) { P = e0; Q = rp; R = c1; S = c2; T = rp; }
+        if (lane == 1) { Q = v; R = fe_sub(one, pp); S = rp; T = fe_sub(fe_dbl(pp), one); }
+      } else if (lane < 2) {
+        P = v;
+      }
+      if (wl && tt < t1) {  // the J - 1 factors of corner cl (at most two: S, T)
+        S = one;
+        T = one;
+        bool first = true;
+#pragma unroll
+        for (uint32_t u = 0; u < 3; ++u) {
+          if (u >= J || u == tt) continue;
+          const bool bit = (cl >> (J - 1 - u)) & 1u;
+          const fe x = u < tt ? r[u] : p[u];
+          const fe f = bit ? x : fe_sub(one, x);
+          if (first) S = f; else T = f;
+          first = false;
+        }
+        Q = X;
+      }
+      v = pqrst(P, Q, R, S, T);
+    }
+    if (tt == t1) break;
+    MLH_TAIL_TS(tb);
+    fe pv = fe_zero();
+#pragma unroll
+    for (uint32_t u = 0; u < 3; ++u)
+      if (u == tt) pv = p[u];
+    const bool bt = (cl >> (J - 1 - tt)) & 1u;
+    fe E0 = wl && !bt ? v : fe_zero(), E1 = wl && bt ? v : fe_zero();
+    for (uint32_t m = 1; m < NC; m <<= 1) {
+      E0 = fe_add(E0, shfl_xor_fe(E0, m));
+      E1 = fe_add(E1, shfl_xor_fe(E1, m));
+    }
+    MLH_TAIL_TS(tb + 1);
+    // step B: lane 0 s1 = E1 (c p), lane 1 s2 = (2 E1 - E0)(c (3p - 1))
+    E0 = shfl_fe(E0, 8);
+    E1 = shfl_fe(E1, 8);
+    const fe cs = shfl_fe(v, 1);
+    const fe sB = pqrst(fe_zero(), lane == 0 ? E1 : fe_sub(fe_dbl(E1), E0), fe_zero(), cs,
+                        lane == 0 ? pv : fe_sub(fe_add(fe_dbl(pv), pv), one));
+    const fe s2 = shfl_fe(sB, 1);
+    MLH_TAIL_TS(tb + 2);
+    fe rr = fe_zero();
+    if (lane == 0) {
+      const fe s1 = sB;
+      e0 = fe_sub(v, s1);
+      c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
+      c1 = fe_sub(fe_sub(s1, e0), c2);
+      fe* po = polys + 2 * (tt - t0);
+      fe_store(po, c1);
+      fe_store(po + 1, c2);
+      const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
+      MLH_TAIL_TS(tb + 3);
+      dsha_absorb<8>(s, w, stage);  // LE16(c1) || LE16(c2)
+      MLH_TAIL_TS(tb + 4);
+      rr = dsha_challenge(s);
+      MLH_TAIL_TS(tb + 5);
+      fe_store(rs + tt, rr);
+    }
+    rr = shfl_fe(rr, 0);
+#pragma unroll
+    for (uint32_t u = 0; u < 3; ++u)
+      if (u == tt) r[u] = rr;
+    rp = rr;
+    pp = pv;
+    MLH_TAIL_TS(tb + 7);
+  }
+}
+
+// Rounds t0..t1-1 of a group of J eq-factored head rounds k..k+J-1 from the
+// corner sums (see "grouped eq-factored rounds"): the NC x nb partials are
+// summed 32 lanes per corner, then wave 0 runs eq_group_rounds.  pts, rs:
+// p_k.., r_k.. (rs[u] for u < t0 were written by earlier launches of this
+// group).
+__global__ void __launch_bounds__(kRedThreads)
+sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, uint32_t t0,
+                      uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
+                      const fe* __restrict__ pts, fe* cdev) {
+  __shared__ DevSha s;
+  __shared__ uint32_t stage[8];
+  __shared__ fe slot[kRedThreads / 32];
+  MLH_TAIL_TS(0);
+  if (threadIdx.x < sizeof(DevSha) / 4)
+    reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
+  const uint32_t NC = 1u << J, G = kRedThreads >> J;  // threads per corner (>= 32)
+  {
+    const uint32_t c = threadIdx.x / G, j = threadIdx.x % G;
+    fe acc = fe_zero();
+#pragma unroll 4
+    for (uint32_t b = j; b < nb; b += G) acc = fe_add(acc, fe_load(partials + (uint64_t)c * nb + b));
+    MLH_TAIL_TS(1);
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) acc = fe_add(acc, shfl_xor_fe(acc, m));
+    if ((threadIdx.x & 31) == 0) slot[threadIdx.x >> 5] = acc;
+  }
+  __syncthreads();
+  MLH_TAIL_TS(2);
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  fe X = fe_zero();
+  if (lane >= 8 && lane < 8 + NC)
+    for (uint32_t q = 0; q < G / 32; ++q) X = fe_add(X, slot[(lane - 8) * (G / 32) + q]);
+  fe p[3], r[3];
+#pragma unroll
+  for (uint32_t u = 0; u < 3; ++u) {
+    p[u] = u < J ? fe_load(pts + u) : fe_zero();
+    r[u] = u < t0 ? fe_load(rs + u) : fe_zero();
+  }
+  // lane 0: the claim; lane 1: the eq scale
+  fe v = lane == 0 ? fe_load(prev) : (lane == 1 ? fe_load(cdev) : fe_zero());
+  eq_group_rounds(X, J, t0, t1, p, r, v, s, stage, polys, rs);
+  if (lane == 0) {
+    *t = s;
+    fe_store(prev, v);
+  }
+  if (lane == 1) fe_store(cdev, v);
+  MLH_TAIL_TS(63);
+}
+
+// Fold of the 2^J corners src[c * stride] (c's MSB = the first variable)
+// with r[0..J-1]: the value at the folded table's entry.
+template <int J>
+__device__ __forceinline__ fe fold_corners(const fe* src, uint64_t stride, const fe* r) {
+  fe v[1 << J];
+#pragma unroll
+  for (int c = 0; c < (1 << J); ++c) v[c] = src[(uint64_t)c * stride];
+#pragma unroll
+  for (int u = 0; u < J; ++u) {
+    const int half = (1 << J) >> (u + 1);
+#pragma unroll
+    for (int c = 0; c < half; ++c) v[c] = lerp(v[c], v[c + half], r[u]);
+  }
+  return v[0];
+}
+__device__ __forceinline__ fe fold_corners_n(uint32_t J, const fe* src, uint64_t stride,
+                                             const fe* r) {
+  switch (J) {
+    case 0: return src[0];
+    case 1: return fold_corners<1>(src, stride, r);
+    case 2: return fold_corners<2>(src, stride, r);
+    default: return fold_corners<3>(src, stride, r);
+  }
+}
+
+// The last a rounds of an eq-factored sumcheck (mlh_sumcheck_prove_eq) in ONE
+// workgroup: the 2^a-entry matrix table m and the suffix tables e_j =
+// eq(p_{B+j+1}..p_{L-1}) (2^(a-1-j) entries at offset 2^a - 2^(a-j), as H_k)
+// staged in LDS, delta = c eq(p_B..) never materialised.  The rounds go in
+// groups of up to 3 exactly as the HBM head groups: corner sums of the group
+// over m (all waves), the group's rounds on wave 0 (eq_group_rounds), a
+// J-level fold of m in LDS.  On load, m is Tin folded over Jin <= 3 pending
+// variables with rs_in (the last head group's fold, fused here).  Writes the
+// folded matrix m_out[0], the final delta c_L (eq of no points = 1) to
+// d_out[0], the claim and the transcript.
+__global__ void __launch_bounds__(kRedThreads)
+sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_in, uint32_t a,
+                        const fe* __restrict__ ets, const fe* __restrict__ pts, fe* cdev, fe* prev,
+                        DevSha* t, fe* polys, fe* rs, fe* m_out, fe* d_out) {
+  extern __shared__ fe eq_tail_lds[];
+  fe* lm = eq_tail_lds;                 // 2^a
+  fe* le = eq_tail_lds + (1u << a);     // 2^a - 1
+  __shared__ DevSha s;
+  __shared__ uint32_t stage[8];
+  __shared__ fe slot[kRedThreads / 32];
+  __shared__ fe r_sh[3];
+  if (threadIdx.x < sizeof(DevSha) / 4)
+    reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
+  const uint32_t S0 = 1u << a;
+  MLH_TAIL_TS(38);
+  {
+    fe rin[3];
+#pragma unroll
+    for (uint32_t u = 0; u < 3; ++u) rin[u] = u < Jin ? fe_load(rs_in + u) : fe_zero();
+    if (Jin == 0) {  // plain copies, 8 per thread in flight at a time
+      for (uint32_t x0 = 0; x0 < S0; x0 += 8 * kRedThreads) {
+        fe v[8], w[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+          const uint32_t x = x0 + u * kRedThreads + threadIdx.x;
+          v[u] = x < S0 ? fe_load(Tin + x) : fe_zero();
+          w[u] = x + 1 < S0 ? fe_load(ets + x) : fe_zero();
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+          const uint32_t x = x0 + u * kRedThreads + threadIdx.x;
+          if (x < S0) lm[x] = v[u];
+          if (x + 1 < S0) le[x] = w[u];
+        }
+      }
+    } else {
+      for (uint32_t x = threadIdx.x; x < S0; x += blockDim.x) {
+        lm[x] = fold_corners_n(Jin, Tin + x, S0, rin);
+        if (x + 1 < S0) le[x] = fe_load(ets + x);
+      }
+    }
+  }
+  MLH_TAIL_TS(39);
+  const uint32_t lane = threadIdx.x & 63;
+  fe v = fe_zero();  // wave 0: lane 0 the claim, lane 1 the eq scale
+  if (threadIdx.x == 0) v = fe_load(prev);
+  if (threadIdx.x == 1) v = fe_load(cdev);
+  __syncthreads();
+  for (uint32_t j = 0; j < a;) {
+    const uint32_t J = a - j < 3 ? a - j : 3, NC = 1u << J, G = kRedThreads >> J;
+    const uint32_t S = S0 >> j, Q = S >> J;
+    const fe* e = le + (S0 - (S0 >> (j + J - 1)));  // e_{j+J-1}: Q entries
+    {  // corner sums of the group: 2^J corners x G threads
+      const uint32_t c = threadIdx.x / G, jj = threadIdx.x % G;
+      fe acc = fe_zero();
+      for (uint32_t i = jj; i < Q; i += G) acc = fe_add(acc, fe_mul(lm[c * Q + i], e[i]));
+#pragma unroll
+      for (int m = 16; m >= 1; m >>= 1) acc = fe_add(acc, shfl_xor_fe(acc, m));
+      if ((threadIdx.x & 31) == 0) slot[threadIdx.x >> 5] = acc;
+    }
+    __syncthreads();
+    MLH_TAIL_TS(40 + 4 * (j / 3));
+    if (threadIdx.x < 64) {
+      fe X = fe_zero();
+      if (lane >= 8 && lane < 8 + NC)
+        for (uint32_t q = 0; q < G / 32; ++q) X = fe_add(X, slot[(lane - 8) * (G / 32) + q]);
+      fe p[3], r[3];
+#pragma unroll
+      for (uint32_t u = 0; u < 3; ++u) {
+        p[u] = u < J ? fe_load(pts + j + u) : fe_zero();
+        r[u] = fe_zero();
+      }
+      eq_group_rounds(X, J, 0, J, p, r, v, s, stage, polys + 2 * j, rs + j);
+      if (lane == 0) {
+        r_sh[0] = r[0];
+        r_sh[1] = r[1];
+        r_sh[2] = r[2];
+      }
+    }
+    __syncthreads();
+    MLH_TAIL_TS(41 + 4 * (j / 3));
+    // fold m over the group's J variables (in place: output x reads corner 0 at x)
+    const fe rr[3] = {r_sh[0], r_sh[1], r_sh[2]};
+    for (uint32_t x = threadIdx.x; x < Q; x += blockDim.x) lm[x] = fold_corners_n(J, lm + x, Q, rr);
+    __syncthreads();
+    MLH_TAIL_TS(42 + 4 * (j / 3));
+    j += J;
+  }
+  if (threadIdx.x == 0) {
+    *t = s;
+    fe_store(prev, v);
+    fe_store(m_out, lm[0]);
+  }
+  if (threadIdx.x == 1) {
+    fe_store(cdev, v);
+    fe_store(d_out, v);
   }
 }
 
@@ -744,6 +1198,26 @@ hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, 
                                  fe* poly_out, fe* r_out, hipStream_t st, const fe* pk, fe* c) {
   hipLaunchKernelGGL(sumcheck_round_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nparts,
                      prev, t, poly_out, r_out, pk, c);
+  return hipGetLastError();
+}
+
+hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
+                                   const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
+                                   fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st) {
+  if (a == 0 || a > kTailLogMax || Jin > 3) return hipErrorInvalidValue;
+  const size_t lds = (2ull << a) * sizeof(fe);
+  hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Tin, Jin, rs_in,
+                     a, ets, pts, c, prev, t, polys, rs, m_out, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t t0,
+                                 uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
+                                 const fe* pts, fe* c, hipStream_t st) {
+  if (J < 1 || J > 3 || t0 >= t1 || t1 > J || nb == 0 || (nb << J) > 2 * kMaxRedBlocks)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sumcheck_group_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, J, t0,
+                     t1, prev, t, polys, rs, pts, c);
   return hipGetLastError();
 }
 

@@ -38,6 +38,29 @@ hipError_t launch_sums_eq(const fe* m, uint64_t h, const fe* H, const fe* lo, ui
 hipError_t launch_fold_sums_eq(fe* m, uint64_t S, const fe* r_dev, const fe* H, const fe* lo,
                                uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts,
                                const fe* m_src = nullptr);
+// Grouped eq-factored head rounds (sumcheck.hip, "grouped eq-factored
+// rounds"): corner sums of a group of J <= 3 rounds over T (S entries, e from
+// H = H_{k+J-1}) into partials[corner * nb + block]; a J-level fold of T with
+// rs[0..J-1] into Tout (S / 2^J entries, may alias T) plus the corner sums of
+// the next group of JN rounds (JN = 0: fold only; H = that group's
+// H_{k+J+JN-1}); rounds t0..t1-1 of the group from the partials (polys =
+// round k+t0's slot, rs / pts = round k's r / p).
+hipError_t launch_group_sums_eq(const fe* T, uint64_t S, uint32_t J, const fe* H, const fe* lo,
+                                uint32_t a, fe* partials, hipStream_t st, uint32_t* nb);
+hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t JN, const fe* rs,
+                                fe* Tout, const fe* H, const fe* lo, uint32_t a, fe* partials,
+                                hipStream_t st, uint32_t* nb);
+hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t t0,
+                                 uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
+                                 const fe* pts, fe* c, hipStream_t st);
+// The last a <= 12 rounds of an eq-factored sumcheck in one LDS-resident
+// workgroup (sumcheck_eq_tail_kernel): table = Tin folded over Jin <= 3
+// pending variables with rs_in (2^a entries after it), ets = eq suffix tables
+// of pts (launch_eq_suffix(pts, a)), c = the running eq scale; round j's
+// outputs at polys + 2j, rs + j; m_out[0] / d_out[0] = the folded tables.
+hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
+                                   const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
+                                   fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st);
 // out[i] = (*c) * src[i]
 hipError_t launch_scale_dev(const fe* src, const fe* c, uint64_t n, fe* out, hipStream_t st);
 // Trace::evaluate: out[j] = sum_i eq[i] * m[i * width + j], j < width;

@@ -14,6 +14,7 @@ class SumcheckTables:
         self._delta = delta
         self._evals = None   # build_tables_for_pcs: matrix = clone of these, not yet made
         self._points = None  # build_tables_for_pcs: delta = eq(points), not yet built
+        self._delta_final = None  # after the factored rounds: the 1-entry delta (bytes)
         self._device = 0
         self.height = matrix.shape[0] if matrix is not None else 0
 
@@ -40,7 +41,11 @@ class SumcheckTables:
     @property
     def delta(self):
         if self._delta is None:
-            self._delta = eq_table(self._points, self._device)
+            if self._delta_final is not None:  # uploaded on first access only
+                self._delta = to_device(ints_to_limbs([fe_from_bytes(self._delta_final)]),
+                                        self._device)
+            else:
+                self._delta = eq_table(self._points, self._device)
         return self._delta
 
     def _lh(self):
@@ -68,7 +73,7 @@ class SumcheckTables:
         n = self._lh()
         polys = (ctypes.c_uint8 * (32 * n))()
         rs = (ctypes.c_uint8 * (16 * n))()
-        if self._delta is None:  # delta = eq(points), still unbuilt: factored rounds
+        if self._delta is None and self._delta_final is None:  # delta = eq(points), unbuilt
             dl = (ctypes.c_uint8 * 16)()
             if self._matrix is None:  # read the evaluations, fold into a half-size table
                 src, work = self._evals, empty(self.height // 2, device)
@@ -79,7 +84,8 @@ class SumcheckTables:
                                               transcript.h, polys, rs, dl), ctx)
             if work is not None:
                 self._matrix = work
-            self._delta = to_device(ints_to_limbs([fe_from_bytes(dl)]), device)
+            self._delta_final = bytes(dl)
+            self._device = device
         else:
             check(lib().mlh_sumcheck_prove(ctx, ptr(self.matrix), ptr(self._delta), n,
                                            fe_bytes(total_sum), transcript.h, polys, rs), ctx)

@@ -128,13 +128,15 @@ def test_config3_rs_2_25_and_fri_commit_vs_c_oracle():
 # ---- config 4: 24-variable sumcheck rounds (sumcheck.rs:77-247) ----
 
 @pytest.mark.slow
-def test_config4_sumcheck_24_vars_vs_c_oracle():
+@pytest.mark.parametrize("n", [17, 19, 20, 24])
+def test_config4_sumcheck_24_vars_vs_c_oracle(n):
     """build_tables_for_pcs + compute_sumcheck_polynomials at 24 variables
     (the GPU keeps delta = eq(point) factored) against the reference round loop
     driven by the C oracle's eq table, partial sums and folds and the Python
-    transcript: every round polynomial, every challenge, the final transcript."""
+    transcript: every round polynomial, every challenge, the final transcript.
+    n = 17 / 19 / 20 split the n - 12 eq-factored head rounds into groups
+    3+2 / 3+3+1 / 3+3+2 (one HBM pass per group), n = 24 into 3+3+3+3."""
     Cq = _c()
-    n = 24
     ev = D.random_limbs(1 << n, 2424)
     pts = _rand(n, 24)
     m = ev.copy()

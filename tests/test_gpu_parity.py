@@ -437,7 +437,7 @@ def test_sumcheck_prove_matches_oracle(n, factored):
     assert host(evd) == ev  # build_tables_for_pcs clones: the evaluations are untouched
 
 
-@pytest.mark.parametrize("n", [1, 2, 8, 10, 13, 14, 16])
+@pytest.mark.parametrize("n", [1, 2, 8, 10, 13, 14, 16, 17])
 def test_pcs_prove_matches_oracle(n):
     """multilinear_pcs_bench_test pattern: evals 7i+3, point (0..n)."""
     ev = [F.from_i64(7 * i + 3) for i in range(1 << n)]
