@@ -1368,41 +1368,39 @@ struct EqSumcheck {
   fe* m = nullptr;          // the folded matrix (== src: folded in place)
   uint32_t L = 0, a = 0, B = 0;
   PoolBuf buf;
-  fe *pts = nullptr, *c = nullptr, *lo = nullptr, *d = nullptr, *H = nullptr, *scratch = nullptr;
+  fe *pts = nullptr, *c = nullptr, *lo = nullptr, *d = nullptr, *H = nullptr;
   fe* Hs = nullptr;  // eq suffix tables of the last a points (sumcheck_eq_tail_kernel)
   explicit EqSumcheck(mlh_ctx* c_) : ctx(c_), buf(c_) {}
 
   // matrix: round 0's table; work (2^(L-1) entries, optional) receives the
   // folded table -- the first fold reads `matrix` and writes `work`, so the
   // caller's evaluations are never copied (build_tables_for_pcs's clone)
+  // sha / sum / dt_out / prev_out (optional): also place the transcript state
+  // and the claimed sum on the device in the same launch
   mlh_status init(const fe* matrix, fe* work, uint32_t L_, const uint8_t* host_points,
-                  bool want_tail = false) {
+                  bool want_tail = false, const void* sha = nullptr, const uint8_t* sum = nullptr,
+                  DevSha* dt_out = nullptr, fe* prev_out = nullptr) {
     src = matrix;
     m = work ? work : const_cast<fe*>(matrix);
     L = L_;
     a = L < kEqLo ? L : kEqLo;
     B = L - a;
-    // pts[L] | c | scratch[2^(a/2) + 2^(a - a/2)] | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1]
-    const uint64_t ns = (1ull << (a / 2)) + (1ull << (a - a / 2));
-    MLH_TRY(buf.alloc(16 * (L + 1 + ns + 3 * (1ull << a) + (1ull << B))));
-    pts = buf.as<fe>();
-    c = pts + L;
-    scratch = c + 1;
-    lo = scratch + ns;
+    // c | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1] | pts[L]
+    MLH_TRY(buf.alloc(16 * (1 + 3 * (1ull << a) + (1ull << B) + L)));
+    c = buf.as<fe>();
+    lo = c + 1;
     d = B ? lo + (1ull << a) : lo;  // B == 0: delta is the whole eq table
     H = lo + 2 * (1ull << a);
     Hs = H + (1ull << B);
-    // points and c_0 = 1 through the pinned staging area (pinned + 1024, at
-    // most 41 x 16 B; callers use [0, 144) and [3072, 3088) for other uploads
-    // and download into [0, ...) only after these kernels, on the same stream)
-    uint8_t* hp = ctx->pinned + 1024;
-    memset(hp, 0, 16ull * (L + 1));
-    if (L) memcpy(hp, host_points, 16ull * L);
-    hp[16ull * L] = 1;
-    HIP_TRY(ctx, hipMemcpyAsync(pts, hp, 16ull * (L + 1), hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, launch_eq_table(pts + B, a, scratch, lo, ctx->stream));
-    if (B) HIP_TRY(ctx, launch_eq_suffix(pts, B, H, ctx->stream));
-    if (want_tail) HIP_TRY(ctx, launch_eq_suffix(pts + B, a, Hs, ctx->stream));
+    pts = Hs + (1ull << a);
+    EqSetupArgs args{};
+    if (L) memcpy(args.pts, host_points, 16ull * L);
+    if (sha) memcpy(&args.sha, sha, sizeof(DevSha));
+    if (sum) memcpy(&args.sum, sum, 16);
+    args.L = L;
+    args.B = B;
+    HIP_TRY(ctx, launch_eq_setup(args, pts, c, lo, H, want_tail ? Hs : nullptr, dt_out, prev_out,
+                                 ctx->stream));
     return MLH_OK;
   }
   const fe* Hk(uint32_t k) const { return H + ((1ull << B) - (1ull << (B - k))); }
@@ -1433,18 +1431,35 @@ struct EqSumcheck {
   mlh_status round(uint32_t k, uint32_t np, fe* prev, DevSha* dt, fe* poly, fe* r) {
     if (k < B) {
       const uint32_t t = k - gk;
-      HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, gnb, gJ, t, t + 1, prev, dt, poly, r - t,
+      HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, gnb, gJ, 0, t, t + 1, prev, dt, poly, r - t,
                                          pts + gk, c, ctx->stream));
     } else {
       HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, prev, dt, poly, r, ctx->stream));
     }
     return MLH_OK;
   }
-  // all rounds of the current head group in one launch (no work between them)
-  mlh_status round_group(fe* prev, DevSha* dt, fe* polys_gk, fe* rs_gk) {
-    HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, gnb, gJ, 0, gJ, prev, dt, polys_gk, rs_gk,
-                                       pts + gk, c, ctx->stream));
-    return MLH_OK;
+  // The head of a prove with no work between rounds (mlh_sumcheck_prove_eq):
+  // passes of up to 6 rounds (two chained groups of <= 3 from one set of
+  // corner sums), each folded in one HBM pass that also sums the next; the
+  // last pass's fold leaves T_B (2^a entries) in m for the tail.
+  mlh_status head_rounds(fe* prev, DevSha* dt, fe* polys, fe* rs) {
+    if (!B) return MLH_OK;
+    uint32_t nb = 0, k = 0, JT = B < kMaxGroup ? B : kMaxGroup;
+    HIP_TRY(ctx, launch_group_sums_eq(src, 1ull << L, JT, Hk(JT - 1), lo, a, ctx->partials,
+                                      ctx->stream, &nb));
+    for (;;) {
+      const uint32_t J1 = JT < 3 ? JT : 3;
+      HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, nb, J1, JT - J1, 0, J1, prev, dt,
+                                         polys + 2 * k, rs + k, pts + k, c, ctx->stream));
+      const fe* in = k == 0 ? src : m;
+      const uint64_t S = 1ull << (L - k);
+      k += JT;
+      const uint32_t JN = B - k < kMaxGroup ? B - k : kMaxGroup;
+      HIP_TRY(ctx, launch_fold_group_eq(in, S, JT, JN, rs + k - JT, m, JN ? Hk(k + JN - 1) : nullptr,
+                                        lo, a, ctx->partials, ctx->stream, &nb));
+      if (!JN) return MLH_OK;
+      JT = JN;
+    }
   }
   // after round k's challenge (r_dev): fold what is due (HBM); want_sums: also
   // round k+1's sums.  A head group folds once, after its last round.
@@ -1481,41 +1496,23 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
     return fail(ctx, MLH_ERR_INVALID, "bad argument");
   const uint32_t L = log_height;
   PoolBuf sc(ctx);
-  MLH_TRY(sc.alloc(128 + 16 + 48ull * L));
+  MLH_TRY(sc.alloc(128 + 16 + 48ull * L + 16));
   uint8_t* sb = sc.as<uint8_t>();
   DevSha* dt = reinterpret_cast<DevSha*>(sb);
   fe* prev = reinterpret_cast<fe*>(sb + 128);
   fe* polys = reinterpret_cast<fe*>(sb + 144);
   fe* rs = reinterpret_cast<fe*>(sb + 144 + 32ull * L);
-  memcpy(ctx->pinned, &tr->sha, sizeof(DevSha));
-  memcpy(ctx->pinned + 128, sum, 16);
-  HIP_TRY(ctx, hipMemcpyAsync(sb, ctx->pinned, 144, hipMemcpyHostToDevice, ctx->stream));
-  EqSumcheck es(ctx);
+  fe* dfin = reinterpret_cast<fe*>(sb + 144 + 48ull * L);  // the final delta
+  EqSumcheck es(ctx);  // its setup launch also places the transcript state and the claim
   MLH_TRY(es.init(reinterpret_cast<const fe*>(dev_evals), reinterpret_cast<fe*>(dev_work), L,
-                  host_points, true));
-  // head rounds stream only the matrix; the last a rounds (delta materialised,
-  // 2^a entries) run in the LDS-resident tail launch
-  // head groups: one launch for a group's rounds, one HBM pass folding it and
-  // summing the next group; the last group's fold is fused into the tail's load
-  uint32_t np = 0;
-  if (es.B) MLH_TRY(es.first_sums(&np));
-  for (uint32_t k = 0; k < es.B;) {
-    const uint32_t J = es.gJ;
-    MLH_TRY(es.round_group(prev, dt, polys + 2 * k, rs + k));
-    k += J;
-    if (k < es.B) MLH_TRY(es.fold(k - 1, rs + k - 1, &np, false));
-  }
-  if (es.B) {  // the last group's fold: a wide launch (the tail's 256 threads are latency-bound on it)
-    uint32_t nb = 0;
-    HIP_TRY(ctx, launch_fold_group_eq(es.gk == 0 ? es.src : es.m, 1ull << (L - es.gk), es.gJ, 0,
-                                      rs + es.gk, es.m, nullptr, nullptr, es.a, ctx->partials,
-                                      ctx->stream, &nb));
-  }
+                  host_points, true, &tr->sha, sum, dt, prev));
+  // head rounds stream only the matrix (passes of up to 6 rounds); the last a
+  // rounds run in the LDS-resident eq tail on the 2^a-entry folded table
+  MLH_TRY(es.head_rounds(prev, dt, polys, rs));
   HIP_TRY(ctx, launch_sumcheck_eq_tail(es.B ? es.m : es.src, 0, nullptr, es.a, es.Hs,
                                        es.pts + es.B, es.c, prev, dt, polys + 2 * es.B, rs + es.B,
-                                       es.m, es.d, ctx->stream));
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 48ull * L, es.d, 16, hipMemcpyDeviceToHost,
+                                       es.m, dfin, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L + 16, hipMemcpyDeviceToHost,
                               ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   std::vector<uint8_t> host(ctx->pinned, ctx->pinned + 48ull * L + 16);

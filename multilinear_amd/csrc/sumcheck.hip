@@ -98,6 +98,48 @@ __device__ __forceinline__ fe lerp(const fe& lo, const fe& hi, const fe& r) {
   return fe_add(lo, fe_mul(r, fe_sub(hi, lo)));
 }
 
+// Fold of 2^J values in registers (index MSB = the first variable) with
+// r[0..J-1]; v[0] ends with the folded value.
+template <int J>
+__device__ __forceinline__ void fold_regs(fe (&v)[1 << J], const fe* r) {
+#pragma unroll
+  for (int u = 0; u < J; ++u) {
+    const int half = (1 << J) >> (u + 1);
+#pragma unroll
+    for (int c = 0; c < half; ++c) v[c] = lerp(v[c], v[c + half], r[u]);
+  }
+}
+// Fold of the 2^J corners src[c * stride] (c's MSB = the first variable) with
+// r[0..J-1]: the folded table's entry.  J > 3: the top 3 variables per group
+// of 8 loads first (8 values in flight, not 2^J), then the rest in registers.
+template <int J>
+__device__ __forceinline__ fe fold_corners(const fe* src, uint64_t stride, const fe* r) {
+  if constexpr (J <= 3) {
+    fe v[1 << J];
+#pragma unroll
+    for (int c = 0; c < (1 << J); ++c) v[c] = src[(uint64_t)c * stride];
+    fold_regs<J>(v, r);
+    return v[0];
+  } else {
+    constexpr int J2 = J - 3;
+    fe part[1 << J2];
+#pragma unroll
+    for (int cl = 0; cl < (1 << J2); ++cl)
+      part[cl] = fold_corners<3>(src + (uint64_t)cl * stride, stride << J2, r);
+    fold_regs<J2>(part, r + 3);
+    return part[0];
+  }
+}
+__device__ __forceinline__ fe fold_corners_n(uint32_t J, const fe* src, uint64_t stride,
+                                             const fe* r) {
+  switch (J) {
+    case 0: return src[0];
+    case 1: return fold_corners<1>(src, stride, r);
+    case 2: return fold_corners<2>(src, stride, r);
+    default: return fold_corners<3>(src, stride, r);
+  }
+}
+
 // Fold tables of size S with r (in place, first half) and emit the next
 // round's sums over the folded tables (h' = S/4).
 __global__ void __launch_bounds__(kRedThreads)
@@ -246,9 +288,8 @@ fold_sums_eq_kernel(fe* m, uint64_t S, const fe* __restrict__ rp, const fe* __re
 // 2^J corners x nbc blocks (block = c * nbc + bb, so partials[block] is
 // corner-major); a corner's nbc * 256 threads (a power of two >= 2^a) stride
 // over its Q entries, so a thread's i mod 2^a is fixed and lo is applied once.
-template <int J>
 __global__ void __launch_bounds__(kRedThreads)
-group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, const fe* __restrict__ H,
+group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe* __restrict__ H,
                      const fe* __restrict__ lo, uint32_t a, uint32_t nbc,
                      fe* __restrict__ partials) {
   const uint64_t Q = S >> J;
@@ -276,37 +317,45 @@ group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, const fe* __restrict_
 // (S / 2^J entries; Tout == T allowed: each output slot is read, as corner 0,
 // only by the thread that writes it), and (JN > 0) the corner sums of the next
 // group of JN rounds over the folded table (grid: 2^JN corners x nbc blocks,
-// as group_sums_eq_kernel).
-template <int J, int JN>
+// as group_sums_eq_kernel, but the eq weight applied per output: any stride).
+template <int J, bool SPLIT>
 __global__ void __launch_bounds__(kRedThreads)
-fold_group_eq_kernel(const fe* Tin, uint64_t S, const fe* __restrict__ rs, fe* Tout,
+fold_group_eq_kernel(const fe* Tin, uint64_t S, uint32_t JN, const fe* __restrict__ rs, fe* Tout,
                      const fe* __restrict__ H, const fe* __restrict__ lo, uint32_t a,
                      uint32_t nbc, fe* __restrict__ partials) {
-  constexpr int NI = 1 << J;
+  // SPLIT (J > 3, few outputs): 2^(J-3) lanes per output, lane l folds the 8
+  // corners (c_hi, l) over the top 3 variables, then shuffle-lerps combine the
+  // lanes over the rest (more loads in flight; without it a thread's 2^J loads
+  // go 8 at a time, and every load instruction stays one 1 KiB run)
+  constexpr int J2 = SPLIT && J > 3 ? J - 3 : 0, JH = J - J2;
   const uint64_t Sp = S >> J, Qp = Sp >> JN;
   const uint32_t co = blockIdx.x / nbc, bb = blockIdx.x % nbc;
+  const uint32_t l = threadIdx.x & ((1u << J2) - 1);
   fe r[J];
 #pragma unroll
   for (int u = 0; u < J; ++u) r[u] = fe_load(rs + u);
   fe acc = fe_zero();
-  const uint64_t stride = (uint64_t)nbc * blockDim.x;
-  const uint64_t i0 = (uint64_t)bb * blockDim.x + threadIdx.x;
+  const uint64_t stride = ((uint64_t)nbc * blockDim.x) >> J2;
+  const uint64_t i0 = ((uint64_t)bb * blockDim.x + threadIdx.x) >> J2;
   for (uint64_t i = i0; i < Qp; i += stride) {
     const uint64_t x = (uint64_t)co * Qp + i;
-    fe v[NI];
+    fe v = fold_corners<JH>(Tin + (uint64_t)l * Sp + x, Sp << J2, r);
 #pragma unroll
-    for (int c = 0; c < NI; ++c) v[c] = fe_load(Tin + (uint64_t)c * Sp + x);
-#pragma unroll
-    for (int u = 0; u < J; ++u) {
-      const int half = NI >> (u + 1);
-#pragma unroll
-      for (int c = 0; c < half; ++c) v[c] = lerp(v[c], v[c + half], r[u]);
+    for (int u = 0; u < J2; ++u) {
+      const uint32_t m = 1u << (J2 - 1 - u);
+      const fe o = shfl_xor_fe(v, m);
+      const bool hi = l & m;
+      v = lerp(hi ? o : v, hi ? v : o, r[JH + u]);
     }
-    fe_store(Tout + x, v[0]);
-    if (JN) acc = fe_add(acc, fe_mul(v[0], fe_load(H + (i >> a))));
+    if (l == 0) {
+      fe_store(Tout + x, v);
+      // e(i) = H[i >> a] lo[i mod 2^a] in full: one output per 2^J inputs
+      if (JN)
+        acc = fe_add(acc, fe_mul(v, fe_mul(fe_load(H + (i >> a)),
+                                           fe_load(lo + (i & ((1ull << a) - 1))))));
+    }
   }
   if (JN) {
-    if (i0 < Qp) acc = fe_mul(acc, fe_load(lo + (i0 & ((1ull << a) - 1))));
     fe z = fe_zero();
     block_reduce2(acc, z);
     if (threadIdx.x == 0) fe_store(partials + blockIdx.x, acc);
@@ -523,6 +572,63 @@ static inline unsigned eq_blocks(uint64_t work) {
   return b < MLH_EQ_BLOCKS ? b : MLH_EQ_BLOCKS;
 }
 
+// One launch for the eq-factored sumcheck's setup (EqSetupArgs by value, so no
+// host-to-device copies): lo = eq(p_B..p_{L-1}) (2^a), the head suffix tables
+// H (2^B - 1, as eq_suffix_kernel over p_0..p_{B-1}), the tail suffix tables
+// Hs (2^a - 1, over p_B..p_{L-1}; optional); thread 0 also writes the points,
+// c_0 = 1 and (optional) the transcript state and the claim.
+__global__ void __launch_bounds__(256)
+eq_setup_kernel(const EqSetupArgs args, fe* __restrict__ pts_out, fe* __restrict__ c_out,
+                fe* __restrict__ lo, fe* __restrict__ H, fe* __restrict__ Hs, DevSha* dt_out,
+                fe* prev_out) {
+  const uint32_t L = args.L, B = args.B, a = L - B;
+  const uint64_t NL = 1ull << a, NH = (1ull << B) - 1, NS = Hs ? NL - 1 : 0;
+  uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x == 0) {
+    for (uint32_t i = 0; i < L; ++i) pts_out[i] = args.pts[i];
+    *c_out = fe_one();
+    if (dt_out) *dt_out = args.sha;
+    if (prev_out) *prev_out = args.sum;
+  }
+  // entry j of an eq suffix family over points q[0..n): the table of index k
+  // (2^(n-1-k) entries at offset 2^n - 2^(n-k)) = prod_{i < n-1-k} (bit_i(j) ?
+  // q[n-1-i] : 1 - q[n-1-i]); lo = the family's "k = -1" table (n factors)
+  const fe* q;
+  uint32_t n, cnt;
+  uint64_t j;
+  fe* out;
+  if (x < NL) {
+    q = args.pts + B; n = a; cnt = a; j = x; out = lo + x;
+  } else if ((x -= NL) < NH) {
+    const uint64_t y = (1ull << B) - x;
+    const uint32_t k = B - (64 - __builtin_clzll(y - 1));
+    q = args.pts; n = B; cnt = B - 1 - k; j = x - ((1ull << B) - (1ull << (B - k))); out = H + x;
+  } else if ((x -= NH) < NS) {
+    const uint64_t y = NL - x;
+    const uint32_t k = a - (64 - __builtin_clzll(y - 1));
+    q = args.pts + B; n = a; cnt = a - 1 - k; j = x - (NL - (NL >> k)); out = Hs + x;
+  } else {
+    return;
+  }
+  fe acc = fe_one();
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const fe p = q[n - 1 - i];
+    acc = fe_mul(acc, ((j >> i) & 1) ? p : fe_sub(fe_one(), p));
+  }
+  fe_store(out, acc);
+}
+
+hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* lo, fe* H, fe* Hs,
+                           DevSha* dt_out, fe* prev_out, hipStream_t st) {
+  if (args.L == 0 || args.L > 40 || args.B > args.L || args.L - args.B > kTailLogMax)
+    return hipErrorInvalidValue;
+  const uint64_t NL = 1ull << (args.L - args.B);
+  const uint64_t total = NL + (1ull << args.B) - 1 + (Hs ? NL - 1 : 0);
+  hipLaunchKernelGGL(eq_setup_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, args,
+                     pts_out, c_out, lo, H, Hs, dt_out, prev_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_eq_suffix(const fe* pts, uint32_t B, fe* H, hipStream_t st) {
   const uint64_t total = (1ull << B) - 1;
   if (total == 0) return hipSuccess;
@@ -563,47 +669,40 @@ static inline unsigned group_blocks(uint64_t work, uint32_t corners) {
 
 hipError_t launch_group_sums_eq(const fe* T, uint64_t S, uint32_t J, const fe* H, const fe* lo,
                                 uint32_t a, fe* partials, hipStream_t st, uint32_t* nb) {
-  if (J < 1 || J > 3 || a < 8 || (S >> J) < (1ull << a)) return hipErrorInvalidValue;
+  if (J < 1 || J > kMaxGroup || a < 8 || (S >> J) < (1ull << a)) return hipErrorInvalidValue;
   uint32_t nbc = group_blocks(S >> J, 1u << J);
   while ((uint64_t)nbc * kRedThreads < (1ull << a)) nbc *= 2;  // stride >= 2^a
+  if ((nbc << J) > 2 * kMaxRedBlocks) return hipErrorInvalidValue;
   *nb = nbc;
-  const dim3 g(nbc << J), b(kRedThreads);
-  if (J == 1) hipLaunchKernelGGL(group_sums_eq_kernel<1>, g, b, 0, st, T, S, H, lo, a, nbc, partials);
-  if (J == 2) hipLaunchKernelGGL(group_sums_eq_kernel<2>, g, b, 0, st, T, S, H, lo, a, nbc, partials);
-  if (J == 3) hipLaunchKernelGGL(group_sums_eq_kernel<3>, g, b, 0, st, T, S, H, lo, a, nbc, partials);
+  hipLaunchKernelGGL(group_sums_eq_kernel, dim3(nbc << J), dim3(kRedThreads), 0, st, T, S, J, H, lo,
+                     a, nbc, partials);
   return hipGetLastError();
-}
-
-template <int J>
-static void launch_fold_group_j(uint32_t JN, uint32_t nbc, hipStream_t st, const fe* Tin,
-                                uint64_t S, const fe* rs, fe* Tout, const fe* H, const fe* lo,
-                                uint32_t a, fe* partials) {
-  const dim3 g(nbc << JN), b(kRedThreads);
-  if (JN == 0)
-    hipLaunchKernelGGL((fold_group_eq_kernel<J, 0>), g, b, 0, st, Tin, S, rs, Tout, H, lo, a, nbc, partials);
-  if (JN == 1)
-    hipLaunchKernelGGL((fold_group_eq_kernel<J, 1>), g, b, 0, st, Tin, S, rs, Tout, H, lo, a, nbc, partials);
-  if (JN == 2)
-    hipLaunchKernelGGL((fold_group_eq_kernel<J, 2>), g, b, 0, st, Tin, S, rs, Tout, H, lo, a, nbc, partials);
-  if (JN == 3)
-    hipLaunchKernelGGL((fold_group_eq_kernel<J, 3>), g, b, 0, st, Tin, S, rs, Tout, H, lo, a, nbc, partials);
 }
 
 hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t JN, const fe* rs,
                                 fe* Tout, const fe* H, const fe* lo, uint32_t a, fe* partials,
                                 hipStream_t st, uint32_t* nb) {
-  if (J < 1 || J > 3 || JN > 3 || a < 8 || (S >> (J + JN)) < (1ull << a))
+  if (J < 1 || J > kMaxGroup || JN > kMaxGroup || a < 8 || (S >> (J + JN)) < (1ull << a))
     return hipErrorInvalidValue;
-  const uint64_t work = S >> (J + JN);  // per output corner
-  uint32_t nbc = (uint32_t)(work / kRedThreads < 1 ? 1 : work / kRedThreads);  // one output per thread
+#ifndef MLH_FOLD_SPLIT
+#define MLH_FOLD_SPLIT (1u << 16)  // outputs below which a J > 3 fold splits across lanes
+#endif
+  const bool split = J > 3 && (S >> J) < MLH_FOLD_SPLIT;
+  const uint32_t lanes = split ? 1u << (J - 3) : 1u;  // threads per output
+  const uint64_t work = (S >> (J + JN)) * lanes;      // threads per output corner
+  uint32_t nbc = (uint32_t)(work / kRedThreads < 1 ? 1 : work / kRedThreads);
   const uint32_t cap = (2 * kMaxRedBlocks) >> JN;
   if (nbc > cap) nbc = cap;
-  if (JN)
-    while ((uint64_t)nbc * kRedThreads < (1ull << a)) nbc *= 2;
   *nb = nbc;
-  if (J == 1) launch_fold_group_j<1>(JN, nbc, st, Tin, S, rs, Tout, H, lo, a, partials);
-  if (J == 2) launch_fold_group_j<2>(JN, nbc, st, Tin, S, rs, Tout, H, lo, a, partials);
-  if (J == 3) launch_fold_group_j<3>(JN, nbc, st, Tin, S, rs, Tout, H, lo, a, partials);
+  const dim3 g(nbc << JN), b(kRedThreads);
+#define MLH_FOLD_J(j, sp)                                                                   \
+  if (J == j && split == sp)                                                                \
+    hipLaunchKernelGGL((fold_group_eq_kernel<j, sp>), g, b, 0, st, Tin, S, JN, rs, Tout, H, lo, a, \
+                       nbc, partials);
+  MLH_FOLD_J(1, false) MLH_FOLD_J(2, false) MLH_FOLD_J(3, false)
+  MLH_FOLD_J(4, false) MLH_FOLD_J(5, false) MLH_FOLD_J(6, false)
+  MLH_FOLD_J(4, true) MLH_FOLD_J(5, true) MLH_FOLD_J(6, true)
+#undef MLH_FOLD_J
   return hipGetLastError();
 }
 
@@ -900,33 +999,34 @@ __device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_
 // p_k.., r_k.. (rs[u] for u < t0 were written by earlier launches of this
 // group).
 __global__ void __launch_bounds__(kRedThreads)
-sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, uint32_t t0,
-                      uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
+sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, uint32_t J2,
+                      uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
                       const fe* __restrict__ pts, fe* cdev) {
   __shared__ DevSha s;
   __shared__ uint32_t stage[8];
-  __shared__ fe slot[kRedThreads / 32];
+  __shared__ fe slot[64];
   MLH_TAIL_TS(0);
   if (threadIdx.x < sizeof(DevSha) / 4)
     reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
-  const uint32_t NC = 1u << J, G = kRedThreads >> J;  // threads per corner (>= 32)
+  const uint32_t JT = J + J2, NC = 1u << JT, G = kRedThreads >> JT;  // threads per corner
+  const uint32_t GW = G < 64 ? G : 64;                                // ... within one wave
   {
     const uint32_t c = threadIdx.x / G, j = threadIdx.x % G;
     fe acc = fe_zero();
 #pragma unroll 4
     for (uint32_t b = j; b < nb; b += G) acc = fe_add(acc, fe_load(partials + (uint64_t)c * nb + b));
     MLH_TAIL_TS(1);
-#pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) acc = fe_add(acc, shfl_xor_fe(acc, m));
-    if ((threadIdx.x & 31) == 0) slot[threadIdx.x >> 5] = acc;
+    for (uint32_t m = GW / 2; m >= 1; m >>= 1) acc = fe_add(acc, shfl_xor_fe(acc, m));
+    if (threadIdx.x % GW == 0) slot[threadIdx.x / GW] = acc;
   }
   __syncthreads();
   MLH_TAIL_TS(2);
   if (threadIdx.x >= 64) return;
-  const uint32_t lane = threadIdx.x;
-  fe X = fe_zero();
-  if (lane >= 8 && lane < 8 + NC)
-    for (uint32_t q = 0; q < G / 32; ++q) X = fe_add(X, slot[(lane - 8) * (G / 32) + q]);
+  const uint32_t lane = threadIdx.x, per = G / GW;  // slots per corner
+  // lane c < NC: the corner sum Y_c
+  fe Y = fe_zero();
+  if (lane < NC)
+    for (uint32_t q = 0; q < per; ++q) Y = fe_add(Y, slot[lane * per + q]);
   fe p[3], r[3];
 #pragma unroll
   for (uint32_t u = 0; u < 3; ++u) {
@@ -935,38 +1035,51 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
   }
   // lane 0: the claim; lane 1: the eq scale
   fe v = lane == 0 ? fe_load(prev) : (lane == 1 ? fe_load(cdev) : fe_zero());
-  eq_group_rounds(X, J, t0, t1, p, r, v, s, stage, polys, rs);
+  const fe one = fe_one();
+  // one group (J2 == 0): its corner sums; two chained groups over the corners
+  // c = (c_hi: J bits, c_lo: J2 bits): group 1's corner sums sum out c_lo with
+  // its eq weights, group 2's fold c_hi with group 1's challenges (see
+  // "grouped eq-factored rounds").  One loop body for both (code size: the
+  // one-lane transcript is instruction-fetch bound).
+  const uint32_t chi = lane >> J2, clo = lane & ((1u << J2) - 1);
+  for (uint32_t g = 0; g < (J2 ? 2u : 1u); ++g) {
+    const uint32_t Jg = g ? J2 : J;
+    fe x = Y;
+    if (J2) {
+      fe pr[3];  // the summed-out variables' factors: group 2's points / group 1's challenges
+      if (g == 0) {
+#pragma unroll
+        for (uint32_t u = 0; u < 3; ++u) pr[u] = u < J2 ? fe_load(pts + J + u) : fe_zero();
+      } else {
+#pragma unroll
+        for (uint32_t u = 0; u < 3; ++u) pr[u] = r[u];
+      }
+      const uint32_t nb_ = g ? J : J2, bits = g ? chi : clo;
+#pragma unroll
+      for (uint32_t u = 0; u < 3; ++u)
+        if (u < nb_) x = fe_mul(x, (bits >> (nb_ - 1 - u)) & 1u ? pr[u] : fe_sub(one, pr[u]));
+      const uint32_t m0 = g ? 1u << J2 : 1u, m1 = g ? NC : 1u << J2;
+      for (uint32_t m = m0; m < m1; m <<= 1) x = fe_add(x, shfl_xor_fe(x, m));
+      if (g == 1) {
+#pragma unroll
+        for (uint32_t u = 0; u < 3; ++u) {
+          p[u] = u < J2 ? fe_load(pts + J + u) : fe_zero();
+          r[u] = fe_zero();
+        }
+      }
+    }
+    // group g's corner sum X_c to lane 8 + c (group 1 of two: from lane c << J2)
+    const uint32_t src = (g == 0 && J2) ? ((lane - 8) << J2) : (lane - 8);
+    const fe X = shfl_fe(x, src & 63);
+    eq_group_rounds(lane >= 8 && lane < 8 + (1u << Jg) ? X : fe_zero(), Jg, g ? 0 : t0,
+                    g ? Jg : t1, p, r, v, s, stage, g ? polys + 2 * J : polys, g ? rs + J : rs);
+  }
   if (lane == 0) {
     *t = s;
     fe_store(prev, v);
   }
   if (lane == 1) fe_store(cdev, v);
   MLH_TAIL_TS(63);
-}
-
-// Fold of the 2^J corners src[c * stride] (c's MSB = the first variable)
-// with r[0..J-1]: the value at the folded table's entry.
-template <int J>
-__device__ __forceinline__ fe fold_corners(const fe* src, uint64_t stride, const fe* r) {
-  fe v[1 << J];
-#pragma unroll
-  for (int c = 0; c < (1 << J); ++c) v[c] = src[(uint64_t)c * stride];
-#pragma unroll
-  for (int u = 0; u < J; ++u) {
-    const int half = (1 << J) >> (u + 1);
-#pragma unroll
-    for (int c = 0; c < half; ++c) v[c] = lerp(v[c], v[c + half], r[u]);
-  }
-  return v[0];
-}
-__device__ __forceinline__ fe fold_corners_n(uint32_t J, const fe* src, uint64_t stride,
-                                             const fe* r) {
-  switch (J) {
-    case 0: return src[0];
-    case 1: return fold_corners<1>(src, stride, r);
-    case 2: return fold_corners<2>(src, stride, r);
-    default: return fold_corners<3>(src, stride, r);
-  }
 }
 
 // The last a rounds of an eq-factored sumcheck (mlh_sumcheck_prove_eq) in ONE
@@ -1211,13 +1324,14 @@ hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in,
   return hipGetLastError();
 }
 
-hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t t0,
-                                 uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
+hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t J2,
+                                 uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
                                  const fe* pts, fe* c, hipStream_t st) {
-  if (J < 1 || J > 3 || t0 >= t1 || t1 > J || nb == 0 || (nb << J) > 2 * kMaxRedBlocks)
+  if (J < 1 || J > 3 || J2 > 3 || t0 >= t1 || t1 > J || (J2 && (t0 != 0 || t1 != J)) || nb == 0 ||
+      (nb << (J + J2)) > 2 * kMaxRedBlocks)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(sumcheck_group_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, J, t0,
-                     t1, prev, t, polys, rs, pts, c);
+  hipLaunchKernelGGL(sumcheck_group_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, J, J2,
+                     t0, t1, prev, t, polys, rs, pts, c);
   return hipGetLastError();
 }
 

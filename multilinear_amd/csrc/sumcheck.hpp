@@ -4,10 +4,15 @@
 #include <stdint.h>
 
 #include "field.hpp"
+#include "transcript_dev.hpp"
 
 namespace mlh {
 
 constexpr uint32_t kMaxRedBlocks = 2048;  // partials buffer: 2 * kMaxRedBlocks elements
+#ifndef MLH_MAX_GROUP
+#define MLH_MAX_GROUP 6
+#endif
+constexpr uint32_t kMaxGroup = MLH_MAX_GROUP;  // eq-factored head rounds per HBM pass (3 + 3)
 
 // out[0] = s1, out[1] = s2 over tables of size 2h (device).
 hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* out,
@@ -20,7 +25,6 @@ hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* ou
                             const fe* m_src = nullptr);
 hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe* r_dev = nullptr,
                        const fe* m_src = nullptr);
-struct DevSha;
 // one sumcheck round on the device: reduce the nparts partial sum pairs,
 // interpolate, absorb, challenge, new claim
 // pk/c non-null: eq-factored round (partials are (E0, E1), see sums_eq_kernel;
@@ -39,7 +43,7 @@ hipError_t launch_fold_sums_eq(fe* m, uint64_t S, const fe* r_dev, const fe* H, 
                                uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts,
                                const fe* m_src = nullptr);
 // Grouped eq-factored head rounds (sumcheck.hip, "grouped eq-factored
-// rounds"): corner sums of a group of J <= 3 rounds over T (S entries, e from
+// rounds"): corner sums of a group of J <= 6 rounds over T (S entries, e from
 // H = H_{k+J-1}) into partials[corner * nb + block]; a J-level fold of T with
 // rs[0..J-1] into Tout (S / 2^J entries, may alias T) plus the corner sums of
 // the next group of JN rounds (JN = 0: fold only; H = that group's
@@ -50,8 +54,10 @@ hipError_t launch_group_sums_eq(const fe* T, uint64_t S, uint32_t J, const fe* H
 hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t JN, const fe* rs,
                                 fe* Tout, const fe* H, const fe* lo, uint32_t a, fe* partials,
                                 hipStream_t st, uint32_t* nb);
-hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t t0,
-                                 uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
+// J2 > 0: two chained groups (J then J2 rounds, all of them) from the
+// 2^(J+J2) corner sums of one pass.
+hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t J2,
+                                 uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
                                  const fe* pts, fe* c, hipStream_t st);
 // The last a <= 12 rounds of an eq-factored sumcheck in one LDS-resident
 // workgroup (sumcheck_eq_tail_kernel): table = Tin folded over Jin <= 3
@@ -61,6 +67,18 @@ hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, ui
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st);
+// Setup of the eq-factored sumcheck in one launch (arguments by value): the
+// points, c_0 = 1, lo = eq(p_B..p_{L-1}), head suffix tables H (over
+// p_0..p_{B-1}), tail suffix tables Hs (optional), transcript state and claim
+// (optional).  Requires L <= 40, L - B <= 12.
+struct EqSetupArgs {
+  fe pts[40];
+  fe sum;
+  DevSha sha;
+  uint32_t L, B;
+};
+hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* lo, fe* H, fe* Hs,
+                           DevSha* dt_out, fe* prev_out, hipStream_t st);
 // out[i] = (*c) * src[i]
 hipError_t launch_scale_dev(const fe* src, const fe* c, uint64_t n, fe* out, hipStream_t st);
 // Trace::evaluate: out[j] = sum_i eq[i] * m[i * width + j], j < width;

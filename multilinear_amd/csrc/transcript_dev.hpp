@@ -49,8 +49,10 @@ __device__ inline void dsha_compress_buf(DevSha& s) {
 
 // Word path when the fill and the length are multiples of 4 and p is
 // 4-byte aligned (every device absorb: roots, field elements); bytes
-// otherwise.  buf keeps memory byte order, exactly as HostSha256.
-__device__ inline void dsha_update(DevSha& s, const uint8_t* p, uint32_t n) {
+// otherwise.  buf keeps memory byte order, exactly as HostSha256.  Out of
+// line: the one-lane transcript kernels are instruction-fetch bound, and
+// unrolled copies of this rare path would evict the compression code.
+__device__ __noinline__ void dsha_update(DevSha& s, const uint8_t* p, uint32_t n) {
   if (((s.len | n | reinterpret_cast<uintptr_t>(p)) & 3) == 0) {
     uint32_t* bw = reinterpret_cast<uint32_t*>(s.buf);
     const uint32_t* pw = reinterpret_cast<const uint32_t*>(p);

@@ -20,7 +20,7 @@
 
 int main() {
   using namespace mlh;
-  const uint32_t J = 3, nb = 512, NP = nb << J;
+  const uint32_t J = 3, J2 = 3, nb = 64, NP = nb << (J + J2);
   std::vector<fe> hp(NP + 8);
   uint64_t x = 0x9E3779B97F4A7C15ull;
   auto next = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return (uint32_t)x; };
@@ -31,8 +31,8 @@ int main() {
   CHECK(hipMalloc(&pts, 8 * sizeof(fe)));
   CHECK(hipMalloc(&c, sizeof(fe)));
   CHECK(hipMalloc(&prev, sizeof(fe)));
-  CHECK(hipMalloc(&polys, 6 * sizeof(fe)));
-  CHECK(hipMalloc(&rs, 3 * sizeof(fe)));
+  CHECK(hipMalloc(&polys, 12 * sizeof(fe)));
+  CHECK(hipMalloc(&rs, 6 * sizeof(fe)));
   CHECK(hipMalloc(&t, sizeof(DevSha)));
   CHECK(hipMemcpy(parts, hp.data(), NP * sizeof(fe), hipMemcpyHostToDevice));
   CHECK(hipMemcpy(pts, hp.data() + NP, 8 * sizeof(fe), hipMemcpyHostToDevice));
@@ -47,7 +47,7 @@ int main() {
       CHECK(hipMemcpy(t, &hs, sizeof hs, hipMemcpyHostToDevice));
       CHECK(hipMemcpy(c, &one, sizeof one, hipMemcpyHostToDevice));
       CHECK(hipMemset(prev, 0, sizeof(fe)));
-      CHECK(launch_sumcheck_group(parts, nb, J, 0, J, prev, t, polys, rs, pts, c, nullptr));
+      CHECK(launch_sumcheck_group(parts, nb, J, J2, 0, J, prev, t, polys, rs, pts, c, nullptr));
       CHECK(hipDeviceSynchronize());
     }
     uint64_t ts[64];
