@@ -1370,6 +1370,7 @@ struct EqSumcheck {
   PoolBuf buf;
   fe *pts = nullptr, *c = nullptr, *lo = nullptr, *d = nullptr, *H = nullptr;
   fe* Hs = nullptr;  // eq suffix tables of the last a points (sumcheck_eq_tail_kernel)
+  uint32_t* kw = nullptr;  // padding-block K + W tables per round (init with a transcript)
   explicit EqSumcheck(mlh_ctx* c_) : ctx(c_), buf(c_) {}
 
   // matrix: round 0's table; work (2^(L-1) entries, optional) receives the
@@ -1385,14 +1386,15 @@ struct EqSumcheck {
     L = L_;
     a = L < kEqLo ? L : kEqLo;
     B = L - a;
-    // c | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1] | pts[L]
-    MLH_TRY(buf.alloc(16 * (1 + 3 * (1ull << a) + (1ull << B) + L)));
+    // c | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1] | pts[L] | kw[64 L words]
+    MLH_TRY(buf.alloc(16 * (1 + 3 * (1ull << a) + (1ull << B) + L + 16ull * L)));
     c = buf.as<fe>();
     lo = c + 1;
     d = B ? lo + (1ull << a) : lo;  // B == 0: delta is the whole eq table
     H = lo + 2 * (1ull << a);
     Hs = H + (1ull << B);
     pts = Hs + (1ull << a);
+    kw = sha ? reinterpret_cast<uint32_t*>(pts + L) : nullptr;
     EqSetupArgs args{};
     if (L) memcpy(args.pts, host_points, 16ull * L);
     if (sha) memcpy(&args.sha, sha, sizeof(DevSha));
@@ -1400,7 +1402,7 @@ struct EqSumcheck {
     args.L = L;
     args.B = B;
     HIP_TRY(ctx, launch_eq_setup(args, pts, c, lo, H, want_tail ? Hs : nullptr, dt_out, prev_out,
-                                 ctx->stream));
+                                 ctx->stream, kw));
     return MLH_OK;
   }
   const fe* Hk(uint32_t k) const { return H + ((1ull << B) - (1ull << (B - k))); }
@@ -1450,7 +1452,8 @@ struct EqSumcheck {
     for (;;) {
       const uint32_t J1 = JT < 3 ? JT : 3;
       HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, nb, J1, JT - J1, 0, J1, prev, dt,
-                                         polys + 2 * k, rs + k, pts + k, c, ctx->stream));
+                                         polys + 2 * k, rs + k, pts + k, c, ctx->stream,
+                                         kw ? kw + 64 * k : nullptr));
       const fe* in = k == 0 ? src : m;
       const uint64_t S = 1ull << (L - k);
       k += JT;
@@ -1511,7 +1514,7 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
   MLH_TRY(es.head_rounds(prev, dt, polys, rs));
   HIP_TRY(ctx, launch_sumcheck_eq_tail(es.B ? es.m : es.src, 0, nullptr, es.a, es.Hs,
                                        es.pts + es.B, es.c, prev, dt, polys + 2 * es.B, rs + es.B,
-                                       es.m, dfin, ctx->stream));
+                                       es.m, dfin, ctx->stream, es.kw ? es.kw + 64 * es.B : nullptr));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L + 16, hipMemcpyDeviceToHost,
                               ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -20,6 +20,7 @@
 // for F_M).  fold_sums fuses round k's fold with round k+1's sums: lane i reads
 // t[i], t[i+h/2], t[i+h], t[i+3h/2] and writes the two folded values, so each
 // round moves 2*S*16 B in and S*16 B out (the survey's 48 S bytes).
+#include "bfly_asm.hpp"
 #include "field.hpp"
 #include "sumcheck.hpp"
 #include "transcript_dev.hpp"
@@ -98,6 +99,27 @@ __device__ __forceinline__ fe lerp(const fe& lo, const fe& hi, const fe& r) {
   return fe_add(lo, fe_mul(r, fe_sub(hi, lo)));
 }
 
+// Throughput form of the product for the HBM-streaming kernels: the
+// generated hand-scheduled 128x128 product + special-form fold (bfly_asm.hpp,
+// kind "f": any a < 2^128, canonical b; 62 VALU, no per-MAC pads) and one
+// conditional subtraction back to canonical form.
+#ifndef MLH_SC_ASM_MUL
+#define MLH_SC_ASM_MUL 1
+#endif
+__device__ __forceinline__ fe fe_mul_s(const fe& a, const fe& b) {
+#if MLH_SC_ASM_MUL
+  fe x = a;
+  uint64_t rare;
+  bfly_f_v(x, b, rare);
+  return relaxed_canon(x);
+#else
+  return fe_mul(a, b);
+#endif
+}
+__device__ __forceinline__ fe lerp_s(const fe& lo, const fe& hi, const fe& r) {
+  return fe_add(lo, fe_mul_s(fe_sub(hi, lo), r));
+}
+
 // Fold of 2^J values in registers (index MSB = the first variable) with
 // r[0..J-1]; v[0] ends with the folded value.
 template <int J>
@@ -106,7 +128,7 @@ __device__ __forceinline__ void fold_regs(fe (&v)[1 << J], const fe* r) {
   for (int u = 0; u < J; ++u) {
     const int half = (1 << J) >> (u + 1);
 #pragma unroll
-    for (int c = 0; c < half; ++c) v[c] = lerp(v[c], v[c + half], r[u]);
+    for (int c = 0; c < half; ++c) v[c] = lerp_s(v[c], v[c + half], r[u]);
   }
 }
 // Fold of the 2^J corners src[c * stride] (c's MSB = the first variable) with
@@ -302,10 +324,10 @@ group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe*
   for (; i + stride < Q; i += 2 * stride) {  // two entries in flight per thread
     const fe h0 = fe_load(H + (i >> a)), h1 = fe_load(H + ((i + stride) >> a));
     const fe v0 = fe_load(Tc + i), v1 = fe_load(Tc + i + stride);
-    acc = fe_add(acc, fe_mul(v0, h0));
-    acc2 = fe_add(acc2, fe_mul(v1, h1));
+    acc = fe_add(acc, fe_mul_s(v0, h0));
+    acc2 = fe_add(acc2, fe_mul_s(v1, h1));
   }
-  if (i < Q) acc = fe_add(acc, fe_mul(fe_load(Tc + i), fe_load(H + (i >> a))));
+  if (i < Q) acc = fe_add(acc, fe_mul_s(fe_load(Tc + i), fe_load(H + (i >> a))));
   acc = fe_add(acc, acc2);
   if (i0 < Q) acc = fe_mul(acc, fe_load(lo + (i0 & ((1ull << a) - 1))));
   fe z = fe_zero();
@@ -345,14 +367,14 @@ fold_group_eq_kernel(const fe* Tin, uint64_t S, uint32_t JN, const fe* __restric
       const uint32_t m = 1u << (J2 - 1 - u);
       const fe o = shfl_xor_fe(v, m);
       const bool hi = l & m;
-      v = lerp(hi ? o : v, hi ? v : o, r[JH + u]);
+      v = lerp_s(hi ? o : v, hi ? v : o, r[JH + u]);
     }
     if (l == 0) {
       fe_store(Tout + x, v);
       // e(i) = H[i >> a] lo[i mod 2^a] in full: one output per 2^J inputs
       if (JN)
-        acc = fe_add(acc, fe_mul(v, fe_mul(fe_load(H + (i >> a)),
-                                           fe_load(lo + (i & ((1ull << a) - 1))))));
+        acc = fe_add(acc, fe_mul_s(v, fe_mul_s(fe_load(H + (i >> a)),
+                                               fe_load(lo + (i & ((1ull << a) - 1))))));
     }
   }
   if (JN) {
@@ -580,10 +602,18 @@ static inline unsigned eq_blocks(uint64_t work) {
 __global__ void __launch_bounds__(256)
 eq_setup_kernel(const EqSetupArgs args, fe* __restrict__ pts_out, fe* __restrict__ c_out,
                 fe* __restrict__ lo, fe* __restrict__ H, fe* __restrict__ Hs, DevSha* dt_out,
-                fe* prev_out) {
+                fe* prev_out, uint32_t* __restrict__ kw) {
   const uint32_t L = args.L, B = args.B, a = L - B;
   const uint64_t NL = 1ull << a, NH = (1ull << B) - 1, NS = Hs ? NL - 1 : 0;
   uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // kw: per round k whose absorb of (c1, c2) empties the buffer, the padding
+  // block's K + W table (the transcript then grows 32 bytes per round)
+  if (kw && x >= NL + NH + NS && x < NL + NH + NS + L) {
+    const uint32_t k = (uint32_t)(x - (NL + NH + NS));
+    const uint64_t len = args.sha.len + 32ull * (k + 1);
+    if ((len & 63) == 0) sha256_pad_kw(len, kw + 64 * k);
+    return;
+  }
   if (x == 0) {
     for (uint32_t i = 0; i < L; ++i) pts_out[i] = args.pts[i];
     *c_out = fe_one();
@@ -619,13 +649,13 @@ eq_setup_kernel(const EqSetupArgs args, fe* __restrict__ pts_out, fe* __restrict
 }
 
 hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* lo, fe* H, fe* Hs,
-                           DevSha* dt_out, fe* prev_out, hipStream_t st) {
+                           DevSha* dt_out, fe* prev_out, hipStream_t st, uint32_t* kw) {
   if (args.L == 0 || args.L > 40 || args.B > args.L || args.L - args.B > kTailLogMax)
     return hipErrorInvalidValue;
   const uint64_t NL = 1ull << (args.L - args.B);
-  const uint64_t total = NL + (1ull << args.B) - 1 + (Hs ? NL - 1 : 0);
+  const uint64_t total = NL + (1ull << args.B) - 1 + (Hs ? NL - 1 : 0) + (kw ? args.L : 0);
   hipLaunchKernelGGL(eq_setup_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, args,
-                     pts_out, c_out, lo, H, Hs, dt_out, prev_out);
+                     pts_out, c_out, lo, H, Hs, dt_out, prev_out, kw);
   return hipGetLastError();
 }
 
@@ -905,10 +935,13 @@ __device__ __forceinline__ fe shfl_fe(const fe& x, int src) {
 // step B (pqrst) = s1 = (c p) E1 on lane 0 and s2 = (c (3p - 1)) (2 E1 - E0) on
 // lane 1; lane 0 interpolates, absorbs and draws r.  p / r: the group's
 // points / challenges (r[u] for u < t0 known on entry; the rest filled in);
-// polys: round t0's slot; rs: round 0's r slot (lane 0 stores r_t at rs + t).
+// polys: round t0's slot; rs: round 0's r slot (lane 0 stores r_t at rs + t);
+// kw (or nullptr): per round t the padding-block K + W table at kw + 64 t
+// (eq_setup_kernel; used when round t's absorb leaves the buffer empty).
 __device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_t t0, uint32_t t1,
                                                 const fe (&p)[3], fe (&r)[3], fe& v, DevSha& s,
-                                                uint32_t* stage, fe* polys, fe* rs) {
+                                                uint32_t* stage, fe* polys, fe* rs,
+                                                const uint32_t* kw) {
   const uint32_t NC = 1u << J;
   const uint32_t lane = threadIdx.x & 63;
   const bool wl = lane >= 8 && lane < 8 + NC;  // corner-weight lane
@@ -979,7 +1012,7 @@ __device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_
       MLH_TAIL_TS(tb + 3);
       dsha_absorb<8>(s, w, stage);  // LE16(c1) || LE16(c2)
       MLH_TAIL_TS(tb + 4);
-      rr = dsha_challenge(s);
+      rr = dsha_challenge_kw(s, kw ? kw + 64 * tt : nullptr);
       MLH_TAIL_TS(tb + 5);
       fe_store(rs + tt, rr);
     }
@@ -1001,7 +1034,7 @@ __device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_
 __global__ void __launch_bounds__(kRedThreads)
 sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, uint32_t J2,
                       uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
-                      const fe* __restrict__ pts, fe* cdev) {
+                      const fe* __restrict__ pts, fe* cdev, const uint32_t* __restrict__ kw) {
   __shared__ DevSha s;
   __shared__ uint32_t stage[8];
   __shared__ fe slot[64];
@@ -1072,7 +1105,8 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
     const uint32_t src = (g == 0 && J2) ? ((lane - 8) << J2) : (lane - 8);
     const fe X = shfl_fe(x, src & 63);
     eq_group_rounds(lane >= 8 && lane < 8 + (1u << Jg) ? X : fe_zero(), Jg, g ? 0 : t0,
-                    g ? Jg : t1, p, r, v, s, stage, g ? polys + 2 * J : polys, g ? rs + J : rs);
+                    g ? Jg : t1, p, r, v, s, stage, g ? polys + 2 * J : polys, g ? rs + J : rs,
+                    kw ? (g ? kw + 64 * J : kw) : nullptr);
   }
   if (lane == 0) {
     *t = s;
@@ -1095,7 +1129,8 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
 __global__ void __launch_bounds__(kRedThreads)
 sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_in, uint32_t a,
                         const fe* __restrict__ ets, const fe* __restrict__ pts, fe* cdev, fe* prev,
-                        DevSha* t, fe* polys, fe* rs, fe* m_out, fe* d_out) {
+                        DevSha* t, fe* polys, fe* rs, fe* m_out, fe* d_out,
+                        const uint32_t* __restrict__ kw) {
   extern __shared__ fe eq_tail_lds[];
   fe* lm = eq_tail_lds;                 // 2^a
   fe* le = eq_tail_lds + (1u << a);     // 2^a - 1
@@ -1164,7 +1199,8 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
         p[u] = u < J ? fe_load(pts + j + u) : fe_zero();
         r[u] = fe_zero();
       }
-      eq_group_rounds(X, J, 0, J, p, r, v, s, stage, polys + 2 * j, rs + j);
+      eq_group_rounds(X, J, 0, J, p, r, v, s, stage, polys + 2 * j, rs + j,
+                      kw ? kw + 64 * j : nullptr);
       if (lane == 0) {
         r_sh[0] = r[0];
         r_sh[1] = r[1];
@@ -1316,22 +1352,23 @@ hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, 
 
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
-                                   fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st) {
+                                   fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
+                                   const uint32_t* kw) {
   if (a == 0 || a > kTailLogMax || Jin > 3) return hipErrorInvalidValue;
   const size_t lds = (2ull << a) * sizeof(fe);
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Tin, Jin, rs_in,
-                     a, ets, pts, c, prev, t, polys, rs, m_out, d_out);
+                     a, ets, pts, c, prev, t, polys, rs, m_out, d_out, kw);
   return hipGetLastError();
 }
 
 hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t J2,
                                  uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
-                                 const fe* pts, fe* c, hipStream_t st) {
+                                 const fe* pts, fe* c, hipStream_t st, const uint32_t* kw) {
   if (J < 1 || J > 3 || J2 > 3 || t0 >= t1 || t1 > J || (J2 && (t0 != 0 || t1 != J)) || nb == 0 ||
       (nb << (J + J2)) > 2 * kMaxRedBlocks)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(sumcheck_group_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, J, J2,
-                     t0, t1, prev, t, polys, rs, pts, c);
+                     t0, t1, prev, t, polys, rs, pts, c, kw);
   return hipGetLastError();
 }
 

@@ -56,9 +56,11 @@ hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t 
                                 hipStream_t st, uint32_t* nb);
 // J2 > 0: two chained groups (J then J2 rounds, all of them) from the
 // 2^(J+J2) corner sums of one pass.
+// kw (optional): the padding-block K + W tables of eq_setup (round t0's at kw).
 hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t J2,
                                  uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
-                                 const fe* pts, fe* c, hipStream_t st);
+                                 const fe* pts, fe* c, hipStream_t st,
+                                 const uint32_t* kw = nullptr);
 // The last a <= 12 rounds of an eq-factored sumcheck in one LDS-resident
 // workgroup (sumcheck_eq_tail_kernel): table = Tin folded over Jin <= 3
 // pending variables with rs_in (2^a entries after it), ets = eq suffix tables
@@ -66,7 +68,8 @@ hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, ui
 // outputs at polys + 2j, rs + j; m_out[0] / d_out[0] = the folded tables.
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
-                                   fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st);
+                                   fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
+                                   const uint32_t* kw = nullptr);
 // Setup of the eq-factored sumcheck in one launch (arguments by value): the
 // points, c_0 = 1, lo = eq(p_B..p_{L-1}), head suffix tables H (over
 // p_0..p_{B-1}), tail suffix tables Hs (optional), transcript state and claim
@@ -77,8 +80,11 @@ struct EqSetupArgs {
   DevSha sha;
   uint32_t L, B;
 };
+// kw (optional, 64 L words): per round k whose (c1, c2) absorb leaves the
+// transcript buffer empty (len + 32 (k + 1) = 0 mod 64), the padding block's
+// K + W table at kw + 64 k.
 hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* lo, fe* H, fe* Hs,
-                           DevSha* dt_out, fe* prev_out, hipStream_t st);
+                           DevSha* dt_out, fe* prev_out, hipStream_t st, uint32_t* kw = nullptr);
 // out[i] = (*c) * src[i]
 hipError_t launch_scale_dev(const fe* src, const fe* c, uint64_t n, fe* out, hipStream_t st);
 // Trace::evaluate: out[j] = sum_i eq[i] * m[i * width + j], j < width;

@@ -161,6 +161,72 @@ __device__ inline void dsha_digest(const DevSha& s0, uint8_t out[32]) {
   }
 }
 
+// K[t] + W[t] of the padding-only final block of a message of `len` bytes
+// (len % 64 == 0: 0x80, zeros, the bit length): the schedule depends on len
+// alone, so the transcript's challenge after a block-completing absorb can run
+// the round function only (sha256_compress_kw).
+__device__ inline void sha256_pad_kw(uint64_t len, uint32_t* kw) {
+  constexpr uint32_t K[64] = MLH_SHA_K;
+  uint32_t w[16] = {};
+  w[0] = 0x80000000u;
+  w[14] = (uint32_t)((len * 8) >> 32);
+  w[15] = (uint32_t)(len * 8);
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    uint32_t x;
+    if (t < 16) {
+      x = w[t];
+    } else {
+      const uint32_t a = w[(t - 15) & 15], b = w[(t - 2) & 15];
+      const uint32_t s0 = rotr(a, 7) ^ rotr(a, 18) ^ (a >> 3);
+      const uint32_t s1 = rotr(b, 17) ^ rotr(b, 19) ^ (b >> 10);
+      x = w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+    }
+    kw[t] = K[t] + x;
+  }
+}
+
+// One compression whose K[t] + W[t] come precomputed (a constant block).
+__device__ __forceinline__ void sha256_compress_kw(Sha256State& st, const uint32_t* __restrict__ kw) {
+  uint32_t k[64];
+#pragma unroll
+  for (int t = 0; t < 64; t += 4) {
+    const uint4 q = *reinterpret_cast<const uint4*>(kw + t);
+    k[t] = q.x;
+    k[t + 1] = q.y;
+    k[t + 2] = q.z;
+    k[t + 3] = q.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pin_vgpr(st.h[i]);
+  uint32_t a = st.h[0], b = st.h[1], c = st.h[2], d = st.h[3];
+  uint32_t e = st.h[4], f = st.h[5], g = st.h[6], h = st.h[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + k[t];
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t maj = maj3(a, b, c);
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + S0 + maj;
+  }
+  st.h[0] += a;
+  st.h[1] += b;
+  st.h[2] += c;
+  st.h[3] += d;
+  st.h[4] += e;
+  st.h[5] += f;
+  st.h[6] += g;
+  st.h[7] += h;
+}
+
 // Field128::from(u128) (field.rs:138-142): one conditional subtraction of M.
 // The u128 is LE over digest bytes 0..15, i.e. limb i = bswap(h[i]).
 __device__ inline fe dsha_challenge(const DevSha& s) {
@@ -168,6 +234,18 @@ __device__ inline fe dsha_challenge(const DevSha& s) {
   dsha_final(s, h);
   fe v;
   for (int i = 0; i < 4; ++i) v.w[i] = bswap32(h[i]);
+  return canon_with_carry(v, 0u);
+}
+
+// dsha_challenge with the padding-only block's K + W table for this length
+// (kw, or nullptr): used when the buffer is empty (len % 64 == 0).
+__device__ inline fe dsha_challenge_kw(const DevSha& s, const uint32_t* kw) {
+  if (!kw || (s.len & 63) != 0) return dsha_challenge(s);
+  Sha256State st;
+  for (int i = 0; i < 8; ++i) st.h[i] = s.h[i];
+  sha256_compress_kw(st, kw);
+  fe v;
+  for (int i = 0; i < 4; ++i) v.w[i] = bswap32(st.h[i]);
   return canon_with_carry(v, 0u);
 }
 
