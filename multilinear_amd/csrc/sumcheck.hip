@@ -916,7 +916,7 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
 // the claim p(r), the eq scale) run side by side on different lanes.
 __device__ __forceinline__ fe pqrst(const fe& P, const fe& Q, const fe& R, const fe& S,
                                     const fe& T) {
-  return fe_add(P, fe_mul(Q, fe_add(R, fe_mul(S, T))));
+  return fe_add(P, fe_mul_s(fe_add(R, fe_mul_s(S, T)), Q));
 }
 __device__ __forceinline__ fe shfl_fe(const fe& x, int src) {
   fe r;
@@ -1090,7 +1090,7 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
       const uint32_t nb_ = g ? J : J2, bits = g ? chi : clo;
 #pragma unroll
       for (uint32_t u = 0; u < 3; ++u)
-        if (u < nb_) x = fe_mul(x, (bits >> (nb_ - 1 - u)) & 1u ? pr[u] : fe_sub(one, pr[u]));
+        if (u < nb_) x = fe_mul_s(x, (bits >> (nb_ - 1 - u)) & 1u ? pr[u] : fe_sub(one, pr[u]));
       const uint32_t m0 = g ? 1u << J2 : 1u, m1 = g ? NC : 1u << J2;
       for (uint32_t m = m0; m < m1; m <<= 1) x = fe_add(x, shfl_xor_fe(x, m));
       if (g == 1) {
@@ -1182,7 +1182,7 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
     {  // corner sums of the group: 2^J corners x G threads
       const uint32_t c = threadIdx.x / G, jj = threadIdx.x % G;
       fe acc = fe_zero();
-      for (uint32_t i = jj; i < Q; i += G) acc = fe_add(acc, fe_mul(lm[c * Q + i], e[i]));
+      for (uint32_t i = jj; i < Q; i += G) acc = fe_add(acc, fe_mul_s(lm[c * Q + i], e[i]));
 #pragma unroll
       for (int m = 16; m >= 1; m >>= 1) acc = fe_add(acc, shfl_xor_fe(acc, m));
       if ((threadIdx.x & 31) == 0) slot[threadIdx.x >> 5] = acc;
