@@ -186,16 +186,23 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   // into LDS, then read the bit-reversed rows from there.
   if constexpr (LAST && ZT == 0) {
     constexpr int NT = kCols * R / EPT;
+    // (the staged tile's columns are XOR-swizzled by row: lanes 0..7 write 8
+    // consecutive rows of one column, which unswizzled sit 128 B apart on the
+    // same LDS banks; the reads take one row's 8 columns, a permutation either way)
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
       const uint32_t idx = (uint32_t)(e * NT + tid);
       const uint32_t l = idx & 63, grp = idx >> 6;
       const uint32_t row = grp * 8 + (l & 7), col = l >> 3;
-      lds[row * kCols + col] = fe_load(in + base + (uint64_t)col * cstride + row);
+      lds[row * kCols + (col ^ (row & (kCols - 1)))] =
+          fe_load(in + base + (uint64_t)col * cstride + row);
     }
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) x[e] = lds[bitrev((uint32_t)(t * EPT + e), LOGR) * kCols + c];
+    for (int e = 0; e < EPT; ++e) {
+      const uint32_t row = bitrev((uint32_t)(t * EPT + e), LOGR);
+      x[e] = lds[row * kCols + (c ^ (row & (kCols - 1)))];
+    }
   } else
 #endif
 #pragma unroll
