@@ -213,87 +213,11 @@ fold_kernel(fe* m, fe* __restrict__ d, uint64_t S, fe r, const fe* __restrict__ 
 //   s1 = c_k p_k E1,  s2 = c_k (3 p_k - 1)(2 E1 - E0),
 //   E0 = sum_{i<h} m[i] e(i),  E1 = sum_{i<h} m[i+h] e(i),
 // and e(i) = H_k[i >> a] * lo[i mod 2^a] (lo = eq of the last a points, H_k =
-// eq(p_{k+1}..p_{L-a-1})).  The kernels stream only m: half the HBM traffic of
-// the two-table rounds, and no 2^L eq table is ever written.  Thread counts are
-// powers of two >= 2^a, so a thread's i mod 2^a is fixed: it accumulates
-// m[i] * H[i >> a] and multiplies by lo once at the end (2 modmuls per pair).
-
-// H_k for k = 0..B-1 concatenated: H_k = eq(p_{k+1}, ..., p_{B-1}) has
-// 2^(B-1-k) entries at offset 2^B - 2^(B-k); entry j = prod_{i < B-1-k}
-// (bit_i(j) ? p[B-1-i] : 1 - p[B-1-i]).
-__global__ void eq_suffix_kernel(const fe* __restrict__ pts, uint32_t B, fe* __restrict__ out) {
-  const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t total = (1ull << B) - 1;
-  if (x >= total) return;
-  const uint64_t y = (1ull << B) - x;                  // >= 2
-  const uint32_t clog = 64 - __builtin_clzll(y - 1);   // ceil(log2 y)
-  const uint32_t k = B - clog;
-  const uint64_t j = x - ((1ull << B) - (1ull << (B - k)));
-  const uint32_t cnt = B - 1 - k;
-  fe acc = fe_one();
-  for (uint32_t i = 0; i < cnt; ++i) {
-    const fe p = pts[B - 1 - i];
-    acc = fe_mul(acc, ((j >> i) & 1) ? p : fe_sub(fe_one(), p));
-  }
-  fe_store(out + x, acc);
-}
-
-__global__ void __launch_bounds__(kRedThreads)
-sums_eq_kernel(const fe* __restrict__ m, uint64_t h, const fe* __restrict__ H,
-               const fe* __restrict__ lo, uint32_t a, fe* __restrict__ partials) {
-  fe e0 = fe_zero(), e1 = fe_zero();
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;  // power of two >= 2^a
-  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (uint64_t i = i0; i < h; i += stride) {
-    const fe hv = fe_load(H + (i >> a));
-    e0 = fe_add(e0, fe_mul(fe_load(m + i), hv));
-    e1 = fe_add(e1, fe_mul(fe_load(m + i + h), hv));
-  }
-  const fe l = fe_load(lo + (i0 & ((1ull << a) - 1)));
-  e0 = fe_mul(e0, l);
-  e1 = fe_mul(e1, l);
-  block_reduce2(e0, e1);
-  if (threadIdx.x == 0) {
-    fe_store(partials + 2 * blockIdx.x, e0);
-    fe_store(partials + 2 * blockIdx.x + 1, e1);
-  }
-}
-
-// fold m (size S) with r, then the eq-factored sums of the folded table
-// (h' = S/4, next round's H table).  msrc: the table folded (== m in place; a
-// separate source lets the first fold read the caller's evaluations without
-// the build_tables_for_pcs clone).
-__global__ void __launch_bounds__(kRedThreads)
-fold_sums_eq_kernel(fe* m, uint64_t S, const fe* __restrict__ rp, const fe* __restrict__ H,
-                    const fe* __restrict__ lo, uint32_t a, fe* __restrict__ partials,
-                    const fe* msrc) {
-  const fe r = fe_load(rp);
-  const uint64_t h = S / 2, q = S / 4;
-  fe e0 = fe_zero(), e1 = fe_zero();
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (uint64_t i = i0; i < q; i += stride) {
-    const fe ma = fe_load(msrc + i), mb = fe_load(msrc + i + q);
-    const fe mc = fe_load(msrc + i + h), md = fe_load(msrc + i + h + q);
-    const fe hv = fe_load(H + (i >> a));
-    const fe m0 = lerp(ma, mc, r), m1 = lerp(mb, md, r);
-    fe_store(m + i, m0);
-    fe_store(m + i + q, m1);
-    e0 = fe_add(e0, fe_mul(m0, hv));
-    e1 = fe_add(e1, fe_mul(m1, hv));
-  }
-  const fe l = fe_load(lo + (i0 & ((1ull << a) - 1)));
-  e0 = fe_mul(e0, l);
-  e1 = fe_mul(e1, l);
-  block_reduce2(e0, e1);
-  if (threadIdx.x == 0) {
-    fe_store(partials + 2 * blockIdx.x, e0);
-    fe_store(partials + 2 * blockIdx.x + 1, e1);
-  }
-}
+// eq(p_{k+1}..p_{L-a-1}), eq_setup_kernel).  The kernels stream only m: half
+// the HBM traffic of the two-table rounds, and no 2^L eq table is ever written.
 
 // ---- grouped eq-factored rounds ------------------------------------------------
-// A group of J <= 3 consecutive head rounds k..k+J-1 is served by ONE read of
+// A group of J consecutive head rounds k..k+J-1 is served by ONE read of
 // its table T (S entries): with Q = S / 2^J and the corner sums
 //   X_c = sum_{i<Q} T[c Q + i] e(i),  e = eq(p_{k+J}, ..., p_{L-1}) = H_{k+J-1}[i >> a] lo[..],
 // round k+t's eq-factored sums are the contraction
@@ -305,6 +229,8 @@ fold_sums_eq_kernel(fe* m, uint64_t S, const fe* __restrict__ rp, const fe* __re
 // E0/E1 equal the per-round kernels' exactly.  One 16-B read and one modmul per
 // element serve J rounds; the J folds are applied in one pass afterwards
 // (fold_group_eq_kernel), which also emits the next group's corner sums.
+// mlh_sumcheck_prove_eq takes 6 rounds per pass (64 corners, contracted as two
+// chained 3-round groups in sumcheck_group_kernel); the PCS 3-round groups.
 
 // corner sums X_c of a group of J rounds over T (S entries).  The grid is
 // 2^J corners x nbc blocks (block = c * nbc + bb, so partials[block] is
@@ -585,15 +511,6 @@ hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe*
   return hipGetLastError();
 }
 
-// thread count for the eq-factored kernels: a power of two >= 2^a (work >= 2^a)
-#ifndef MLH_EQ_BLOCKS
-#define MLH_EQ_BLOCKS 1024  // 2048 and 512 measured 1-2 % slower (tools/sumcheck_ab.py)
-#endif
-static inline unsigned eq_blocks(uint64_t work) {
-  const unsigned b = red_blocks(work);
-  return b < MLH_EQ_BLOCKS ? b : MLH_EQ_BLOCKS;
-}
-
 // One launch for the eq-factored sumcheck's setup (EqSetupArgs by value, so no
 // host-to-device copies): lo = eq(p_B..p_{L-1}) (2^a), the head suffix tables
 // H (2^B - 1, as eq_suffix_kernel over p_0..p_{B-1}), the tail suffix tables
@@ -656,34 +573,6 @@ hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* 
   const uint64_t total = NL + (1ull << args.B) - 1 + (Hs ? NL - 1 : 0) + (kw ? args.L : 0);
   hipLaunchKernelGGL(eq_setup_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, args,
                      pts_out, c_out, lo, H, Hs, dt_out, prev_out, kw);
-  return hipGetLastError();
-}
-
-hipError_t launch_eq_suffix(const fe* pts, uint32_t B, fe* H, hipStream_t st) {
-  const uint64_t total = (1ull << B) - 1;
-  if (total == 0) return hipSuccess;
-  hipLaunchKernelGGL(eq_suffix_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, pts,
-                     B, H);
-  return hipGetLastError();
-}
-
-hipError_t launch_sums_eq(const fe* m, uint64_t h, const fe* H, const fe* lo, uint32_t a,
-                          fe* partials, hipStream_t st, uint32_t* nparts) {
-  if (h < (1ull << a) || a < 8) return hipErrorInvalidValue;  // stride must be a multiple of 2^a
-  const unsigned nb = eq_blocks(h);
-  hipLaunchKernelGGL(sums_eq_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, h, H, lo, a, partials);
-  *nparts = nb;
-  return hipGetLastError();
-}
-
-hipError_t launch_fold_sums_eq(fe* m, uint64_t S, const fe* r_dev, const fe* H, const fe* lo,
-                               uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts,
-                               const fe* m_src) {
-  if (S / 4 < (1ull << a) || a < 8) return hipErrorInvalidValue;
-  const unsigned nb = eq_blocks(S / 4);
-  hipLaunchKernelGGL(fold_sums_eq_kernel, dim3(nb), dim3(kRedThreads), 0, st, m, S, r_dev, H, lo, a,
-                     partials, m_src ? m_src : m);
-  *nparts = nb;
   return hipGetLastError();
 }
 
@@ -857,45 +746,24 @@ __device__ __forceinline__ fe round_step(const fe& s1, const fe& s2, fe& claim, 
   claim = fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r))));
   return r;
 }
-// eq-factored round: (E0, E1) -> (s1, s2) = (c p E1, c (3p - 1)(2 E1 - E0))
-__device__ __forceinline__ void eq_round_sums(fe& s1, fe& s2, const fe& c, const fe& pv) {
-  const fe E0 = s1, E1 = s2;
-  const fe three_p_1 = fe_sub(fe_add(fe_dbl(pv), pv), fe_one());
-  s1 = fe_mul(fe_mul(c, pv), E1);
-  s2 = fe_mul(fe_mul(c, three_p_1), fe_sub(fe_dbl(E1), E0));
-}
-// c <- c ((1 - r)(1 - p) + r p) = c (1 - p - r + 2 r p)
-__device__ __forceinline__ fe eq_scale_next(const fe& c, const fe& pv, const fe& r) {
-  const fe f = fe_add(fe_sub(fe_sub(fe_one(), pv), r), fe_dbl(fe_mul(r, pv)));
-  return fe_mul(c, f);
-}
-
-// sums = (s1, s2) = p(1), p(2); prev = claimed sum = p(0) + p(1).  Closed-form
-// interpolation on x = 0,1,2 (polynomials.rs:51-87): e0 = prev - s1,
-// c2 = (s2 - 2 s1 + e0) / 2, c1 = s1 - e0 - c2; absorb LE16(c1), LE16(c2)
-// (sumcheck.rs:188-199), r = next_challenge(), prev = e0 + r (c1 + c2 r).
-// pk != null: eq-factored round (partials hold (E0, E1); s1 = c p_k E1,
-// s2 = c (3 p_k - 1)(2 E1 - E0)), and the scale advances to
-// c <- c ((1 - r)(1 - p_k) + r p_k) once r is known.
+// One two-table round (mlh_sumcheck_prove's per-round path, the PCS's rounds
+// after the eq-factored head, mlh_device_sumcheck_round): reduce the
+// per-workgroup partial (s1, s2) = p(1), p(2) pairs, then lane 0 runs
+// round_step (the closed-form interpolation on x = 0,1,2 of polynomials.rs:51-87,
+// absorb LE16(c1) || LE16(c2) as sumcheck.rs:188-199, r = next_challenge(),
+// claim = p(r)).
 __global__ void __launch_bounds__(kRedThreads)
 sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev, DevSha* t,
-                      fe* poly_out, fe* r_out, const fe* __restrict__ pk, fe* cdev) {
+                      fe* poly_out, fe* r_out) {
   __shared__ DevSha s;
   __shared__ uint32_t stage[8];
-  // the transcript state (one word per lane) and lane 0's scalars are loaded
-  // first, so their latency overlaps the partial-sum reduction
+  // the transcript state (one word per lane) and the claim are loaded first, so
+  // their latency overlaps the partial-sum reduction
   if (threadIdx.x < sizeof(DevSha) / 4)
     reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
-  fe p = fe_zero(), c = fe_zero(), pv = fe_zero();
-  if (threadIdx.x == 0) {
-    p = fe_load(prev);
-    if (pk) {
-      c = fe_load(cdev);
-      pv = fe_load(pk);
-    }
-  }
-  // the round sums: reduce the per-workgroup partials (loads unrolled so a
-  // lane's few loads are in flight together), then one lane runs the round
+  fe p = fe_zero();
+  if (threadIdx.x == 0) p = fe_load(prev);
+  // loads unrolled so a lane's few loads are in flight together
   fe s1 = fe_zero(), s2 = fe_zero();
 #pragma unroll 4
   for (uint32_t i = threadIdx.x; i < nparts; i += kRedThreads) {
@@ -904,11 +772,9 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
   }
   block_reduce2(s1, s2);  // (its barriers also publish the staged state)
   if (threadIdx.x != 0) return;
-  if (pk) eq_round_sums(s1, s2, c, pv);
-  const fe r = round_step(s1, s2, p, s, stage, poly_out, r_out);
+  round_step(s1, s2, p, s, stage, poly_out, r_out);
   *t = s;
   fe_store(prev, p);
-  if (pk) fe_store(cdev, eq_scale_next(c, pv, r));
 }
 
 // out = P + Q (R + S T): the one two-modmul form every lane-parallel step of
@@ -1344,9 +1210,9 @@ hipError_t launch_sumcheck_tail(fe* m, fe* d, uint32_t log_s, fe* prev, DevSha* 
 }
 
 hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, DevSha* t,
-                                 fe* poly_out, fe* r_out, hipStream_t st, const fe* pk, fe* c) {
+                                 fe* poly_out, fe* r_out, hipStream_t st) {
   hipLaunchKernelGGL(sumcheck_round_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nparts,
-                     prev, t, poly_out, r_out, pk, c);
+                     prev, t, poly_out, r_out);
   return hipGetLastError();
 }
 

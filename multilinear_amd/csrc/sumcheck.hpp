@@ -25,23 +25,10 @@ hipError_t launch_fold_sums(fe* m, fe* d, uint64_t S, fe r, fe* partials, fe* ou
                             const fe* m_src = nullptr);
 hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe* r_dev = nullptr,
                        const fe* m_src = nullptr);
-// one sumcheck round on the device: reduce the nparts partial sum pairs,
-// interpolate, absorb, challenge, new claim
-// pk/c non-null: eq-factored round (partials are (E0, E1), see sums_eq_kernel;
-// *c is the running eq scale, advanced with r)
+// one two-table sumcheck round on the device: reduce the nparts partial sum
+// pairs, interpolate, absorb, challenge, new claim
 hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, DevSha* t,
-                                 fe* poly_out, fe* r_out, hipStream_t st,
-                                 const fe* pk = nullptr, fe* c = nullptr);
-// eq-factored sumcheck (delta = c_k eq(p_k..p_{L-1}) never materialised):
-// H_k tables for k < B (concatenated, H_k at offset 2^B - 2^(B-k)); sums of
-// round k over m (h = half size) with e(i) = H_k[i >> a] lo[i mod 2^a]; fold
-// with r (HBM) + the next round's sums.  Require half sizes >= 2^a, a >= 8.
-hipError_t launch_eq_suffix(const fe* pts, uint32_t B, fe* H, hipStream_t st);
-hipError_t launch_sums_eq(const fe* m, uint64_t h, const fe* H, const fe* lo, uint32_t a,
-                          fe* partials, hipStream_t st, uint32_t* nparts);
-hipError_t launch_fold_sums_eq(fe* m, uint64_t S, const fe* r_dev, const fe* H, const fe* lo,
-                               uint32_t a, fe* partials, hipStream_t st, uint32_t* nparts,
-                               const fe* m_src = nullptr);
+                                 fe* poly_out, fe* r_out, hipStream_t st);
 // Grouped eq-factored head rounds (sumcheck.hip, "grouped eq-factored
 // rounds"): corner sums of a group of J <= 6 rounds over T (S entries, e from
 // H = H_{k+J-1}) into partials[corner * nb + block]; a J-level fold of T with
@@ -64,7 +51,7 @@ hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, ui
 // The last a <= 12 rounds of an eq-factored sumcheck in one LDS-resident
 // workgroup (sumcheck_eq_tail_kernel): table = Tin folded over Jin <= 3
 // pending variables with rs_in (2^a entries after it), ets = eq suffix tables
-// of pts (launch_eq_suffix(pts, a)), c = the running eq scale; round j's
+// of pts (eq_setup_kernel's Hs), c = the running eq scale; round j's
 // outputs at polys + 2j, rs + j; m_out[0] / d_out[0] = the folded tables.
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,

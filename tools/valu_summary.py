@@ -22,7 +22,7 @@ NOMINAL = 7.864e13
 def main():
     tag, d = sys.argv[1], sys.argv[2]
     want = sys.argv[3:] or ["ntt_pass", "level2", "leaf_pairs", "fri_fold_leaves", "top_kernel",
-                            "fold_sums", "shard_dft", "mobius", "sums_eq", "subtree"]
+                            "fold_sums", "shard_dft", "mobius", "group_sums", "fold_group", "sumcheck_", "subtree"]
     ctr = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
         ctr[r["Kernel_Name"]][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
