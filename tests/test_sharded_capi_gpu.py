@@ -2,7 +2,8 @@
 
 * 2 and 4 real processes sharing the one GPU, exchanges through
   sharded.HostTransport (torch.distributed gloo as C callbacks): the sharded
-  NTT / INTT / RS outputs reassemble to the single-GPU transforms, the sharded
+  NTT / INTT / RS outputs reassemble to the single-GPU transforms and to the C
+  oracle's (oracle/c/oracle.c: ntt / reed_solomon), the sharded
   FRI proof equals the single-GPU mlh_fri_prove proof byte for byte (and
   verifies), the sharded eq table + sumcheck give the single-GPU round
   polynomials and challenges.
@@ -25,6 +26,7 @@ pytestmark = pytest.mark.gpu
 from multilinear_amd import device as DV  # noqa: E402
 from multilinear_amd import dist as D  # noqa: E402
 from multilinear_amd import sharded as S  # noqa: E402
+from oracle import coracle as C  # noqa: E402  (checker only)
 
 
 def _free_port():
@@ -122,6 +124,14 @@ def test_sharded_capi_multiprocess(world, cfg):
         assert "error" not in res[r], res[r].get("error")
     ref = res[0].pop("ref")
     ln, lc = cfg["log_ntt"], cfg["log_code"]
+    # the single-GPU references are themselves checked against the C oracle on
+    # the same inputs (worker seeds 31 / 11)
+    from multilinear_amd import ntt as MN
+
+    x = DV.random_limbs(1 << ln, seed=31)
+    assert (C.ntt(x, ln, MN.pow_2_generator(ln)) == ref["ntt"]).all()
+    coeffs = DV.random_limbs(1 << (lc - 1), seed=11)
+    assert (C.reed_solomon(coeffs, lc - 1, MN.pow_2_generator(lc)) == ref["code"]).all()
     parts = [np.frombuffer(res[r]["ntt"], dtype=np.uint32).reshape(-1, 4) for r in range(world)]
     assert (D.unshard_blocks(parts, ln - 2 * (world.bit_length() - 1)) == ref["ntt"]).all()
     parts = [np.frombuffer(res[r]["code"], dtype=np.uint32).reshape(-1, 4) for r in range(world)]
