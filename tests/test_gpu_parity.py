@@ -437,6 +437,33 @@ def test_sumcheck_prove_matches_oracle(n, factored):
     assert host(evd) == ev  # build_tables_for_pcs clones: the evaluations are untouched
 
 
+@pytest.mark.parametrize("label", [b"abc", b"x" * 33, b""])
+@pytest.mark.parametrize("n", [3, 14, 18])
+def test_sumcheck_prove_eq_transcript_alignments(n, label):
+    """The device transcript's word path needs len % 4 == 0; a 3- or 33-byte
+    prefix sends every absorb of the prove (head groups, eq tail) through the
+    byte path, and an empty one makes every other challenge a padding-only
+    block (the precomputed K + W tables).  Round polynomials, challenges and the
+    final transcript state vs the oracle."""
+    ev = rand_vals(1 << n, 90 + n)
+    pts = rand_vals(n, 91 + n)
+    total = OPL.mle_evaluate(ev, pts)
+    ot = OS.SumcheckTables.build_tables_for_pcs(pts, ev)
+    otr = OT.Transcript()
+    otr.absorb(label)
+    prev, want_polys, want_rs = total, [], []
+    for _ in range(n):
+        nz, r2, prev = ot.compute_sumcheck_polynomial(prev, otr)
+        want_polys.append(tuple(nz))
+        want_rs.append(r2)
+    mt = MS.SumcheckTables.build_tables_for_pcs(pts, dev(ev))
+    tr = Transcript()
+    tr.absorb(label)
+    polys, rs = mt.compute_sumcheck_polynomials(total, tr)
+    assert polys == want_polys and rs == want_rs
+    assert tr.random() == otr.random()
+
+
 @pytest.mark.parametrize("n", [1, 2, 8, 10, 13, 14, 16, 17])
 def test_pcs_prove_matches_oracle(n):
     """multilinear_pcs_bench_test pattern: evals 7i+3, point (0..n)."""
