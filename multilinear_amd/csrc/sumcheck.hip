@@ -784,6 +784,31 @@ __device__ __forceinline__ fe pqrst(const fe& P, const fe& Q, const fe& R, const
                                     const fe& T) {
   return fe_add(P, fe_mul_s(fe_add(R, fe_mul_s(S, T)), Q));
 }
+// The same lane's value as a wave-uniform (v_readlane): no LDS round trip.
+__device__ __forceinline__ fe bcast_fe(const fe& x, int src) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.w[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.w[i], src);
+  return r;
+}
+// x from the lane at the given DPP pattern (quad_perm / row_half_mirror).
+template <int CTRL>
+__device__ __forceinline__ fe dpp_fe(const fe& x) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    r.w[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.w[i], CTRL, 0xF, 0xF, true);
+  return r;
+}
+// Sum over each aligned group of n (2, 4 or 8) lanes, every lane of the group
+// ending with it: DPP butterflies (xor 1, xor 2 quad_perms, then the mirror
+// within 8 lanes, which pairs the two summed quads), no LDS crossbar.
+__device__ __forceinline__ fe group_sum_dpp(fe x, uint32_t n) {
+  if (n > 1) x = fe_add(x, dpp_fe<0xB1>(x));   // quad_perm [1,0,3,2]
+  if (n > 2) x = fe_add(x, dpp_fe<0x4E>(x));   // quad_perm [2,3,0,1]
+  if (n > 4) x = fe_add(x, dpp_fe<0x141>(x));  // row_half_mirror
+  return x;
+}
 __device__ __forceinline__ fe shfl_fe(const fe& x, int src) {
   fe r;
 #pragma unroll
@@ -852,18 +877,16 @@ __device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_
       if (u == tt) pv = p[u];
     const bool bt = (cl >> (J - 1 - tt)) & 1u;
     fe E0 = wl && !bt ? v : fe_zero(), E1 = wl && bt ? v : fe_zero();
-    for (uint32_t m = 1; m < NC; m <<= 1) {
-      E0 = fe_add(E0, shfl_xor_fe(E0, m));
-      E1 = fe_add(E1, shfl_xor_fe(E1, m));
-    }
+    E0 = group_sum_dpp(E0, NC);  // corner lanes 8..8+NC: an aligned group
+    E1 = group_sum_dpp(E1, NC);
     MLH_TAIL_TS(tb + 1);
     // step B: lane 0 s1 = E1 (c p), lane 1 s2 = (2 E1 - E0)(c (3p - 1))
-    E0 = shfl_fe(E0, 8);
-    E1 = shfl_fe(E1, 8);
-    const fe cs = shfl_fe(v, 1);
+    E0 = bcast_fe(E0, 8);
+    E1 = bcast_fe(E1, 8);
+    const fe cs = bcast_fe(v, 1);
     const fe sB = pqrst(fe_zero(), lane == 0 ? E1 : fe_sub(fe_dbl(E1), E0), fe_zero(), cs,
                         lane == 0 ? pv : fe_sub(fe_add(fe_dbl(pv), pv), one));
-    const fe s2 = shfl_fe(sB, 1);
+    const fe s2 = bcast_fe(sB, 1);
     MLH_TAIL_TS(tb + 2);
     fe rr = fe_zero();
     if (lane == 0) {
@@ -882,7 +905,7 @@ __device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_
       MLH_TAIL_TS(tb + 5);
       fe_store(rs + tt, rr);
     }
-    rr = shfl_fe(rr, 0);
+    rr = bcast_fe(rr, 0);
 #pragma unroll
     for (uint32_t u = 0; u < 3; ++u)
       if (u == tt) r[u] = rr;
