@@ -1371,6 +1371,7 @@ struct EqSumcheck {
   fe *pts = nullptr, *c = nullptr, *lo = nullptr, *d = nullptr, *H = nullptr;
   fe* Hs = nullptr;  // eq suffix tables of the last a points (sumcheck_eq_tail_kernel)
   uint32_t* kw = nullptr;  // padding-block K + W tables per round (init with a transcript)
+  fe* wts = nullptr;       // eq weights of the last finished group's challenges (its fold)
   explicit EqSumcheck(mlh_ctx* c_) : ctx(c_), buf(c_) {}
 
   // matrix: round 0's table; work (2^(L-1) entries, optional) receives the
@@ -1386,8 +1387,8 @@ struct EqSumcheck {
     L = L_;
     a = L < kEqLo ? L : kEqLo;
     B = L - a;
-    // c | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1] | pts[L] | kw[64 L words]
-    MLH_TRY(buf.alloc(16 * (1 + 3 * (1ull << a) + (1ull << B) + L + 16ull * L)));
+    // c | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1] | pts[L] | kw[64 L words] | wts[64]
+    MLH_TRY(buf.alloc(16 * (1 + 3 * (1ull << a) + (1ull << B) + L + 16ull * L + 64)));
     c = buf.as<fe>();
     lo = c + 1;
     d = B ? lo + (1ull << a) : lo;  // B == 0: delta is the whole eq table
@@ -1395,6 +1396,7 @@ struct EqSumcheck {
     Hs = H + (1ull << B);
     pts = Hs + (1ull << a);
     kw = sha ? reinterpret_cast<uint32_t*>(pts + L) : nullptr;
+    wts = pts + L + 16ull * L;
     EqSetupArgs args{};
     if (L) memcpy(args.pts, host_points, 16ull * L);
     if (sha) memcpy(&args.sha, sha, sizeof(DevSha));
@@ -1434,7 +1436,7 @@ struct EqSumcheck {
     if (k < B) {
       const uint32_t t = k - gk;
       HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, gnb, gJ, 0, t, t + 1, prev, dt, poly, r - t,
-                                         pts + gk, c, ctx->stream));
+                                         pts + gk, c, ctx->stream, nullptr, wts));
     } else {
       HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, prev, dt, poly, r, ctx->stream));
     }
@@ -1453,13 +1455,14 @@ struct EqSumcheck {
       const uint32_t J1 = JT < 3 ? JT : 3;
       HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, nb, J1, JT - J1, 0, J1, prev, dt,
                                          polys + 2 * k, rs + k, pts + k, c, ctx->stream,
-                                         kw ? kw + 64 * k : nullptr));
+                                         kw ? kw + 64 * k : nullptr, wts));
       const fe* in = k == 0 ? src : m;
       const uint64_t S = 1ull << (L - k);
       k += JT;
       const uint32_t JN = B - k < kMaxGroup ? B - k : kMaxGroup;
-      HIP_TRY(ctx, launch_fold_group_eq(in, S, JT, JN, rs + k - JT, m, JN ? Hk(k + JN - 1) : nullptr,
-                                        lo, a, ctx->partials, ctx->stream, &nb));
+      HIP_TRY(ctx, launch_fold_group_eq(in, S, JT, JN, rs + k - JT, wts, m,
+                                        JN ? Hk(k + JN - 1) : nullptr, lo, a, ctx->partials,
+                                        ctx->stream, &nb));
       if (!JN) return MLH_OK;
       JT = JN;
     }
@@ -1472,7 +1475,7 @@ struct EqSumcheck {
       if (k + 1 < gk + gJ) return MLH_OK;  // mid-group: nothing to fold yet
       const fe* in = gk == 0 ? src : m;
       const uint32_t JN = group_len(k + 1);
-      HIP_TRY(ctx, launch_fold_group_eq(in, 1ull << (L - gk), gJ, JN, r_dev - (gJ - 1), m,
+      HIP_TRY(ctx, launch_fold_group_eq(in, 1ull << (L - gk), gJ, JN, r_dev - (gJ - 1), wts, m,
                                         JN ? Hk(k + JN) : nullptr, lo, a, ctx->partials,
                                         ctx->stream, &gnb));
       if (JN) {

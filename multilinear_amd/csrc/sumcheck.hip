@@ -120,6 +120,42 @@ __device__ __forceinline__ fe lerp_s(const fe& lo, const fe& hi, const fe& r) {
   return fe_add(lo, fe_mul_s(fe_sub(hi, lo), r));
 }
 
+// Lazy accumulation for the streaming sums: acc (9 limbs) += a b unreduced.
+// Operand scanning: row i's product a_i b_j takes acc[i+j] + carry as its
+// 64-bit addend, which cannot overflow ((2^32-1)^2 + 2 (2^32-1) = 2^64 - 1),
+// so no carry-out is needed inside a row (16 mads, ~52 VALU per product
+// against ~85 for a reduced product plus a modular add).
+struct acc9 {
+  uint32_t w[9];
+};
+__device__ __forceinline__ void acc_zero(acc9& a) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) a.w[i] = 0;
+}
+__device__ __forceinline__ void mulacc(acc9& acc, const fe& a, const fe& b) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t t = (uint64_t)a.w[i] * b.w[j] + ((uint64_t)acc.w[i + j] + carry);
+      acc.w[i + j] = (uint32_t)t;
+      carry = (uint32_t)(t >> 32);
+    }
+    uint32_t k;
+    acc.w[i + 4] = __builtin_addc(acc.w[i + 4], carry, 0u, &k);
+#pragma unroll
+    for (int j = i + 5; j < 9; ++j) acc.w[j] = __builtin_addc(acc.w[j], 0u, k, &k);
+  }
+}
+// Canonical value of an accumulator (< 2^288): the low 256 bits reduced, plus
+// the top limb times 2^256 mod M = C^2 (< 2^91).
+__device__ __forceinline__ fe acc_reduce(const acc9& a) {
+  const fe lo = reduce_wide(a.w);
+  const fe k256{{0x00000001u, 0xFFFFA600u, 0x07E8FFFFu, 0u}};
+  return fe_add(lo, fe_mul_s(fe{{a.w[8], 0u, 0u, 0u}}, k256));
+}
+
 // Fold of 2^J values in registers (index MSB = the first variable) with
 // r[0..J-1]; v[0] ends with the folded value.
 template <int J>
@@ -243,19 +279,21 @@ group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe*
   const uint64_t Q = S >> J;
   const uint32_t c = blockIdx.x / nbc, bb = blockIdx.x % nbc;
   const fe* Tc = T + (uint64_t)c * Q;
-  fe acc = fe_zero(), acc2 = fe_zero();
+  acc9 s0, s1;  // unreduced (two for ILP); < 2^288 for < 2^32 products each
+  acc_zero(s0);
+  acc_zero(s1);
   const uint64_t stride = (uint64_t)nbc * blockDim.x;
   const uint64_t i0 = (uint64_t)bb * blockDim.x + threadIdx.x;
   uint64_t i = i0;
   for (; i + stride < Q; i += 2 * stride) {  // two entries in flight per thread
     const fe h0 = fe_load(H + (i >> a)), h1 = fe_load(H + ((i + stride) >> a));
     const fe v0 = fe_load(Tc + i), v1 = fe_load(Tc + i + stride);
-    acc = fe_add(acc, fe_mul_s(v0, h0));
-    acc2 = fe_add(acc2, fe_mul_s(v1, h1));
+    mulacc(s0, v0, h0);
+    mulacc(s1, v1, h1);
   }
-  if (i < Q) acc = fe_add(acc, fe_mul_s(fe_load(Tc + i), fe_load(H + (i >> a))));
-  acc = fe_add(acc, acc2);
-  if (i0 < Q) acc = fe_mul(acc, fe_load(lo + (i0 & ((1ull << a) - 1))));
+  if (i < Q) mulacc(s0, fe_load(Tc + i), fe_load(H + (i >> a)));
+  fe acc = fe_add(acc_reduce(s0), acc_reduce(s1));
+  if (i0 < Q) acc = fe_mul_s(acc, fe_load(lo + (i0 & ((1ull << a) - 1))));
   fe z = fe_zero();
   block_reduce2(acc, z);
   if (threadIdx.x == 0) fe_store(partials + blockIdx.x, acc);
@@ -268,32 +306,59 @@ group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe*
 // as group_sums_eq_kernel, but the eq weight applied per output: any stride).
 template <int J, bool SPLIT>
 __global__ void __launch_bounds__(kRedThreads)
-fold_group_eq_kernel(const fe* Tin, uint64_t S, uint32_t JN, const fe* __restrict__ rs, fe* Tout,
-                     const fe* __restrict__ H, const fe* __restrict__ lo, uint32_t a,
-                     uint32_t nbc, fe* __restrict__ partials) {
+fold_group_eq_kernel(const fe* Tin, uint64_t S, uint32_t JN, const fe* __restrict__ rs,
+                     const fe* __restrict__ w, fe* Tout, const fe* __restrict__ H,
+                     const fe* __restrict__ lo, uint32_t a, uint32_t nbc,
+                     fe* __restrict__ partials) {
+  // !SPLIT: the folded entry is the eq-weighted sum of its 2^J corners,
+  //   Tout[x] = sum_c w_c Tin[c Sp + x],  w_c = prod_u (c_u ? r_u : 1 - r_u)
+  // (the same field value as J rounds of lerps), accumulated unreduced with the
+  // weights (sumcheck_group_kernel's output) broadcast from LDS.
   // SPLIT (J > 3, few outputs): 2^(J-3) lanes per output, lane l folds the 8
-  // corners (c_hi, l) over the top 3 variables, then shuffle-lerps combine the
-  // lanes over the rest (more loads in flight; without it a thread's 2^J loads
-  // go 8 at a time, and every load instruction stays one 1 KiB run)
+  // corners (c_hi, l) over the top 3 variables by lerps, then shuffle-lerps
+  // combine the lanes over the rest (more loads in flight per output).
   constexpr int J2 = SPLIT && J > 3 ? J - 3 : 0, JH = J - J2;
   const uint64_t Sp = S >> J, Qp = Sp >> JN;
   const uint32_t co = blockIdx.x / nbc, bb = blockIdx.x % nbc;
   const uint32_t l = threadIdx.x & ((1u << J2) - 1);
-  fe r[J];
+  __shared__ fe wsh[SPLIT ? 1 : 1 << J];
+  fe r[SPLIT ? J : 1];
+  if constexpr (SPLIT) {
 #pragma unroll
-  for (int u = 0; u < J; ++u) r[u] = fe_load(rs + u);
+    for (int u = 0; u < J; ++u) r[u] = fe_load(rs + u);
+  } else {
+    if (threadIdx.x < (1u << J)) wsh[threadIdx.x] = fe_load(w + threadIdx.x);
+    __syncthreads();
+  }
   fe acc = fe_zero();
   const uint64_t stride = ((uint64_t)nbc * blockDim.x) >> J2;
   const uint64_t i0 = ((uint64_t)bb * blockDim.x + threadIdx.x) >> J2;
   for (uint64_t i = i0; i < Qp; i += stride) {
     const uint64_t x = (uint64_t)co * Qp + i;
-    fe v = fold_corners<JH>(Tin + (uint64_t)l * Sp + x, Sp << J2, r);
+    fe v;
+    if constexpr (SPLIT) {
+      v = fold_corners<JH>(Tin + (uint64_t)l * Sp + x, Sp << J2, r);
 #pragma unroll
-    for (int u = 0; u < J2; ++u) {
-      const uint32_t m = 1u << (J2 - 1 - u);
-      const fe o = shfl_xor_fe(v, m);
-      const bool hi = l & m;
-      v = lerp_s(hi ? o : v, hi ? v : o, r[JH + u]);
+      for (int u = 0; u < J2; ++u) {
+        const uint32_t m = 1u << (J2 - 1 - u);
+        const fe o = shfl_xor_fe(v, m);
+        const bool hi = l & m;
+        v = lerp_s(hi ? o : v, hi ? v : o, r[JH + u]);
+      }
+    } else {
+      acc9 t;
+      acc_zero(t);
+#pragma unroll
+      for (int c0 = 0; c0 < (1 << J); c0 += 8) {  // 8 loads in flight at a time
+        fe tv[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (c0 + c < (1 << J)) tv[c] = fe_load(Tin + (uint64_t)(c0 + c) * Sp + x);
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (c0 + c < (1 << J)) mulacc(t, tv[c], wsh[c0 + c]);
+      }
+      v = acc_reduce(t);
     }
     if (l == 0) {
       fe_store(Tout + x, v);
@@ -599,9 +664,9 @@ hipError_t launch_group_sums_eq(const fe* T, uint64_t S, uint32_t J, const fe* H
 }
 
 hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t JN, const fe* rs,
-                                fe* Tout, const fe* H, const fe* lo, uint32_t a, fe* partials,
-                                hipStream_t st, uint32_t* nb) {
-  if (J < 1 || J > kMaxGroup || JN > kMaxGroup || a < 8 || (S >> (J + JN)) < (1ull << a))
+                                const fe* w, fe* Tout, const fe* H, const fe* lo, uint32_t a,
+                                fe* partials, hipStream_t st, uint32_t* nb) {
+  if (J < 1 || J > kMaxGroup || JN > kMaxGroup || a < 8 || (S >> (J + JN)) < (1ull << a) || !w)
     return hipErrorInvalidValue;
 #ifndef MLH_FOLD_SPLIT
 #define MLH_FOLD_SPLIT (1u << 16)  // outputs below which a J > 3 fold splits across lanes
@@ -616,8 +681,8 @@ hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t 
   const dim3 g(nbc << JN), b(kRedThreads);
 #define MLH_FOLD_J(j, sp)                                                                   \
   if (J == j && split == sp)                                                                \
-    hipLaunchKernelGGL((fold_group_eq_kernel<j, sp>), g, b, 0, st, Tin, S, JN, rs, Tout, H, lo, a, \
-                       nbc, partials);
+    hipLaunchKernelGGL((fold_group_eq_kernel<j, sp>), g, b, 0, st, Tin, S, JN, rs, w, Tout, H, lo, \
+                       a, nbc, partials);
   MLH_FOLD_J(1, false) MLH_FOLD_J(2, false) MLH_FOLD_J(3, false)
   MLH_FOLD_J(4, false) MLH_FOLD_J(5, false) MLH_FOLD_J(6, false)
   MLH_FOLD_J(4, true) MLH_FOLD_J(5, true) MLH_FOLD_J(6, true)
@@ -923,7 +988,8 @@ __device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_
 __global__ void __launch_bounds__(kRedThreads)
 sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, uint32_t J2,
                       uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
-                      const fe* __restrict__ pts, fe* cdev, const uint32_t* __restrict__ kw) {
+                      const fe* __restrict__ pts, fe* cdev, const uint32_t* __restrict__ kw,
+                      fe* wout) {
   __shared__ DevSha s;
   __shared__ uint32_t stage[8];
   __shared__ fe slot[64];
@@ -964,6 +1030,7 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
   // "grouped eq-factored rounds").  One loop body for both (code size: the
   // one-lane transcript is instruction-fetch bound).
   const uint32_t chi = lane >> J2, clo = lane & ((1u << J2) - 1);
+  fe w1 = fe_one();  // two groups: group 1's factor of the fold weight (lane = corner)
   for (uint32_t g = 0; g < (J2 ? 2u : 1u); ++g) {
     const uint32_t Jg = g ? J2 : J;
     fe x = Y;
@@ -983,6 +1050,10 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
       const uint32_t m0 = g ? 1u << J2 : 1u, m1 = g ? NC : 1u << J2;
       for (uint32_t m = m0; m < m1; m <<= 1) x = fe_add(x, shfl_xor_fe(x, m));
       if (g == 1) {
+        // group 1's factor of this lane's fold weight, while its r's are at hand
+#pragma unroll
+        for (uint32_t u = 0; u < 3; ++u)
+          if (u < J) w1 = fe_mul_s(w1, (chi >> (J - 1 - u)) & 1u ? r[u] : fe_sub(one, r[u]));
 #pragma unroll
         for (uint32_t u = 0; u < 3; ++u) {
           p[u] = u < J2 ? fe_load(pts + J + u) : fe_zero();
@@ -1002,6 +1073,16 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
     fe_store(prev, v);
   }
   if (lane == 1) fe_store(cdev, v);
+  // the eq weights of the finished group's challenges for the fold pass:
+  // w_c = prod_u (c_u ? r_u : 1 - r_u) over the J (+ J2) variables, lane c
+  if (wout && t1 == J && lane < NC) {
+    fe wc = w1;  // J2 == 0: r holds the group's challenges; else group 2's
+    const uint32_t nbits = J2 ? J2 : J, bits = J2 ? clo : chi;
+#pragma unroll
+    for (uint32_t u = 0; u < 3; ++u)
+      if (u < nbits) wc = fe_mul_s(wc, (bits >> (nbits - 1 - u)) & 1u ? r[u] : fe_sub(one, r[u]));
+    fe_store(wout + lane, wc);
+  }
   MLH_TAIL_TS(63);
 }
 
@@ -1252,12 +1333,13 @@ hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in,
 
 hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t J2,
                                  uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
-                                 const fe* pts, fe* c, hipStream_t st, const uint32_t* kw) {
+                                 const fe* pts, fe* c, hipStream_t st, const uint32_t* kw,
+                                 fe* wout) {
   if (J < 1 || J > 3 || J2 > 3 || t0 >= t1 || t1 > J || (J2 && (t0 != 0 || t1 != J)) || nb == 0 ||
       (nb << (J + J2)) > 2 * kMaxRedBlocks)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(sumcheck_group_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, J, J2,
-                     t0, t1, prev, t, polys, rs, pts, c, kw);
+                     t0, t1, prev, t, polys, rs, pts, c, kw, wout);
   return hipGetLastError();
 }
 

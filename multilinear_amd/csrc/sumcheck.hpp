@@ -38,16 +38,19 @@ hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, 
 // round k+t0's slot, rs / pts = round k's r / p).
 hipError_t launch_group_sums_eq(const fe* T, uint64_t S, uint32_t J, const fe* H, const fe* lo,
                                 uint32_t a, fe* partials, hipStream_t st, uint32_t* nb);
+// (w: the 2^J eq weights of rs, sumcheck_group_kernel's wout)
 hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t JN, const fe* rs,
-                                fe* Tout, const fe* H, const fe* lo, uint32_t a, fe* partials,
-                                hipStream_t st, uint32_t* nb);
+                                const fe* w, fe* Tout, const fe* H, const fe* lo, uint32_t a,
+                                fe* partials, hipStream_t st, uint32_t* nb);
 // J2 > 0: two chained groups (J then J2 rounds, all of them) from the
 // 2^(J+J2) corner sums of one pass.
-// kw (optional): the padding-block K + W tables of eq_setup (round t0's at kw).
+// kw (optional): the padding-block K + W tables of eq_setup (round t0's at kw);
+// wout (optional): a launch that finishes the group writes the 2^(J+J2) eq
+// weights of its challenges there (corner c's MSB = the first variable).
 hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t J2,
                                  uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
                                  const fe* pts, fe* c, hipStream_t st,
-                                 const uint32_t* kw = nullptr);
+                                 const uint32_t* kw = nullptr, fe* wout = nullptr);
 // The last a <= 12 rounds of an eq-factored sumcheck in one LDS-resident
 // workgroup (sumcheck_eq_tail_kernel): table = Tin folded over Jin <= 3
 // pending variables with rs_in (2^a entries after it), ets = eq suffix tables
