@@ -272,13 +272,23 @@ fold_kernel(fe* m, fe* __restrict__ d, uint64_t S, fe r, const fe* __restrict__ 
 // 2^J corners x nbc blocks (block = c * nbc + bb, so partials[block] is
 // corner-major); a corner's nbc * 256 threads (a power of two >= 2^a) stride
 // over its Q entries, so a thread's i mod 2^a is fixed and lo is applied once.
+constexpr uint32_t kGroupHLds = 1024;  // group_sums_eq_kernel: H entries staged in LDS (16 KiB)
 __global__ void __launch_bounds__(kRedThreads)
-group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe* __restrict__ H,
+group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe* H,
                      const fe* __restrict__ lo, uint32_t a, uint32_t nbc,
                      fe* __restrict__ partials) {
   const uint64_t Q = S >> J;
   const uint32_t c = blockIdx.x / nbc, bb = blockIdx.x % nbc;
   const fe* Tc = T + (uint64_t)c * Q;
+  // H (Q >> a entries) from LDS when it fits: one vector-memory instruction
+  // per element instead of two (the H reads are wave-uniform broadcasts)
+  __shared__ fe hs[kGroupHLds];
+  const uint64_t nh = Q >> a;
+  if (nh <= kGroupHLds) {
+    for (uint32_t k = threadIdx.x; k < nh; k += blockDim.x) hs[k] = fe_load(H + k);
+    __syncthreads();
+    H = hs;
+  }
   acc9 s0, s1;  // unreduced (two for ILP); < 2^288 for < 2^32 products each
   acc_zero(s0);
   acc_zero(s1);
