@@ -36,7 +36,8 @@ typedef enum mlh_status {
   MLH_OK = 0,
   MLH_ERR_INVALID = 1,       /* bad argument (null pointer, size out of range)   */
   MLH_ERR_NOT_POW2 = 2,      /* "must be a power of two" asserts                   */
-  MLH_ERR_BAD_GENERATOR = 3, /* generator is not of order exactly 2^log_n          */
+  MLH_ERR_BAD_GENERATOR = 3, /* generator not canonical, or (FRI / sharded entry
+                                points) not of order exactly 2^log_n              */
   MLH_ERR_HIP = 4,           /* HIP runtime error / no device                      */
   MLH_ERR_OOM = 5,           /* device allocation failed                           */
   MLH_ERR_NOT_RS_CODE = 6,   /* fri/mod.rs:119-122 "not an RS code"                */
@@ -95,12 +96,16 @@ mlh_status mlh_field_scale(mlh_ctx* ctx, const void* dev_a, const uint8_t c[16],
 
 /* ---- NTT (src/ntt/mod.rs) ------------------------------------------------ */
 /* Polynomial::ntt (ntt/mod.rs:69-110): evals[i] = sum_j coeffs[j] gen^(ij),
- * natural order in and out.  gen must have order exactly 2^log_n.  In-place
- * (dev_in == dev_out) is allowed. */
+ * natural order in and out, when gen has order exactly 2^log_n (the fast
+ * passes).  Any other canonical gen (0 included) gets the reference's own
+ * bit-reverse + radix-2 network output -- well defined but not a DFT -- from a
+ * stage-by-stage path (log_n + 1 - 11 launches; a correctness path, not tuned).
+ * In-place (dev_in == dev_out) is allowed. */
 mlh_status mlh_ntt(mlh_ctx* ctx, const void* dev_coeffs, void* dev_evals, uint32_t log_n,
                    const uint8_t gen[16]);
 /* LagrangePolynomial::intt (ntt/mod.rs:132-173): gen is the forward
- * generator (LagrangePolynomial::gen); uses gen^-1 and scales by 1/n. */
+ * generator (LagrangePolynomial::gen); uses gen^-1 (0 for gen = 0, as
+ * winter-math's inverse) and scales by 1/n.  Generators as mlh_ntt. */
 mlh_status mlh_intt(mlh_ctx* ctx, const void* dev_evals, void* dev_coeffs, uint32_t log_n,
                     const uint8_t gen[16]);
 /* bit_reverse_permutation (ntt/mod.rs:113-123), out of place (in != out). */
@@ -112,7 +117,8 @@ mlh_status mlh_ntt_host(mlh_ctx* ctx, const uint8_t* host_in, uint8_t* host_out,
 
 /* ---- Reed-Solomon, Merkle, FRI (src/fri, src/merkle_tree) -------------------- */
 /* reed_solomon (fri/mod.rs:19-28): zero-pad 2^log_n coeffs to 2^(log_n+1) and
- * NTT with gen (order 2^(log_n+1)).  dev_code holds 2^(log_n+1) elements. */
+ * NTT with gen (order 2^(log_n+1); any other canonical gen as mlh_ntt).
+ * dev_code holds 2^(log_n+1) elements. */
 mlh_status mlh_reed_solomon(mlh_ctx* ctx, const void* dev_coeffs, uint32_t log_n,
                             const uint8_t gen[16], void* dev_code);
 /* reed_solomon(bit_reverse_permutation(coeffs)) in one transform: the commit

@@ -162,6 +162,40 @@ static bool check_generator(u128 gen, uint32_t log_n) {
   return half == kModulus - 1;  // gen^(N/2) = -1  <=>  order exactly N
 }
 
+static mlh_status ensure_ntt_scratch(mlh_ctx* ctx, uint32_t log_n) {
+  const size_t need = (size_t)16 << log_n;
+  if (ctx->ntt_scratch_bytes < need) {
+    if (ctx->ntt_scratch) {
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+      HIP_TRY(ctx, hipFree(ctx->ntt_scratch));
+      ctx->ntt_scratch = nullptr;
+      ctx->ntt_scratch_bytes = 0;
+    }
+    HIP_TRY(ctx, hipMalloc(&ctx->ntt_scratch, need));
+    ctx->ntt_scratch_bytes = need;
+  }
+  return MLH_OK;
+}
+
+// Generator of any other order (gen < M; 0 included): the reference's radix-2
+// network stage by stage (ntt.hip "general-generator network"), w = gen or,
+// for the inverse, gen^-1 (winter-math inverts 0 to 0, as h_inv does).
+static mlh_status ntt_network_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, u128 gen,
+                                   bool inverse, int zero_top) {
+  const u128 w = inverse ? h_inv(gen) : gen;
+  const fe* pw;
+  MLH_TRY(get_table(ctx, w, 1ull << (log_n - 1), 1, &pw));
+  fe* scratch = nullptr;
+  if (in == out && log_n > 11) {
+    MLH_TRY(ensure_ntt_scratch(ctx, log_n));
+    scratch = ctx->ntt_scratch;
+  }
+  const u128 scale = inverse ? h_inv((u128)1 << log_n) : (u128)1;
+  HIP_TRY(ctx, launch_ntt_network(in, out, scratch, pw, log_n, zero_top, to_fe(scale), inverse,
+                                  ctx->stream));
+  return MLH_OK;
+}
+
 // Core NTT on device (in may equal out; zero_top 1: input has N/2 elements,
 // 2: N/2 elements stored bit-reversed -- then in must not equal out).
 static mlh_status ntt_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, u128 gen,
@@ -177,17 +211,7 @@ static mlh_status ntt_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, 
                                   inverse, ctx->stream, 1, zero_top == 2));
     return MLH_OK;
   }
-  const size_t need = (size_t)16 << log_n;
-  if (ctx->ntt_scratch_bytes < need) {
-    if (ctx->ntt_scratch) {
-      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-      HIP_TRY(ctx, hipFree(ctx->ntt_scratch));
-      ctx->ntt_scratch = nullptr;
-      ctx->ntt_scratch_bytes = 0;
-    }
-    HIP_TRY(ctx, hipMalloc(&ctx->ntt_scratch, need));
-    ctx->ntt_scratch_bytes = need;
-  }
+  MLH_TRY(ensure_ntt_scratch(ctx, log_n));
   if (ctx->prof_on) {
     std::vector<hipEvent_t> ev(tb.nradix + 1);
     for (auto& e : ev) e = take_event(ctx);
@@ -331,7 +355,10 @@ static mlh_status ntt_entry(mlh_ctx* ctx, const void* in, void* out, uint32_t lo
   if (!ctx || !in || !out || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
   if (log_n < 1 || log_n > 32) return fail(ctx, MLH_ERR_NOT_POW2, "The number of coeffs must be a power of 2 (n >= 2)");
   const u128 g = h_load(gen);
-  if (!check_generator(g, log_n)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != n");
+  if (g >= kModulus) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator not canonical");
+  if (!check_generator(g, log_n))  // not of order n: the reference's network, not a DFT
+    return ntt_network_core(ctx, reinterpret_cast<const fe*>(in), reinterpret_cast<fe*>(out),
+                            log_n, g, inverse, 0);
   return ntt_core(ctx, reinterpret_cast<const fe*>(in), reinterpret_cast<fe*>(out), log_n, g,
                   inverse, false);
 }
@@ -406,7 +433,10 @@ mlh_status mlh_reed_solomon(mlh_ctx* ctx, const void* dev_coeffs, uint32_t log_n
   if (dev_coeffs == dev_code) return fail(ctx, MLH_ERR_INVALID, "reed_solomon is out of place");
   const uint32_t lc = log_n + MLH_LOG_BLOWUP;
   const u128 g = h_load(gen);
-  if (!check_generator(g, lc)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != 2n");
+  if (g >= kModulus) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator not canonical");
+  if (!check_generator(g, lc))  // not of order 2n: the reference's network, not a DFT
+    return ntt_network_core(ctx, reinterpret_cast<const fe*>(dev_coeffs),
+                            reinterpret_cast<fe*>(dev_code), lc, g, false, 1);
   return ntt_core(ctx, reinterpret_cast<const fe*>(dev_coeffs), reinterpret_cast<fe*>(dev_code),
                   lc, g, false, 1);
 }
@@ -418,7 +448,10 @@ mlh_status mlh_reed_solomon_brev(mlh_ctx* ctx, const void* dev_coeffs, uint32_t 
   if (dev_coeffs == dev_code) return fail(ctx, MLH_ERR_INVALID, "reed_solomon is out of place");
   const uint32_t lc = log_n + MLH_LOG_BLOWUP;
   const u128 g = h_load(gen);
-  if (!check_generator(g, lc)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != 2n");
+  if (g >= kModulus) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator not canonical");
+  if (!check_generator(g, lc))  // not of order 2n: the reference's network, not a DFT
+    return ntt_network_core(ctx, reinterpret_cast<const fe*>(dev_coeffs),
+                            reinterpret_cast<fe*>(dev_code), lc, g, false, 2);
   return ntt_core(ctx, reinterpret_cast<const fe*>(dev_coeffs), reinterpret_cast<fe*>(dev_code),
                   lc, g, false, 2);
 }

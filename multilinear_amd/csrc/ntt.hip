@@ -470,6 +470,130 @@ __global__ void pow_series_kernel(fe* __restrict__ out, const fe* __restrict__ t
   fe_store(out + t, fe_mul(tlo[t & 4095], thi[t >> 12]));
 }
 
+// ---- general-generator network --------------------------------------------
+// Polynomial::ntt / LagrangePolynomial::intt (src/ntt/mod.rs:69-110, :132-173)
+// for a generator whose order is not exactly N.  The reference's loop --
+// bit-reverse, then stage len = 4..N with butterflies u +- v * g_len^j,
+// g_len = gen^(N/len) -- is then a well-defined linear map but no DFT: with
+// gen^(N/2) != -1, "u - w v" is not "u + w' v" for any power w', so the
+// four-step passes above (which rely on that) cannot reproduce it.  These
+// kernels run the same butterfly network stage by stage: the first kNetLB
+// stages per LDS-resident block of 2^kNetLB positions, the rest up to 4 per
+// launch in registers.  pw[t] = w^t (t < N/2); stage s (len = 2^(s+1)) uses
+// pw[j << (log_n - 1 - s)] = g_len^j, the reference's gen_pows[j] (exact: the
+// field is exact, however the power is formed).  Correctness path, not tuned.
+constexpr uint32_t kNetLB = 11;  // 2^11 entries = 32 KiB of LDS
+
+__device__ __forceinline__ uint64_t bitrev64(uint64_t x, uint32_t bits) {
+  return bits ? __builtin_bitreverse64(x) >> (64 - bits) : 0;
+}
+
+// zero_top: 0 = N inputs; 1 = N/2 inputs, the rest zero (reed_solomon's
+// resize, fri/mod.rs:19-28); 2 = as 1, coefficient c stored at
+// in[bitrev_{log_n - 1}(c)].
+__global__ void __launch_bounds__(1024)
+ntt_net_block_kernel(const fe* __restrict__ in, fe* __restrict__ out, const fe* __restrict__ pw,
+                     uint32_t log_n, uint32_t lb, int zero_top, fe scale, int apply_scale) {
+  __shared__ fe lds[1u << kNetLB];
+  const uint32_t B = 1u << lb;
+  const uint64_t N = 1ull << log_n, base = (uint64_t)blockIdx.x << lb;
+  for (uint32_t i = threadIdx.x; i < B; i += blockDim.x) {
+    const uint64_t src = bitrev64(base + i, log_n);  // bit_reverse_permutation (ntt/mod.rs:113-123)
+    fe v;
+    if (zero_top == 0) v = fe_load(in + src);
+    else if (src >= N / 2) v = fe_zero();
+    else v = fe_load(in + (zero_top == 2 ? bitrev64(src, log_n - 1) : src));
+    lds[i] = v;
+  }
+  __syncthreads();
+  for (uint32_t s = 0; s < lb; ++s) {
+    const uint32_t h = 1u << s;
+    for (uint32_t b = threadIdx.x; b < B / 2; b += blockDim.x) {
+      const uint32_t j = b & (h - 1);
+      const uint32_t p0 = j + ((b >> s) << (s + 1));
+      const fe u = lds[p0];
+      fe v = lds[p0 + h];
+      if (j) v = fe_mul(v, fe_load(pw + ((uint64_t)j << (log_n - 1 - s))));  // gen_pows[0] = 1
+      lds[p0] = fe_add(u, v);
+      lds[p0 + h] = fe_sub(u, v);
+    }
+    __syncthreads();
+  }
+  for (uint32_t i = threadIdx.x; i < B; i += blockDim.x) {
+    fe v = lds[i];
+    if (apply_scale) v = fe_mul(v, scale);
+    fe_store(out + base + i, v);
+  }
+}
+
+// Stages s0 .. s0 + Q - 1 (s0 >= kNetLB): each thread owns the 2^Q positions
+// base + m 2^s0 (m < 2^Q) that these stages couple; consecutive threads take
+// consecutive low bits, so every load and store is a contiguous wave run.
+// Runs in place (in == out) or out of place.
+template <int Q>
+__global__ void __launch_bounds__(256)
+ntt_net_stage_kernel(const fe* in, fe* out, const fe* __restrict__ pw, uint32_t log_n,
+                     uint32_t s0, fe scale, int apply_scale) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (1ull << (log_n - Q))) return;
+  const uint64_t low = g & ((1ull << s0) - 1);
+  const uint64_t base = ((g >> s0) << (s0 + Q)) | low;
+  fe x[1 << Q];
+#pragma unroll
+  for (int m = 0; m < (1 << Q); ++m) x[m] = fe_load(in + base + ((uint64_t)m << s0));
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const uint32_t s = s0 + q;
+    const int d = 1 << q;
+#pragma unroll
+    for (int b = 0; b < (1 << (Q - 1)); ++b) {
+      const int m = ((b >> q) << (q + 1)) | (b & (d - 1));  // pairs (m, m + d)
+      const uint64_t j = (base + ((uint64_t)m << s0)) & ((1ull << s) - 1);
+      const fe v = j ? fe_mul(x[m + d], fe_load(pw + (j << (log_n - 1 - s)))) : x[m + d];
+      const fe u = x[m];
+      x[m] = fe_add(u, v);
+      x[m + d] = fe_sub(u, v);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < (1 << Q); ++m) {
+    fe v = x[m];
+    if (apply_scale) v = fe_mul(v, scale);
+    fe_store(out + base + ((uint64_t)m << s0), v);
+  }
+}
+
+hipError_t launch_ntt_network(const fe* in, fe* out, fe* scratch, const fe* pw, uint32_t log_n,
+                              int zero_top, fe scale, bool apply_scale, hipStream_t st) {
+  if (log_n < 1 || log_n > 40 || (zero_top && in == out)) return hipErrorInvalidValue;
+  const uint32_t lb = log_n < kNetLB ? log_n : kNetLB;
+  const uint64_t blocks = 1ull << (log_n - lb);
+  // the block pass gathers bit-reversed positions from all of `in`: out of
+  // place whenever it has more than one block
+  fe* first = (in == out && blocks > 1) ? scratch : out;
+  const bool only = lb == log_n;
+  const uint32_t threads = lb >= 11 ? 1024 : (1u << lb) / 2 < 64 ? 64 : (1u << lb) / 2;
+  hipLaunchKernelGGL(ntt_net_block_kernel, dim3((unsigned)blocks), dim3(threads), 0, st, in, first,
+                     pw, log_n, lb, zero_top, scale, (only && apply_scale) ? 1 : 0);
+  hipError_t e = hipGetLastError();
+  for (uint32_t s0 = lb; e == hipSuccess && s0 < log_n;) {
+    const uint32_t q = log_n - s0 < 4 ? log_n - s0 : 4;
+    const bool last = s0 + q == log_n;
+    fe* dst = last ? out : first;
+    const int sc = (last && apply_scale) ? 1 : 0;
+    const dim3 grid((unsigned)(((1ull << (log_n - q)) + 255) / 256)), blk(256);
+    switch (q) {
+      case 1: hipLaunchKernelGGL(ntt_net_stage_kernel<1>, grid, blk, 0, st, first, dst, pw, log_n, s0, scale, sc); break;
+      case 2: hipLaunchKernelGGL(ntt_net_stage_kernel<2>, grid, blk, 0, st, first, dst, pw, log_n, s0, scale, sc); break;
+      case 3: hipLaunchKernelGGL(ntt_net_stage_kernel<3>, grid, blk, 0, st, first, dst, pw, log_n, s0, scale, sc); break;
+      default: hipLaunchKernelGGL(ntt_net_stage_kernel<4>, grid, blk, 0, st, first, dst, pw, log_n, s0, scale, sc); break;
+    }
+    e = hipGetLastError();
+    s0 += q;
+  }
+  return e;
+}
+
 // ---- host-side launchers ---------------------------------------------------
 
 template <int LOGR, int EPT>

@@ -44,8 +44,10 @@ def neg(a):
 
 
 def inv(a):
-    assert a % M != 0
-    return pow(a, M - 2, M)
+    """Field128 Div (field.rs:113-124) -> winterfell 0.12's f128 BaseElement
+    division, self * rhs.inv(); winter-math documents inv(ZERO) = ZERO, which
+    a^(M-2) gives as well (LagrangePolynomial::intt with gen = 0)."""
+    return pow(a % M, M - 2, M)
 
 
 def div(a, b):

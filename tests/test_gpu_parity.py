@@ -99,11 +99,67 @@ def test_ntt_in_place_and_host_path():
 def test_ntt_rejects_bad_inputs():
     ctx = D.context()
     x = dev(list(range(16)))
-    # not a generator of order 16
-    st = D.lib().mlh_ntt(ctx, D.ptr(x), D.ptr(x), 4, D.fe_bytes(F.pow_2_generator(5)))
+    # not a canonical field element (a generator of any order is accepted)
+    st = D.lib().mlh_ntt(ctx, D.ptr(x), D.ptr(x), 4, D.fe_bytes(F.M))
     assert st == 3
     st = D.lib().mlh_ntt(ctx, D.ptr(x), D.ptr(x), 0, D.fe_bytes(1))
     assert st == 2
+
+
+def _other_order_generators(log_n, seed):
+    """Generators whose order is not 2^log_n (order 2N, N/2, 1; zero; -1; a
+    random element): Polynomial::ntt still runs its bit-reverse + radix-2 loop
+    (ntt/mod.rs:69-110), a linear map that is not a DFT, and the device's
+    stage-by-stage network must give the same values."""
+    return [F.pow_2_generator(log_n + 1), F.pow_2_generator(max(log_n - 1, 0)), 1, 0, F.M - 1,
+            rand_vals(1, seed)[0]]
+
+
+@pytest.mark.parametrize("log_n", [1, 2, 3, 6, 10, 11, 12, 13])
+def test_ntt_intt_any_generator_match_oracle(log_n):
+    n = 1 << log_n
+    vals = rand_vals(n, 31 + log_n)
+    for g in _other_order_generators(log_n, 700 + log_n):
+        assert host(MN.Polynomial(dev(vals)).ntt(g).evals) == ON.ntt(vals, g), g
+        assert host(MN.LagrangePolynomial(g, dev(vals)).intt().coeffs) == ON.intt(vals, g), g
+        x = dev(vals)  # in place (the network's block pass goes through scratch)
+        ctx = D.context()
+        D.check(D.lib().mlh_ntt(ctx, D.ptr(x), D.ptr(x), log_n, D.fe_bytes(g)), ctx)
+        assert host(x) == ON.ntt(vals, g), g
+
+
+@pytest.mark.parametrize("log_n", [0, 1, 5, 11, 12])
+def test_reed_solomon_any_generator_matches_oracle(log_n):
+    n = 1 << log_n
+    vals = rand_vals(n, 55 + log_n)
+    perm = [int(format(i, "0%db" % log_n)[::-1], 2) if log_n else 0 for i in range(n)]
+    for g in _other_order_generators(log_n + 1, 800 + log_n):
+        want = OF.reed_solomon(vals, g)
+        assert host(MF.reed_solomon(dev(vals), g)) == want, g
+        # reed_solomon_brev(x) = reed_solomon(bit_reverse_permutation(x))
+        assert host(MF.reed_solomon_brev(dev([vals[perm[i]] for i in range(n)]), g)) == want, g
+
+
+@pytest.mark.parametrize("log_n", [15, 16, 20])
+def test_ntt_any_generator_vs_c_oracle(log_n):
+    """Past the LDS block (2^11): the register stage launches (4 + 4 + 1 stages
+    at 2^20), in and out of place, forward and inverse, RS with an order-N
+    generator (half the 2N the code needs)."""
+    C = _c_oracle()
+    g = rand_vals(1, 4000 + log_n)[0]
+    x = D.random_limbs(1 << log_n, 600 + log_n)
+    want = C.ntt(x, log_n, g)
+    assert (D.from_device(MN.Polynomial(D.to_device(x)).ntt(g).evals) == want).all()
+    d = D.to_device(x)
+    ctx = D.context()
+    D.check(D.lib().mlh_ntt(ctx, D.ptr(d), D.ptr(d), log_n, D.fe_bytes(g)), ctx)
+    assert (D.from_device(d) == want).all()
+    want_i = C.ntt(x, log_n, g, inverse=True)
+    assert (D.from_device(MN.LagrangePolynomial(g, D.to_device(x)).intt().coeffs) == want_i).all()
+    h = F.pow_2_generator(log_n - 1)
+    half = np.ascontiguousarray(x[: 1 << (log_n - 2)])
+    want_rs = C.reed_solomon(half, log_n - 2, h)
+    assert (D.from_device(MF.reed_solomon(D.to_device(half), h)) == want_rs).all()
 
 
 def test_bit_reverse_and_generator_powers():
