@@ -61,7 +61,7 @@ def main():
         text = open(asm).read()
     out = {}
     # kernel bodies: "<mangled>:  ; @<mangled>" ... "s_endpgm"
-    for m in re.finditer(r"\n(_ZN3mlh15ntt_pass_kernelILi(\d)ELi(\d)ELi(\d)ELi(\d+)\w*):\s*;\s*@",
+    for m in re.finditer(r"\n(_ZN3mlh15ntt_pass_kernelILi(\d+)ELi(\d)ELi(\d)ELi(\d+)\w*):\s*;\s*@",
                          text):
         name, logr, tw, zt, ept = m.group(1), m.group(2), m.group(3), m.group(4), m.group(5)
         end = text.index("s_endpgm", m.end())
