@@ -37,6 +37,7 @@
 namespace mlh {
 
 constexpr int kCols = 8;  // columns per tile (8 x 16 B = 128 B runs)
+constexpr int kLogCols = 3;
 constexpr int kEPT = 8;   // elements per thread
 
 __device__ __forceinline__ uint32_t bitrev(uint32_t x, int bits) {
@@ -48,12 +49,13 @@ struct PassGeom {
   uint32_t nradix;      // P
   uint32_t p;           // 0-based pass index
   uint32_t logr[kMaxPasses];
-  uint64_t stride;      // W_p (elements between consecutive rows of this digit)
-  uint64_t S;           // R_1*...*R_{p-1}
+  // every stride and count is a power of two: log2 of each, so that the
+  // kernels index by shifts (no 64-bit multiplies or divisions per address)
+  uint32_t lstride;     // W_p = 2^lstride (elements between consecutive rows of this digit)
   uint32_t loga;        // inter-pass twiddle split jrest = jh * 2^loga + jl
-  uint64_t tpv;         // tiles per vector (batched transforms: blockIdx.x = b*tpv + tile)
-  uint64_t in_vstride;  // elements between consecutive input vectors
-  uint64_t out_vstride; // elements between consecutive output vectors
+  uint32_t ltpv;        // tiles per vector (batched transforms: blockIdx.x = b*2^ltpv + tile)
+  uint32_t lin_v;       // elements between consecutive input vectors
+  uint32_t lout_v;      // elements between consecutive output vectors
 };
 
 // Last pass: natural output index is K = k_1 + R_1*rev(mid) + (N/R_P)*k_P,
@@ -129,38 +131,34 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   const int tid = threadIdx.x;
   const int c = tid % kCols;
   const int t = tid / kCols;
-  const uint64_t N = 1ull << g.log_n;
-  const uint64_t vec = blockIdx.x / g.tpv;
-  const uint64_t tile = blockIdx.x % g.tpv;
-  in += vec * g.in_vstride;
-  out += vec * g.out_vstride;
+  const uint64_t vec = (uint64_t)blockIdx.x >> g.ltpv;
+  const uint64_t tile = blockIdx.x & ((1ull << g.ltpv) - 1);
+  in += vec << g.lin_v;
+  out += vec << g.lout_v;
 
   // ---- tile geometry -----------------------------------------------------
   uint64_t base, jrest = 0, k1 = 0, mid = 0;
-  uint64_t rstride;  // element stride between rows of this digit
-  uint64_t cstride;  // element stride between the 8 columns
+  uint32_t rshift;  // log2 element stride between rows of this digit
+  uint32_t cshift;  // log2 element stride between the 8 columns
   if (!LAST) {
-    const uint64_t W = g.stride;
-    const uint64_t lowcount = W / kCols;
-    const uint64_t hi = tile / lowcount, lo = tile % lowcount;
-    base = hi * (uint64_t)R * W + lo * kCols;
-    jrest = lo * kCols + c;
-    rstride = W;
-    cstride = 1;
+    const uint32_t lw = g.lstride;  // W >= kCols
+    const uint64_t hi = tile >> (lw - kLogCols), lo = tile & ((1ull << (lw - kLogCols)) - 1);
+    base = (hi << (LOGR + lw)) + (lo << kLogCols);
+    jrest = (lo << kLogCols) + c;
+    rshift = lw;
+    cshift = 0;
   } else {
-    const uint64_t RP = (uint64_t)R;
-    const uint64_t R1 = 1ull << g.logr[0];
-    const uint64_t W1 = N >> g.logr[0];
-    const uint64_t MID = N / (R1 * RP);
-    const uint64_t d1hi = tile / MID;
-    mid = tile % MID;
-    base = d1hi * kCols * W1 + mid * RP;
-    k1 = d1hi * kCols + c;
-    rstride = 1;
-    cstride = W1;
+    const uint32_t lw1 = g.log_n - g.logr[0];  // W1 = N / R1
+    const uint32_t lmid = lw1 - LOGR;          // MID = N / (R1 R_P)
+    const uint64_t d1hi = tile >> lmid;
+    mid = tile & ((1ull << lmid) - 1);
+    base = (d1hi << (kLogCols + lw1)) + (mid << LOGR);
+    k1 = (d1hi << kLogCols) + c;
+    rshift = 0;
+    cshift = lw1;
   }
-  const fe* src = in + base + (uint64_t)c * cstride;
-  fe* dst = out + base + (uint64_t)c * cstride;
+  const fe* src = in + base + ((uint64_t)c << cshift);
+  fe* dst = out + base + ((uint64_t)c << cshift);
 
 #if MLH_LDS_TB
   // Two-table twiddle: TB[k][jh] has one jh for the tile's 8 columns (loga >=
@@ -171,9 +169,10 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   fe tbv[kTbPerThread];
   if constexpr (TW == 0) {
     constexpr int NT = kCols * R / EPT;
-    const uint64_t jh = jrest >> g.loga, tcols = g.stride >> g.loga;
+    const uint64_t jh = jrest >> g.loga;
+    const uint32_t ltcols = g.lstride - g.loga;
 #pragma unroll
-    for (int e = 0; e < kTbPerThread; ++e) tbv[e] = fe_load(tb + (uint64_t)(e * NT + tid) * tcols + jh);
+    for (int e = 0; e < kTbPerThread; ++e) tbv[e] = fe_load(tb + ((uint64_t)(e * NT + tid) << ltcols) + jh);
   }
 #endif
 
@@ -195,7 +194,7 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
       const uint32_t l = idx & 63, grp = idx >> 6;
       const uint32_t row = grp * 8 + (l & 7), col = l >> 3;
       lds[row * kCols + (col ^ (row & (kCols - 1)))] =
-          fe_load(in + base + (uint64_t)col * cstride + row);
+          fe_load(in + base + ((uint64_t)col << cshift) + row);
     }
     __syncthreads();
 #pragma unroll
@@ -219,7 +218,7 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
       const uint64_t colr = __builtin_bitreverse64(jrest) >> (64 - logw);
       x[e] = fe_load(in + (colr << (LOGR - 1)) + ((uint32_t)(t * EPT + e) >> 1));
     } else {
-      x[e] = fe_load(src + (uint64_t)row * rstride);
+      x[e] = fe_load(src + ((uint64_t)row << rshift));
     }
   }
 
@@ -360,14 +359,15 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
 #if MLH_LDS_TB
         const fe b0 = lds[pos[e]], b1 = lds[pos[e + 1]];
 #else
-        const uint64_t tcols = g.stride >> g.loga, jh = jrest >> g.loga;
-        const fe b0 = fe_load(tb + (uint64_t)pos[e] * tcols + jh);
-        const fe b1 = fe_load(tb + (uint64_t)pos[e + 1] * tcols + jh);
+        const uint32_t ltcols = g.lstride - g.loga;
+        const uint64_t jh = jrest >> g.loga;
+        const fe b0 = fe_load(tb + ((uint64_t)pos[e] << ltcols) + jh);
+        const fe b1 = fe_load(tb + ((uint64_t)pos[e + 1] << ltcols) + jh);
 #endif
         bfly_ff_v(x[e], b0, x[e + 1], b1, rare);
       }
-      fe_store(dst + (uint64_t)pos[e] * rstride, x[e]);
-      fe_store(dst + (uint64_t)pos[e + 1] * rstride, x[e + 1]);
+      fe_store(dst + ((uint64_t)pos[e] << rshift), x[e]);
+      fe_store(dst + ((uint64_t)pos[e + 1] << rshift), x[e + 1]);
     }
   } else {
     // canonical output, four elements per asm statement
@@ -686,20 +686,18 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
   g.nradix = tb.nradix;
   for (uint32_t p = 0; p < tb.nradix; ++p) g.logr[p] = tb.logr[p];
   const uint64_t N = 1ull << log_n;
-  uint64_t S = 1;
   uint64_t W = N;
   for (uint32_t p = 0; p < tb.nradix; ++p) {
     const uint32_t lr = tb.logr[p];
     W >>= lr;
     g.p = p;
-    g.stride = W;
-    g.S = S;
+    g.lstride = (uint32_t)__builtin_ctzll(W);
     g.loga = tb.loga[p];
     const bool last = (p + 1 == tb.nradix);
-    g.tpv = N / ((uint64_t)kCols << lr);
-    const uint64_t tiles = g.tpv * batch;
-    g.in_vstride = (p == 0) ? (zero_top ? N / 2 : N) : N;
-    g.out_vstride = N;
+    g.ltpv = log_n - kLogCols - lr;
+    const uint64_t tiles = (N >> (kLogCols + lr)) * batch;
+    g.lin_v = (p == 0 && zero_top) ? log_n - 1 : log_n;
+    g.lout_v = log_n;
     // pass 0: in -> scratch; middle passes in place on scratch; the last pass
     // (a digit-reversal permutation of its tiles) scratch -> out.  The last
     // pass can never run in place: a block would overwrite tiles that other,
@@ -723,7 +721,6 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
       e = hipStreamSynchronize(st);
       if (e != hipSuccess) return e;
     }
-    S <<= lr;
   }
   if (ev) (void)hipEventRecord(ev[tb.nradix], st);
   return hipSuccess;
