@@ -439,7 +439,8 @@ def main():
             D.check(lib.mlh_reed_solomon(ctx, D.ptr(x), log_n, g2, D.ptr(code)), ctx)
             D.check(lib.mlh_merkle_commit_pairs(ctx, D.ptr(code), log_n + 1, D.ptr(layers), root), ctx)
 
-        fri_commit()
+        for _ in range(3):  # untimed: the first commits after the NTT loop run ~7 % slower
+            fri_commit()
         torch.cuda.synchronize()
         creps = max(reps, 10)  # ~30 ms of commits: a steadier mean than 3
         t0 = time.perf_counter()
