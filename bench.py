@@ -180,7 +180,11 @@ def load_valu_profile():
     out = {"source": os.path.basename(paths[0]),
            "clock": "GRBM_GUI_ACTIVE / 8 XCDs / wall, capped at the chip's %.1f GHz; kernels "
                     "under 50 us get the cap (the derivation breaks for short dispatches)"
-                    % CHIP_MAX_GHZ, "kernels": {}}
+                    % CHIP_MAX_GHZ,
+           "issue_frac": "lane-instr/s over one wave64 VALU instruction per 4 cycles per SIMD at "
+                         "that clock; the clock derivation is good to ~2 %, so issue_frac_raw "
+                         "slightly above 1 means at the ceiling (issue_frac caps it at 1)",
+           "kernels": {}}
     for name, k in d.get("kernels", {}).items():
         for key, what in picks.items():
             if name.endswith("mlh::" + key) and k.get("eff_clock_ghz"):
@@ -190,7 +194,8 @@ def load_valu_profile():
                 out["kernels"][key] = {"what": what, "avg_ms": k["avg_ms"],
                                        "lane_instr_per_s": k["lane_instr_per_s"],
                                        "clock_ghz": clk,
-                                       "issue_frac": min(1.0, k["lane_instr_per_s"] / ceiling)}
+                                       "issue_frac": min(1.0, k["lane_instr_per_s"] / ceiling),
+                                       "issue_frac_raw": k["lane_instr_per_s"] / ceiling}
     return out
 
 
