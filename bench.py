@@ -221,6 +221,9 @@ def main():
     ap.add_argument("--spinup-s", type=float, default=0.3,
                     help="untimed setup: run the step this long first so clocks settle")
     ap.add_argument("--log-n", type=int, default=24)
+    ap.add_argument("--prof-every", type=int, default=8,
+                    help="HIP-event kernel timer on every k-th step of the timed region (each "
+                         "timing event costs the stream a few us; 1 = every step)")
     ap.add_argument("--extra-reps", type=int, default=3, help="reps of the secondary timings")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
@@ -315,7 +318,7 @@ def main():
     ntt_drain()
     barrier()
     lib.mlh_profile_reset(ctx)
-    lib.mlh_profile_enable(ctx, 1)
+    lib.mlh_profile_enable(ctx, max(1, args.prof_every))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ntt_once()
@@ -387,6 +390,10 @@ def main():
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
             "launch_avg_ms": dom_stat["avg_ms"],
+            "launch_timing": "HIP events on the launch stream around %s of the timed region "
+                             "(%d timed launches)" % (
+                                 "every step" if args.prof_every <= 1
+                                 else "every %dth step" % args.prof_every, dom_stat["launches"]),
             "alg_bytes_per_launch": alg_bytes,
             "alg_bytes_rule": "32 B x 2^%d / %d passes (SURVEY.md 8(d))" % (log_n, passes),
             "valu_frac": valu_frac,
@@ -658,7 +665,7 @@ def sharded_ntt_extra(args, pipe, x, world, barrier, log_n, log_p, lib, ctx):
     pipe.drain()
     barrier()
     lib.mlh_profile_reset(ctx)
-    lib.mlh_profile_enable(ctx, 1)
+    lib.mlh_profile_enable(ctx, max(1, args.prof_every))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pipe.submit(x)

@@ -492,9 +492,12 @@ mlh_status mlh_sharded_sumcheck_prove(mlh_ctx* ctx, const mlh_transport* tp, voi
                                       uint8_t* polys_out, uint8_t* rs_out);
 
 /* ---- device timing helpers (bench / profiling) --------------------------- */
-/* Kernel timer: while enabled, every NTT pass launch is bracketed by HIP
- * events on the context stream; mlh_profile_get (synchronising) returns the
- * launch count and summed milliseconds for a kernel label such as
+/* Kernel timer: while enabled, the NTT pass launches are bracketed by HIP
+ * events on the context stream -- those of every transform for on = 1, of
+ * every on-th transform for on > 1 (each timing event costs the stream a few
+ * microseconds; sampling keeps that out of a throughput measurement);
+ * mlh_profile_get (synchronising) returns the launch count and summed
+ * milliseconds of the bracketed launches for a kernel label such as
  * "ntt_pass<8,0,0>" (radix log2, last pass, zero-padded input). */
 mlh_status mlh_profile_enable(mlh_ctx* ctx, int on);
 mlh_status mlh_profile_reset(mlh_ctx* ctx);

@@ -204,15 +204,13 @@ static mlh_status ntt_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, 
   MLH_TRY(get_ntt_tables(ctx, gen, log_n, inverse, &tb));
   if (log_n <= 10) {
     const uint64_t N = 1ull << log_n;
-    if (in == out && log_n > 0) {
-      // small kernel reads everything into LDS before writing; in-place is safe
-    }
+    // (in-place is safe: the small kernel reads everything into LDS before writing)
     HIP_TRY(ctx, launch_ntt_small(in, out, tb.tw_small, log_n, zero_top ? N / 2 : N, tb.scale,
                                   inverse, ctx->stream, 1, zero_top == 2));
     return MLH_OK;
   }
   MLH_TRY(ensure_ntt_scratch(ctx, log_n));
-  if (ctx->prof_on) {
+  if (prof_sample(ctx)) {
     std::vector<hipEvent_t> ev(tb.nradix + 1);
     for (auto& e : ev) e = take_event(ctx);
     HIP_TRY(ctx, launch_ntt_passes(in, out, ctx->ntt_scratch, tb, log_n, zero_top, ctx->stream,
@@ -1657,8 +1655,10 @@ extern "C" {
 // kernel timer
 // ---------------------------------------------------------------------------
 mlh_status mlh_profile_enable(mlh_ctx* ctx, int on) {
-  if (!ctx) return MLH_ERR_INVALID;
+  if (!ctx || on < 0) return MLH_ERR_INVALID;
   ctx->prof_on = on != 0;
+  ctx->prof_every = on > 1 ? (uint32_t)on : 1u;
+  ctx->prof_tick = 0;
   return MLH_OK;
 }
 

@@ -67,6 +67,8 @@ struct mlh_ctx {
   uint32_t forced_plan_len = 0;
   // kernel timer (mlh_profile_*): HIP events on the launch stream
   bool prof_on = false;
+  uint32_t prof_every = 1;  // bracket every prof_every-th transform / launch
+  uint64_t prof_tick = 0;
   std::vector<hipEvent_t> ev_free;
   struct Pending {
     std::string label;
@@ -108,13 +110,19 @@ inline void resolve_profile(mlh_ctx* ctx) {
   ctx->pending.clear();
 }
 
+// Whether the kernel timer brackets this transform / launch: every
+// prof_every-th one while enabled (the events cost the stream a few us each).
+inline bool prof_sample(mlh_ctx* ctx) {
+  return ctx->prof_on && ctx->prof_tick++ % ctx->prof_every == 0;
+}
+
 // Kernel-timer bracket around one launch (no-op unless mlh_profile_enable).
 struct ProfScope {
   mlh_ctx* ctx;
   const char* label;
   hipEvent_t a = nullptr;
   ProfScope(mlh_ctx* c, const char* lab) : ctx(c), label(lab) {
-    if (ctx->prof_on) {
+    if (prof_sample(ctx)) {
       a = take_event(ctx);
       (void)hipEventRecord(a, ctx->stream);
     }

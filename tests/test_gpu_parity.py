@@ -1045,3 +1045,25 @@ def test_table_cache_is_bounded_and_results_stay_exact():
         assert lib.mlh_table_cache_bytes(ctx) <= 2 << 20
     finally:
         D.check(lib.mlh_set_table_cache_limit(ctx, 1 << 30), ctx)
+
+
+def test_kernel_timer_sampling():
+    """mlh_profile_enable(ctx, k): HIP events around every k-th transform only
+    (bench.py --prof-every); k = 1 brackets every launch."""
+    import ctypes
+
+    ctx = D.context()
+    lib = D.lib()
+    x = D.random_device(1 << 16, 77)
+    g = D.fe_bytes(F.pow_2_generator(16))
+    for k, want in ((1, 8), (4, 2), (3, 3)):
+        lib.mlh_profile_reset(ctx)
+        D.check(lib.mlh_profile_enable(ctx, k), ctx)
+        for _ in range(8):
+            D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(x), 16, g), ctx)
+        lib.mlh_profile_enable(ctx, 0)
+        for lab in (b"ntt_pass<8,3,0>", b"ntt_pass<8,2,0>"):
+            cnt, tot = ctypes.c_uint64(), ctypes.c_double()
+            D.check(lib.mlh_profile_get(ctx, lab, ctypes.byref(cnt), ctypes.byref(tot)), ctx)
+            assert cnt.value == want and tot.value > 0, (k, lab, cnt.value)
+    assert lib.mlh_profile_enable(ctx, -1) == _lib.MLH_ERR_INVALID
