@@ -910,61 +910,52 @@ __device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_
                                                 const uint32_t* kw) {
   const uint32_t NC = 1u << J;
   const uint32_t lane = threadIdx.x & 63;
+  const bool is0 = lane == 0, is1 = lane == 1;
   const bool wl = lane >= 8 && lane < 8 + NC;  // corner-weight lane
   const uint32_t cl = lane - 8;                // its corner
-  fe e0 = fe_zero(), c1 = fe_zero(), c2 = fe_zero(), rp = fe_zero(), pp = fe_zero();
   const fe one = fe_one();
-  for (uint32_t tt = t0; tt <= t1; ++tt) {
+  // A corner lane's weight in round t is X_c times the J - 1 factors
+  // (c_u ? x_u : 1 - x_u), u != t, x_u = r_u (u < t) or p_u (u > t), kept in
+  // increasing u in F0, F1 (one when absent).  Going from round t to t + 1
+  // only slot t changes (p_{t+1}'s factor becomes r_t's), so after each
+  // challenge one factor is replaced instead of all being re-selected.
+  fe F0 = one, F1 = one;
+  {
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < 3; ++u) {
+      if (u >= J || u == t0) continue;
+      const fe x = u < t0 ? r[u] : p[u];
+      const fe f = (cl >> (J - 1 - u)) & 1u ? x : fe_sub(one, x);
+      if (k == 0) F0 = f; else F1 = f;
+      ++k;
+    }
+  }
+  // step A operands, v = P + Q (R + S T): round t0 keeps the claim (lane 0)
+  // and the eq scale (lane 1) as given; corner lanes X F0 F1
+  fe P = is0 || is1 ? v : fe_zero(), Q = wl ? X : fe_zero(), R = fe_zero(), S = F0, T = F1;
+  for (uint32_t tt = t0;; ++tt) {
     const int tb = 3 + 8 * (int)tt;
     (void)tb;
-    // step A: lane 0 claim = e0 + r (c1 + c2 r), lane 1 c (0 + c (1-p + r (2p-1))),
-    // weight lanes X_c prod(factors); first round of the launch: v as loaded
-    {
-      fe P = fe_zero(), Q = fe_zero(), R = fe_zero(), S = fe_zero(), T = fe_zero();
-      if (tt > t0) {
-        if (lane == 0) { P = e0; Q = rp; R = c1; S = c2; T = rp; }
-        if (lane == 1) { Q = v; R = fe_sub(one, pp); S = rp; T = fe_sub(fe_dbl(pp), one); }
-      } else if (lane < 2) {
-        P = v;
-      }
-      if (wl && tt < t1) {  // the J - 1 factors of corner cl (at most two: S, T)
-        S = one;
-        T = one;
-        bool first = true;
-#pragma unroll
-        for (uint32_t u = 0; u < 3; ++u) {
-          if (u >= J || u == tt) continue;
-          const bool bit = (cl >> (J - 1 - u)) & 1u;
-          const fe x = u < tt ? r[u] : p[u];
-          const fe f = bit ? x : fe_sub(one, x);
-          if (first) S = f; else T = f;
-          first = false;
-        }
-        Q = X;
-      }
-      v = pqrst(P, Q, R, S, T);
-    }
+    v = pqrst(P, Q, R, S, T);
     if (tt == t1) break;
     MLH_TAIL_TS(tb);
-    fe pv = fe_zero();
-#pragma unroll
-    for (uint32_t u = 0; u < 3; ++u)
-      if (u == tt) pv = p[u];
+    const fe pv = tt == 0 ? p[0] : (tt == 1 ? p[1] : p[2]);  // wave-uniform
     const bool bt = (cl >> (J - 1 - tt)) & 1u;
     fe E0 = wl && !bt ? v : fe_zero(), E1 = wl && bt ? v : fe_zero();
     E0 = group_sum_dpp(E0, NC);  // corner lanes 8..8+NC: an aligned group
     E1 = group_sum_dpp(E1, NC);
     MLH_TAIL_TS(tb + 1);
-    // step B: lane 0 s1 = E1 (c p), lane 1 s2 = (2 E1 - E0)(c (3p - 1))
+    // step B: lane 0 s1 = E1 (c p), the others s2 = (2 E1 - E0)(c (3p - 1))
     E0 = bcast_fe(E0, 8);
     E1 = bcast_fe(E1, 8);
     const fe cs = bcast_fe(v, 1);
-    const fe sB = pqrst(fe_zero(), lane == 0 ? E1 : fe_sub(fe_dbl(E1), E0), fe_zero(), cs,
-                        lane == 0 ? pv : fe_sub(fe_add(fe_dbl(pv), pv), one));
+    const fe sB = fe_mul_s(fe_mul_s(cs, is0 ? pv : fe_sub(fe_add(fe_dbl(pv), pv), one)),
+                           is0 ? E1 : fe_sub(fe_dbl(E1), E0));
     const fe s2 = bcast_fe(sB, 1);
     MLH_TAIL_TS(tb + 2);
-    fe rr = fe_zero();
-    if (lane == 0) {
+    fe rr = fe_zero(), e0 = fe_zero(), c1 = fe_zero(), c2 = fe_zero();
+    if (is0) {
       const fe s1 = sB;
       e0 = fe_sub(v, s1);
       c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
@@ -981,11 +972,17 @@ __device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_
       fe_store(rs + tt, rr);
     }
     rr = bcast_fe(rr, 0);
-#pragma unroll
-    for (uint32_t u = 0; u < 3; ++u)
-      if (u == tt) r[u] = rr;
-    rp = rr;
-    pp = pv;
+    if (tt == 0) r[0] = rr; else if (tt == 1) r[1] = rr; else r[2] = rr;
+    // the next round's factor slot tt: r_t's in place of p_{t+1}'s
+    const fe f = bt ? rr : fe_sub(one, rr);
+    if (tt == 0) F0 = f; else if (tt == 1) F1 = f;
+    // step A of the next round: lane 0 the claim e0 + r (c1 + c2 r), lane 1
+    // the scale c ((1 - p) + r (2p - 1)), corner lanes X F0 F1
+    P = e0;  // zero off lane 0
+    Q = is0 ? rr : (is1 ? v : Q);
+    R = is0 ? c1 : (is1 ? fe_sub(one, pv) : fe_zero());
+    S = is0 ? c2 : (is1 ? rr : F0);
+    T = is0 ? rr : (is1 ? fe_sub(fe_dbl(pv), one) : F1);
     MLH_TAIL_TS(tb + 7);
   }
 }
