@@ -108,7 +108,8 @@ mlh_status mlh_ntt(mlh_ctx* ctx, const void* dev_coeffs, void* dev_evals, uint32
  * winter-math's inverse) and scales by 1/n.  Generators as mlh_ntt. */
 mlh_status mlh_intt(mlh_ctx* ctx, const void* dev_evals, void* dev_coeffs, uint32_t log_n,
                     const uint8_t gen[16]);
-/* bit_reverse_permutation (ntt/mod.rs:113-123), out of place (in != out). */
+/* bit_reverse_permutation (ntt/mod.rs:113-123), out of place (in != out);
+ * log_n >= 1 (n = 1 panics in the reference: MLH_ERR_NOT_POW2). */
 mlh_status mlh_bit_reverse_permutation(mlh_ctx* ctx, const void* dev_in, void* dev_out,
                                        uint32_t log_n);
 /* Vec -> Vec convenience (host buffers, includes PCIe copies). */

@@ -403,6 +403,9 @@ mlh_status mlh_bit_reverse_permutation(mlh_ctx* ctx, const void* dev_in, void* d
   if (!ctx || !dev_in || !dev_out || dev_in == dev_out)
     return fail(ctx, MLH_ERR_INVALID, "bit_reverse_permutation is out of place");
   if (log_n > 40) return fail(ctx, MLH_ERR_INVALID, "log_n too large");
+  // n = 1 has no bit reversal in the reference (a usize shifted by 64: a
+  // panic); n >= 2 as there
+  if (log_n == 0) return fail(ctx, MLH_ERR_NOT_POW2, "bit_reverse_permutation needs n >= 2");
   HIP_TRY(ctx, launch_bitrev(reinterpret_cast<const fe*>(dev_in), reinterpret_cast<fe*>(dev_out),
                              log_n, ctx->stream));
   return MLH_OK;

@@ -163,11 +163,15 @@ def test_ntt_any_generator_vs_c_oracle(log_n):
 
 
 def test_bit_reverse_and_generator_powers():
-    vals = rand_vals(1 << 10, 7)
-    got = host(MN.bit_reverse_permutation(dev(vals)))
-    want = list(vals)
-    ON.bit_reverse_permutation(want)
-    assert got == want
+    for ln in (1, 2, 10):
+        vals = rand_vals(1 << ln, 7 + ln)
+        got = host(MN.bit_reverse_permutation(dev(vals)))
+        want = list(vals)
+        ON.bit_reverse_permutation(want)
+        assert got == want
+    with pytest.raises(_lib.MlhError) as e:  # n = 1: a panic in the reference
+        MN.bit_reverse_permutation(dev([5]))
+    assert e.value.status == _lib.MLH_ERR_NOT_POW2
     for ls in (3, 12, 13):
         assert host(MN.pow_2_generator_powers(ls)) == F.pow_2_generator_powers(ls)
     assert MN.pow_2_generator(40) == F.WINTER_TWO_ADIC_ROOT
