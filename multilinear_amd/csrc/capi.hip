@@ -147,8 +147,8 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
     tb->loga[p] = loga;
     MLH_TRY(get_table2d(ctx, ws, R, 1ull << loga, 1, p == 0 ? scale : (u128)1, &tb->ta[p]));
     tb->tb[p] = nullptr;
-    if (logw > loga)
-      MLH_TRY(get_table2d(ctx, ws, R, 1ull << (logw - loga), 1ull << loga, 1, &tb->tb[p]));
+    if (logw > loga)  // expanded: the kernel multiplies by it with the expanded product
+      MLH_TRY(get_table2d(ctx, ws, R, 1ull << (logw - loga), 1ull << loga, 1, &tb->tb[p], true));
     S <<= tb->logr[p];
   }
   return MLH_OK;

@@ -18,7 +18,8 @@
 //     DIT output is in natural order;
 //   * passes p < P multiply by the inter-pass twiddle w^(j_rest*k*S_p), read
 //     from one table TA[k][j_rest] or, when that would exceed 2^22 entries,
-//     TA[k][j_lo] * TB[k][j_hi] (TB staged through LDS: one j_hi per tile);
+//     TA[k][j_lo] * TB[k][j_hi] (TB expanded, staged through LDS: one j_hi
+//     per tile);
 //     for the inverse, pass 0's TA carries the n^-1 scale (no extra pass);
 //   * stage twiddles: expanded tables (fe_mul_pre), the lane-dependent ones
 //     read from a per-workgroup LDS copy;
@@ -89,9 +90,6 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 #ifndef MLH_LDS_TW
 #define MLH_LDS_TW 1  // stage twiddles of the lane-dependent phases read from an LDS copy
 #endif
-#ifndef MLH_LDS_TB
-#define MLH_LDS_TB 1  // two-table passes: the tile's TB column staged through LDS
-#endif
 constexpr int pass_waves_per_simd(int logr, int ept) {
   return ept == 16 ? 2 : (logr == 8 ? MLH_WPS8 : (logr == 9 ? 4 : (logr == 7 ? 4 : 2)));
 }
@@ -160,21 +158,6 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   const fe* src = in + base + ((uint64_t)c << cshift);
   fe* dst = out + base + ((uint64_t)c << cshift);
 
-#if MLH_LDS_TB
-  // Two-table twiddle: TB[k][jh] has one jh for the tile's 8 columns (loga >=
-  // 3), so the 8 lanes of a row read the same entry.  One row per thread is
-  // loaded here (its latency hides behind the phases) and shared through LDS
-  // in the epilogue: 8 lane-replicated global loads per thread become 1.
-  constexpr int kTbPerThread = (TW == 0) ? R / (kCols * R / EPT) : 1;
-  fe tbv[kTbPerThread];
-  if constexpr (TW == 0) {
-    constexpr int NT = kCols * R / EPT;
-    const uint64_t jh = jrest >> g.loga;
-    const uint32_t ltcols = g.lstride - g.loga;
-#pragma unroll
-    for (int e = 0; e < kTbPerThread; ++e) tbv[e] = fe_load(tb + ((uint64_t)(e * NT + tid) << ltcols) + jh);
-  }
-#endif
 
   // ---- phase 1: load bit-reversed rows, stages 0..2 in registers ---------
   fe x[EPT];
@@ -328,15 +311,41 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   }
 
   // ---- epilogue: inter-pass twiddle, store --------------------------------
-#if MLH_LDS_TB
+  // the first pair's inter-pass twiddles, issued before the epilogue's
+  // barriers so that their latency overlaps them (the asm products below keep
+  // later loads from being hoisted, so each pair's are issued one pair ahead)
+  const uint64_t jl = jrest & ((1ull << g.loga) - 1);
+  fe ta_c0, ta_c1;
+  if constexpr (!LAST) {
+    ta_c0 = fe_load(ta + ((uint64_t)pos[0] << g.loga) + jl);
+    ta_c1 = fe_load(ta + ((uint64_t)pos[1] << g.loga) + jl);
+  }
+  // Two-table twiddle: TB[k][jh] has one jh for the tile's 8 columns (loga >=
+  // 3), so the 8 lanes of a row read the same entry: one row per thread is
+  // loaded (with the first pair's TA, its latency overlapping the barrier) and
+  // shared through the idle exchange tile.  TB is stored EXPANDED (the 4
+  // limb-shifted multiples, as the stage twiddles), so its product is the
+  // 43-VALU expanded one (bfly_pp_v) instead of the 62-VALU full product.
   if constexpr (TW == 0) {
     constexpr int NT = kCols * R / EPT;
+    constexpr int kTbPerThread = R / NT;
+    static_assert(4 * R <= R * kCols, "the expanded TB column fits the exchange tile");
+    const uint64_t jh = jrest >> g.loga;
+    const uint32_t ltcols = g.lstride - g.loga;
+    fe tbv[kTbPerThread][4];
+#pragma unroll
+    for (int e = 0; e < kTbPerThread; ++e) {
+      const fe* q = tb + ((((uint64_t)(e * NT + tid) << ltcols) + jh) << 2);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tbv[e][k] = fe_load(q + k);
+    }
     __syncthreads();  // every lane's reads of the exchange tile are done
 #pragma unroll
-    for (int e = 0; e < kTbPerThread; ++e) lds[e * NT + tid] = tbv[e];
+    for (int e = 0; e < kTbPerThread; ++e)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lds[4 * (e * NT + tid) + k] = tbv[e][k];
     __syncthreads();
   }
-#endif
   uint64_t kbase = 0;
   uint32_t kshift = 0;
   if (LAST) {
@@ -348,23 +357,19 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     // consecutive jl, so a wave's lanes read 8 runs of 128 B per table.  The
     // products run two elements per generated asm statement (relaxed result;
     // bfly_asm.hpp), and the next pass takes relaxed input.
-    const uint64_t jl = jrest & ((1ull << g.loga) - 1);
 #pragma unroll
     for (int e = 0; e < EPT; e += 2) {
       uint64_t rare;
-      const fe a0 = fe_load(ta + ((uint64_t)pos[e] << g.loga) + jl);
-      const fe a1 = fe_load(ta + ((uint64_t)pos[e + 1] << g.loga) + jl);
+      const fe a0 = ta_c0, a1 = ta_c1;
+      if (e + 2 < EPT) {  // the next pair's, in flight during this pair's products
+        ta_c0 = fe_load(ta + ((uint64_t)pos[e + 2] << g.loga) + jl);
+        ta_c1 = fe_load(ta + ((uint64_t)pos[e + 3] << g.loga) + jl);
+      }
       bfly_ff_v(x[e], a0, x[e + 1], a1, rare);
       if constexpr (TW == 0) {
-#if MLH_LDS_TB
-        const fe b0 = lds[pos[e]], b1 = lds[pos[e + 1]];
-#else
-        const uint32_t ltcols = g.lstride - g.loga;
-        const uint64_t jh = jrest >> g.loga;
-        const fe b0 = fe_load(tb + ((uint64_t)pos[e] << ltcols) + jh);
-        const fe b1 = fe_load(tb + ((uint64_t)pos[e + 1] << ltcols) + jh);
-#endif
-        bfly_ff_v(x[e], b0, x[e + 1], b1, rare);
+        const fe* b0 = lds + 4 * pos[e];
+        const fe* b1 = lds + 4 * pos[e + 1];
+        bfly_pp_v(x[e], b0[0], b0[1], b0[2], b0[3], x[e + 1], b1[0], b1[1], b1[2], b1[3], rare);
       }
       fe_store(dst + ((uint64_t)pos[e] << rshift), x[e]);
       fe_store(dst + ((uint64_t)pos[e + 1] << rshift), x[e + 1]);
