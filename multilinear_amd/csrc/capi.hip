@@ -210,7 +210,9 @@ static mlh_status ntt_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, 
     return MLH_OK;
   }
   MLH_TRY(ensure_ntt_scratch(ctx, log_n));
-  if (prof_sample(ctx)) {
+  char lab0[64];
+  if (ctx->prof_on) ntt_pass_label(tb, 0, zero_top, lab0, sizeof lab0);
+  if (ctx->prof_on && prof_sample(ctx, lab0)) {
     std::vector<hipEvent_t> ev(tb.nradix + 1);
     for (auto& e : ev) e = take_event(ctx);
     HIP_TRY(ctx, launch_ntt_passes(in, out, ctx->ntt_scratch, tb, log_n, zero_top, ctx->stream,
@@ -1661,7 +1663,7 @@ mlh_status mlh_profile_enable(mlh_ctx* ctx, int on) {
   if (!ctx || on < 0) return MLH_ERR_INVALID;
   ctx->prof_on = on != 0;
   ctx->prof_every = on > 1 ? (uint32_t)on : 1u;
-  ctx->prof_tick = 0;
+  ctx->prof_ticks.clear();
   return MLH_OK;
 }
 

@@ -10,6 +10,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <tuple>
 #include <vector>
 
@@ -67,8 +68,8 @@ struct mlh_ctx {
   uint32_t forced_plan_len = 0;
   // kernel timer (mlh_profile_*): HIP events on the launch stream
   bool prof_on = false;
-  uint32_t prof_every = 1;  // bracket every prof_every-th transform / launch
-  uint64_t prof_tick = 0;
+  uint32_t prof_every = 1;  // bracket every prof_every-th transform / launch of each label
+  std::unordered_map<std::string, uint64_t> prof_ticks;
   std::vector<hipEvent_t> ev_free;
   struct Pending {
     std::string label;
@@ -111,9 +112,12 @@ inline void resolve_profile(mlh_ctx* ctx) {
 }
 
 // Whether the kernel timer brackets this transform / launch: every
-// prof_every-th one while enabled (the events cost the stream a few us each).
-inline bool prof_sample(mlh_ctx* ctx) {
-  return ctx->prof_on && ctx->prof_tick++ % ctx->prof_every == 0;
+// prof_every-th one of its label while enabled (the events cost the stream a
+// few us each; counting per label keeps interleaved kinds all sampled).
+inline bool prof_sample(mlh_ctx* ctx, const char* label) {
+  if (!ctx->prof_on) return false;
+  if (ctx->prof_every <= 1) return true;
+  return ctx->prof_ticks[label]++ % ctx->prof_every == 0;
 }
 
 // Kernel-timer bracket around one launch (no-op unless mlh_profile_enable).
@@ -122,7 +126,7 @@ struct ProfScope {
   const char* label;
   hipEvent_t a = nullptr;
   ProfScope(mlh_ctx* c, const char* lab) : ctx(c), label(lab) {
-    if (prof_sample(ctx)) {
+    if (prof_sample(ctx, label)) {
       a = take_event(ctx);
       (void)hipEventRecord(a, ctx->stream);
     }
