@@ -140,7 +140,7 @@ def test_reed_solomon_any_generator_matches_oracle(log_n):
         assert host(MF.reed_solomon_brev(dev([vals[perm[i]] for i in range(n)]), g)) == want, g
 
 
-@pytest.mark.parametrize("log_n", [15, 16, 20])
+@pytest.mark.parametrize("log_n", [15, 16, 20, 22])
 def test_ntt_any_generator_vs_c_oracle(log_n):
     """Past the LDS block (2^11): the register stage launches (4 + 4 + 1 stages
     at 2^20), in and out of place, forward and inverse, RS with an order-N
