@@ -5,10 +5,11 @@ Metric: "NTT 2^24 field-elems/sec + FRI commit ms; % HBM roofline".
             over a device-resident synthetic vector (seeded uniform elements);
   * N > 1 (default --mode sharded): one forward NTT of N * 2^24 points per
             step, 2^24 per GPU: local NTT, one RCCL all-to-all over xGMI,
-            cross-shard DFT kernel (multilinear_amd/dist.py); the K steps
-            stream through dist.NttPipeline so the exchange of step i overlaps
-            the local NTT of step i+1 (every exchange and cross kernel
-            completes inside the timed region); weak scaling (2^24 per GPU);
+            cross-shard DFT kernel; the K steps are one
+            mlh_sharded_ntt_batch call of the C ABI (csrc/sharded.hip), whose
+            two streams overlap the exchange of step i with the local NTT of
+            step i+1 (every exchange and cross kernel completes inside the
+            timed region); weak scaling (2^24 per GPU);
   * N > 1, --mode replicas: every rank transforms its own 2^24-point
             polynomial per step (no data-path collective; reported as the
             extra "replicas_ntt" in the default mode);
@@ -274,22 +275,17 @@ def main():
     def ntt_local():
         D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(out), log_n, gen), ctx)
 
-    pipe = None
-    if world > 1:
-        from multilinear_amd import dist as DS
+    batch = None
+    if world > 1:  # the C ABI's pipelined sharded NTT over libmlhip's RCCL communicator
+        batch = _ShardedBatch(lib, ctx, _transport(local), x, out, log_n + log_p, local)
 
-        tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
-        g_total = int.from_bytes(bytes(_gen(lib, log_n + log_p)), "little")
-        pipe = DS.NttPipeline(log_n + log_p, g_total, tp, ops)
-
-    def ntt_sharded():  # x: this rank's cyclic shard of the N * 2^24 vector; the
-        pipe.submit(x)  # exchange of step i overlaps the local NTT of step i+1
-
-    ntt_once = ntt_sharded if sharded else ntt_local
-
-    def ntt_drain():
+    def run_steps(k):
+        """k headline steps, enqueued (x: this rank's shard / polynomial)."""
         if sharded:
-            pipe.drain()
+            batch.run(k)  # one mlh_sharded_ntt_batch call: k pipelined transforms
+        else:
+            for _ in range(k):
+                ntt_local()
 
     def barrier():
         torch.cuda.synchronize()
@@ -299,30 +295,22 @@ def main():
 
     # setup (not a step): tables, allocator, clock ramp.  The iteration count
     # is agreed over ranks so the sharded step's collectives stay matched.
-    ntt_once()
-    ntt_drain()
+    run_steps(1)
     barrier()
     t_one = time.perf_counter()
-    ntt_once()
-    ntt_drain()
+    run_steps(1)
     torch.cuda.synchronize()
     iters = int(args.spinup_s / max(time.perf_counter() - t_one, 1e-5)) + 1
     if dist is not None:
         iters = int(_allreduce_max(iters))
-    for _ in range(min(iters, 5000)):
-        ntt_once()
-    ntt_drain()
+    run_steps(min(iters, 5000))
     barrier()
-    for _ in range(args.warmup):
-        ntt_once()
-    ntt_drain()
+    run_steps(args.warmup)
     barrier()
     lib.mlh_profile_reset(ctx)
     lib.mlh_profile_enable(ctx, max(1, args.prof_every))
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ntt_once()
-    ntt_drain()
+    run_steps(args.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     lib.mlh_profile_enable(ctx, 0)
@@ -584,7 +572,7 @@ def main():
             result["config5_error"] = "%s: %s" % (type(e).__name__, e)
         if world > 1 and not sharded:
             try:
-                result["sharded_ntt"] = sharded_ntt_extra(args, pipe, x, world, barrier, log_n,
+                result["sharded_ntt"] = sharded_ntt_extra(args, batch, world, barrier, log_n,
                                                           log_p, lib, ctx)
             except Exception as e:
                 result["sharded_ntt_error"] = "%s: %s" % (type(e).__name__, e)
@@ -661,22 +649,50 @@ class _ExtrasWatchdog:
         os._exit(0)
 
 
-def sharded_ntt_extra(args, pipe, x, world, barrier, log_n, log_p, lib, ctx):
+class _ShardedBatch:
+    """k sharded forward NTTs of the rank's shard as ONE mlh_sharded_ntt_batch
+    call (C ABI, csrc/sharded.hip): outputs alternate between two buffers;
+    the pointer arrays are built once per k, outside any timed region."""
+
+    def __init__(self, lib, ctx, transport, x, out, log_total, local):
+        from multilinear_amd import device as D
+
+        self.lib, self.ctx, self.tp, self.log_total = lib, ctx, transport, log_total
+        self.x, self.outs = x, [out, D.empty(x.shape[0], local)]
+        self.gen = D.fe_bytes(int.from_bytes(bytes(_gen(lib, log_total)), "little"))
+        self.arrays = {}
+
+    def prepare(self, k):
+        if k not in self.arrays:
+            ins = (ctypes.c_void_p * max(1, k))(*([self.x.data_ptr()] * k))
+            outs = (ctypes.c_void_p * max(1, k))(*[self.outs[i & 1].data_ptr() for i in range(k)])
+            self.arrays[k] = (ins, outs)
+        return self.arrays[k]
+
+    def run(self, k):
+        from multilinear_amd import device as D
+
+        if k <= 0:
+            return
+        ins, outs = self.prepare(k)
+        D.check(self.lib.mlh_sharded_ntt_batch(self.ctx, ctypes.byref(self.tp.transport), ins, outs, k,
+                                               self.log_total, self.gen, 0), self.ctx)
+
+
+def sharded_ntt_extra(args, batch, world, barrier, log_n, log_p, lib, ctx):
     """The all-to-all sharded NTT (north star: "the NTT shards across the GPUs
     via an RCCL all-to-all transpose"): N*2^24 points per step, 2^24 per GPU,
-    steps streamed through dist.NttPipeline; same K / W as the headline."""
+    the K steps one pipelined mlh_sharded_ntt_batch call; same K / W as the
+    headline."""
     import torch
 
-    for _ in range(max(1, args.warmup)):
-        pipe.submit(x)
-    pipe.drain()
+    batch.run(max(1, args.warmup))
+    batch.prepare(args.steps)
     barrier()
     lib.mlh_profile_reset(ctx)
     lib.mlh_profile_enable(ctx, max(1, args.prof_every))
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pipe.submit(x)
-    pipe.drain()
+    batch.run(args.steps)
     torch.cuda.synchronize()
     dt = _allreduce_max(time.perf_counter() - t0)
     lib.mlh_profile_enable(ctx, 0)
@@ -751,23 +767,21 @@ def strong_ntt(args, lib, ctx, local, world, rank, barrier):
 
 def config4_sharded(args, local, world, rank, barrier):
     """Config 4 over the N ranks (strong scaling): 2^24-entry MLE in the cyclic
-    layout, sharded eq table + 24 sumcheck rounds (multilinear_amd/dist.py)."""
+    layout, sharded eq table + 24 sumcheck rounds; and config 3 sharded
+    (RS LDE + commit root); all through the C ABI's mlh_sharded_*."""
     import random
 
     import torch
 
     from multilinear_amd import device as D
-    from multilinear_amd import dist as DS
+    from multilinear_amd import sharded as SH
     from multilinear_amd.transcript import Transcript
 
-    from multilinear_amd import sharded as SH
-
     n = args.log_n
-    tp, ops = DS.Transport(host_staged=BACKEND != "nccl"), DS.HipOps(local)
     tr = _transport(local)
     rr = random.Random(5)
     pts = [rr.randrange(D.M) for _ in range(n)]
-    base = D.random_device(1 << (n - tp.world.bit_length() + 1), 500 + rank, local)
+    base = D.random_device(1 << (n - world.bit_length() + 1), 500 + rank, local)
 
     def run():  # the C-ABI schedule over libmlhip's RCCL communicator
         m = base.clone()
@@ -775,12 +789,12 @@ def config4_sharded(args, local, world, rank, barrier):
         return SH.sumcheck_prove(m, d, n, 0, Transcript(), tr, local)
 
     # config 3 sharded: RS LDE of 2^n coefficients + Merkle root over the ranks
-    coeffs = D.random_device(1 << (n - tp.world.bit_length() + 1), 700 + rank, local)
+    coeffs = D.random_device(1 << (n - world.bit_length() + 1), 700 + rank, local)
     g2 = int.from_bytes(bytes(_gen(D.lib(), n + 1)), "little")
 
     def commit():
-        code = DS.reed_solomon(coeffs, n, g2, tp, ops)
-        return DS.commit_rs_code(code, n + 1, tp, ops)
+        code = SH.reed_solomon(coeffs, n, g2, tr, local)
+        return SH.commit_rs_code(code, n + 1, tr, local)
 
     commit()
     barrier()
@@ -858,13 +872,12 @@ def _transport(local):
     communicator (unique id broadcast over the torch.distributed group); in a
     gloo rehearsal, torch collectives as host callbacks."""
     if not _TRANSPORT:
-        from multilinear_amd import dist as DS
         from multilinear_amd import sharded as SH
 
         if BACKEND == "nccl":
             _TRANSPORT.append(SH.RcclComm.from_torch(device=local))
         else:
-            _TRANSPORT.append(SH.HostTransport(DS.Transport(host_staged=True), local))
+            _TRANSPORT.append(SH.HostTransport(SH.Transport(host_staged=True), local))
     return _TRANSPORT[0]
 
 

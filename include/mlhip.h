@@ -156,6 +156,15 @@ mlh_status mlh_fri_fold(mlh_ctx* ctx, const void* dev_layer, uint32_t log_layer,
  * log2(gen_pows.len())) for any geometric table of a generator of order exactly
  * gen_pows.len() (MLH_ERR_BAD_GENERATOR otherwise; MLH_ERR_INVALID when the
  * table is shorter than half the code, where the reference's index underflows). */
+/* The shim from the reference's gen_pows: &[F] (fri/mod.rs:79, :136, :261) to
+ * the _gp arguments: checks that the host table of len entries is a power
+ * series 1, g, g^2, ... of a g of order exactly len (len a power of two >= 2;
+ * gen_pows[0] = 1, gen_pows[2^j] = g^(2^j) for every j, gen_pows[len/2] = -1,
+ * gen_pows[len-1] * g = 1) and returns (g, log2(len)); MLH_ERR_INVALID for
+ * any other table -- which the reference would fold with silently, so a caller
+ * maps it to a panic rather than to a different proof. */
+mlh_status mlh_gen_pows_params(const uint8_t* gen_pows, uint64_t len, uint8_t gen_out[16],
+                               uint32_t* log_len_out);
 mlh_status mlh_fri_prover_init(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
                                mlh_transcript* tr, mlh_fri_prover** out); /* :58-76  */
 mlh_status mlh_fri_prover_init_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
@@ -469,10 +478,25 @@ mlh_status mlh_comm_transport(mlh_comm* comm, mlh_transport* out);
  * returns block 2^log_n / P^2; inverse != 0 the reverse.  One all-to-all. */
 mlh_status mlh_sharded_ntt(mlh_ctx* ctx, const mlh_transport* tp, const void* dev_in, void* dev_out,
                            uint32_t log_n, const uint8_t gen[16], int inverse);
+/* count sharded NTTs (or INTTs) of 2^log_n vectors, dev_in[i] -> dev_out[i]
+ * with mlh_sharded_ntt's layouts, pipelined on two streams: the all-to-all of
+ * transform i (and the local step after it) runs on the context's second
+ * stream while the first local step of transform i + 1 runs on the context
+ * stream.  On return the context stream is ordered after all of them.  This is
+ * Polynomial::ntt (ntt/mod.rs:69-110) called on count polynomials in turn. */
+mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* tp, const void* const* dev_in,
+                                 void* const* dev_out, uint32_t count, uint32_t log_n,
+                                 const uint8_t gen[16], int inverse);
 /* reed_solomon (fri/mod.rs:19-28): 2^log_n coefficients in the cyclic layout,
  * gen of order 2^(log_n + 1) -> the codeword in block 2^(log_n + 1) / P^2. */
 mlh_status mlh_sharded_reed_solomon(mlh_ctx* ctx, const mlh_transport* tp, const void* dev_coeffs,
                                     uint32_t log_n, const uint8_t gen[16], void* dev_code);
+/* commit_rs_code (fri/mod.rs:45-55) + Merkle::commit (merkle_tree/mod.rs:65-85)
+ * of a 2^log_code codeword in the block 2^log_code / P^2 layout: local leaves
+ * and subtrees, one all-gather of the subtree roots, the top levels on every
+ * rank; root_out (host) = the root of the natural-order codeword's tree. */
+mlh_status mlh_sharded_commit_rs_code(mlh_ctx* ctx, const mlh_transport* tp, const void* dev_code,
+                                      uint32_t log_code, uint8_t root_out[32]);
 /* FriProof::prove (fri/mod.rs:261-285) of a 2^log_code codeword in the block
  * 2^log_code / P^2 layout (mlh_sharded_reed_solomon's output); layers below
  * 2^gather_log entries are gathered and finished replicated (16 is a good
@@ -486,8 +510,13 @@ mlh_status mlh_sharded_fri_prove(mlh_ctx* ctx, const mlh_transport* tp, const vo
 mlh_status mlh_sharded_eq_table(mlh_ctx* ctx, const mlh_transport* tp, const uint8_t* points,
                                 uint32_t n, void* dev_out);
 /* compute_sumcheck_polynomials (sumcheck.rs:77-102), composition x[0], of
- * tables in the cyclic layout (folded in place); polys_out [n][2][16],
- * rs_out [n][16] as mlh_sumcheck_prove. */
+ * tables in the cyclic layout; polys_out [n][2][16], rs_out [n][16] as
+ * mlh_sumcheck_prove.  The local tables are folded in place while they hold
+ * >= 2 entries (the last log2 P rounds fold gathered copies); on return entry
+ * 0 of every rank's dev_m / dev_d holds the fully folded m(r) / d(r), the
+ * length-1 tables the reference ends with.  The RCCL transport (mlh_comm) at
+ * P > 1 has run only on the driver's multi-GPU node; the tests drive these
+ * entry points at P > 1 through a host-side transport. */
 mlh_status mlh_sharded_sumcheck_prove(mlh_ctx* ctx, const mlh_transport* tp, void* dev_m, void* dev_d,
                                       uint32_t n, const uint8_t sum[16], mlh_transcript* tr,
                                       uint8_t* polys_out, uint8_t* rs_out);

@@ -202,7 +202,11 @@ SIGNATURES = {
     "mlh_comm_destroy": (None, [_P]),
     "mlh_comm_transport": (_I, [_P, ctypes.POINTER(TransportC)]),
     "mlh_sharded_ntt": (_I, [_P, ctypes.POINTER(TransportC), _P, _P, _U32, _P, _I]),
+    "mlh_gen_pows_params": (_I, [_P, _U64, _P, ctypes.POINTER(_U32)]),
+    "mlh_sharded_ntt_batch": (_I, [_P, ctypes.POINTER(TransportC), ctypes.POINTER(_P),
+                                   ctypes.POINTER(_P), _U32, _U32, _P, _I]),
     "mlh_sharded_reed_solomon": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _P, _P]),
+    "mlh_sharded_commit_rs_code": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _P]),
     "mlh_sharded_fri_prove": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _U32, _P,
                                    ctypes.POINTER(FriProofC)]),
     "mlh_sharded_eq_table": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _P]),

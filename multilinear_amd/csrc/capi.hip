@@ -183,15 +183,16 @@ static mlh_status ensure_ntt_scratch(mlh_ctx* ctx, uint32_t log_n) {
 static mlh_status ntt_network_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t log_n, u128 gen,
                                    bool inverse, int zero_top) {
   const u128 w = inverse ? h_inv(gen) : gen;
-  const fe* pw;
-  MLH_TRY(get_table(ctx, w, 1ull << (log_n - 1), 1, &pw));
+  const fe *tlo, *thi;  // w^t = tlo[t mod 4096] thi[t >> 12], t < N/2
+  MLH_TRY(get_table(ctx, w, 4096, 1, &tlo));
+  MLH_TRY(get_table(ctx, h_pow(w, 4096), hi_count(log_n - 1), 1, &thi));
   fe* scratch = nullptr;
   if (in == out && log_n > 11) {
     MLH_TRY(ensure_ntt_scratch(ctx, log_n));
     scratch = ctx->ntt_scratch;
   }
   const u128 scale = inverse ? h_inv((u128)1 << log_n) : (u128)1;
-  HIP_TRY(ctx, launch_ntt_network(in, out, scratch, pw, log_n, zero_top, to_fe(scale), inverse,
+  HIP_TRY(ctx, launch_ntt_network(in, out, scratch, tlo, thi, log_n, zero_top, to_fe(scale), inverse,
                                   ctx->stream));
   return MLH_OK;
 }
@@ -263,6 +264,10 @@ void mlh_context_destroy(mlh_ctx* ctx) {
   for (auto& kv : ctx->pool) (void)hipFree(kv.second);
   for (auto& kv : ctx->live) (void)hipFree(kv.first);
   (void)hipFree(ctx->ntt_scratch);
+  if (ctx->side) {
+    (void)hipStreamSynchronize(ctx->side);
+    (void)hipStreamDestroy(ctx->side);
+  }
   (void)hipFree(ctx->partials);
   (void)hipFree(ctx->small);
   (void)hipHostFree(ctx->pinned);
@@ -336,6 +341,23 @@ mlh_status mlh_memcpy_d2d(mlh_ctx* ctx, void* dst, const void* src, size_t bytes
 mlh_status mlh_pow_2_generator(uint32_t log_size, uint8_t gen_out[16]) {
   if (!gen_out || log_size > 40) return MLH_ERR_INVALID;
   h_store(gen_out, h_pow2_generator(log_size));
+  return MLH_OK;
+}
+
+mlh_status mlh_gen_pows_params(const uint8_t* gen_pows, uint64_t len, uint8_t gen_out[16],
+                               uint32_t* log_len_out) {
+  if (!gen_pows || !gen_out || !log_len_out) return MLH_ERR_INVALID;
+  if (len < 2 || (len & (len - 1)) || len > (1ull << 40)) return MLH_ERR_INVALID;
+  const uint32_t lg = 63 - __builtin_clzll(len);
+  auto at = [&](uint64_t i) { return h_load(gen_pows + 16 * i); };
+  const u128 g = at(1);
+  if (at(0) != 1 || !check_generator(g, lg)) return MLH_ERR_INVALID;  // order exactly len
+  u128 p = g;
+  for (uint32_t j = 0; j < lg; ++j, p = h_mul(p, p))
+    if (at(1ull << j) != p) return MLH_ERR_INVALID;  // gen_pows[2^j] = g^(2^j)
+  if (at(len / 2) != kModulus - 1 || h_mul(at(len - 1), g) != 1) return MLH_ERR_INVALID;
+  h_store(gen_out, g);
+  *log_len_out = lg;
   return MLH_OK;
 }
 
@@ -1050,7 +1072,7 @@ mlh_status mlh_fri_prover_open_queries(mlh_ctx* ctx, const mlh_fri_prover* p,
 }
 
 // ---------------------------------------------------------------------------
-// sharded building blocks (dist.hip; orchestration in multilinear_amd/dist.py)
+// sharded building blocks (dist.hip; orchestration in tests/dist_spec.py)
 // ---------------------------------------------------------------------------
 mlh_status mlh_shard_ntt_cross(mlh_ctx* ctx, const void* dev_in, void* dev_out, uint32_t log_n,
                                uint32_t log_p, uint32_t rank, const uint8_t gen[16], int inverse) {
@@ -1859,7 +1881,7 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
 
 // ---------------------------------------------------------------------------
 // device-resident transcript + sharded steps that read the challenge from HBM
-// (multilinear_amd/dist.py fri_prove: no host round trip inside the fold loop)
+// (tests/dist_spec.py fri_prove: no host round trip inside the fold loop)
 // ---------------------------------------------------------------------------
 extern "C" {
 
@@ -1957,7 +1979,7 @@ mlh_status mlh_merkle_top(mlh_ctx* ctx, const void* dev_gathered, uint32_t P, ui
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
-// device-resident sumcheck steps (sharded sumcheck in multilinear_amd/dist.py)
+// device-resident sumcheck steps (sharded sumcheck in tests/dist_spec.py)
 // ---------------------------------------------------------------------------
 extern "C" {
 

@@ -61,6 +61,7 @@ struct mlh_ctx {
   size_t qstage_bytes = 0;
   fe* ntt_scratch = nullptr;          // NTT ping-pong buffer (grow-only)
   size_t ntt_scratch_bytes = 0;
+  hipStream_t side = nullptr;         // second stream of pipelined calls (lazy)
   // debug / test hooks, fixed at creation (MLH_DEBUG_SYNC) or set through the
   // API (mlh_set_ntt_plan): never read from the environment on a hot path
   bool debug_sync = false;
@@ -138,6 +139,10 @@ struct ProfScope {
     ctx->pending.push_back(mlh_ctx::Pending{label, a, b});
     a = nullptr;
   }
+  // an early error return skipped end(): recycle the start event
+  ~ProfScope() {
+    if (a) ctx->ev_free.push_back(a);
+  }
 };
 
 
@@ -145,6 +150,15 @@ inline mlh_status fail(mlh_ctx* ctx, mlh_status st, const std::string& msg) {
   if (ctx) ctx->err = msg;
   return st;
 }
+
+// Runs the enclosed entry-point calls on another stream: every launch and
+// copy of the library goes to ctx->stream, which is swapped for the scope.
+struct StreamSwap {
+  mlh_ctx* ctx;
+  hipStream_t saved;
+  StreamSwap(mlh_ctx* c, hipStream_t s) : ctx(c), saved(c->stream) { c->stream = s; }
+  ~StreamSwap() { ctx->stream = saved; }
+};
 
 #define HIP_TRY(ctx, expr)                                                                \
   do {                                                                                    \

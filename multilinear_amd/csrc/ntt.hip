@@ -484,10 +484,20 @@ __global__ void pow_series_kernel(fe* __restrict__ out, const fe* __restrict__ t
 // four-step passes above (which rely on that) cannot reproduce it.  These
 // kernels run the same butterfly network stage by stage: the first kNetLB
 // stages per LDS-resident block of 2^kNetLB positions, the rest up to 4 per
-// launch in registers.  pw[t] = w^t (t < N/2); stage s (len = 2^(s+1)) uses
-// pw[j << (log_n - 1 - s)] = g_len^j, the reference's gen_pows[j] (exact: the
-// field is exact, however the power is formed).  Correctness path, not tuned.
+// launch in registers.  w^t (t < N/2) = tlo[t mod 2^12] * thi[t >> 12] (two
+// small tables instead of one of N/2 entries, which would be 32 GiB at 2^32);
+// stage s (len = 2^(s+1)) uses w^(j << (log_n - 1 - s)) = g_len^j, the
+// reference's gen_pows[j] (exact: the field is exact, however the power is
+// formed).  Correctness path, not tuned.
 constexpr uint32_t kNetLB = 11;  // 2^11 entries = 32 KiB of LDS
+
+__device__ __forceinline__ fe net_tw(const fe* __restrict__ tlo, const fe* __restrict__ thi,
+                                     uint64_t t) {
+  const uint64_t lo = t & 4095, hi = t >> 12;
+  if (!hi) return fe_load(tlo + lo);
+  if (!lo) return fe_load(thi + hi);
+  return fe_mul(fe_load(tlo + lo), fe_load(thi + hi));
+}
 
 __device__ __forceinline__ uint64_t bitrev64(uint64_t x, uint32_t bits) {
   return bits ? __builtin_bitreverse64(x) >> (64 - bits) : 0;
@@ -497,8 +507,8 @@ __device__ __forceinline__ uint64_t bitrev64(uint64_t x, uint32_t bits) {
 // resize, fri/mod.rs:19-28); 2 = as 1, coefficient c stored at
 // in[bitrev_{log_n - 1}(c)].
 __global__ void __launch_bounds__(1024)
-ntt_net_block_kernel(const fe* __restrict__ in, fe* __restrict__ out, const fe* __restrict__ pw,
-                     uint32_t log_n, uint32_t lb, int zero_top, fe scale, int apply_scale) {
+ntt_net_block_kernel(const fe* __restrict__ in, fe* __restrict__ out, const fe* __restrict__ tlo,
+                     const fe* __restrict__ thi, uint32_t log_n, uint32_t lb, int zero_top, fe scale, int apply_scale) {
   __shared__ fe lds[1u << kNetLB];
   const uint32_t B = 1u << lb;
   const uint64_t N = 1ull << log_n, base = (uint64_t)blockIdx.x << lb;
@@ -518,7 +528,7 @@ ntt_net_block_kernel(const fe* __restrict__ in, fe* __restrict__ out, const fe* 
       const uint32_t p0 = j + ((b >> s) << (s + 1));
       const fe u = lds[p0];
       fe v = lds[p0 + h];
-      if (j) v = fe_mul(v, fe_load(pw + ((uint64_t)j << (log_n - 1 - s))));  // gen_pows[0] = 1
+      if (j) v = fe_mul(v, net_tw(tlo, thi, (uint64_t)j << (log_n - 1 - s)));  // gen_pows[0] = 1
       lds[p0] = fe_add(u, v);
       lds[p0 + h] = fe_sub(u, v);
     }
@@ -537,7 +547,8 @@ ntt_net_block_kernel(const fe* __restrict__ in, fe* __restrict__ out, const fe* 
 // Runs in place (in == out) or out of place.
 template <int Q>
 __global__ void __launch_bounds__(256)
-ntt_net_stage_kernel(const fe* in, fe* out, const fe* __restrict__ pw, uint32_t log_n,
+ntt_net_stage_kernel(const fe* in, fe* out, const fe* __restrict__ tlo, const fe* __restrict__ thi,
+                     uint32_t log_n,
                      uint32_t s0, fe scale, int apply_scale) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (1ull << (log_n - Q))) return;
@@ -554,7 +565,7 @@ ntt_net_stage_kernel(const fe* in, fe* out, const fe* __restrict__ pw, uint32_t 
     for (int b = 0; b < (1 << (Q - 1)); ++b) {
       const int m = ((b >> q) << (q + 1)) | (b & (d - 1));  // pairs (m, m + d)
       const uint64_t j = (base + ((uint64_t)m << s0)) & ((1ull << s) - 1);
-      const fe v = j ? fe_mul(x[m + d], fe_load(pw + (j << (log_n - 1 - s)))) : x[m + d];
+      const fe v = j ? fe_mul(x[m + d], net_tw(tlo, thi, j << (log_n - 1 - s))) : x[m + d];
       const fe u = x[m];
       x[m] = fe_add(u, v);
       x[m + d] = fe_sub(u, v);
@@ -568,7 +579,8 @@ ntt_net_stage_kernel(const fe* in, fe* out, const fe* __restrict__ pw, uint32_t 
   }
 }
 
-hipError_t launch_ntt_network(const fe* in, fe* out, fe* scratch, const fe* pw, uint32_t log_n,
+hipError_t launch_ntt_network(const fe* in, fe* out, fe* scratch, const fe* tlo, const fe* thi,
+                              uint32_t log_n,
                               int zero_top, fe scale, bool apply_scale, hipStream_t st) {
   if (log_n < 1 || log_n > 40 || (zero_top && in == out)) return hipErrorInvalidValue;
   const uint32_t lb = log_n < kNetLB ? log_n : kNetLB;
@@ -579,7 +591,7 @@ hipError_t launch_ntt_network(const fe* in, fe* out, fe* scratch, const fe* pw, 
   const bool only = lb == log_n;
   const uint32_t threads = lb >= 11 ? 1024 : (1u << lb) / 2 < 64 ? 64 : (1u << lb) / 2;
   hipLaunchKernelGGL(ntt_net_block_kernel, dim3((unsigned)blocks), dim3(threads), 0, st, in, first,
-                     pw, log_n, lb, zero_top, scale, (only && apply_scale) ? 1 : 0);
+                     tlo, thi, log_n, lb, zero_top, scale, (only && apply_scale) ? 1 : 0);
   hipError_t e = hipGetLastError();
   for (uint32_t s0 = lb; e == hipSuccess && s0 < log_n;) {
     const uint32_t q = log_n - s0 < 4 ? log_n - s0 : 4;
@@ -588,10 +600,10 @@ hipError_t launch_ntt_network(const fe* in, fe* out, fe* scratch, const fe* pw, 
     const int sc = (last && apply_scale) ? 1 : 0;
     const dim3 grid((unsigned)(((1ull << (log_n - q)) + 255) / 256)), blk(256);
     switch (q) {
-      case 1: hipLaunchKernelGGL(ntt_net_stage_kernel<1>, grid, blk, 0, st, first, dst, pw, log_n, s0, scale, sc); break;
-      case 2: hipLaunchKernelGGL(ntt_net_stage_kernel<2>, grid, blk, 0, st, first, dst, pw, log_n, s0, scale, sc); break;
-      case 3: hipLaunchKernelGGL(ntt_net_stage_kernel<3>, grid, blk, 0, st, first, dst, pw, log_n, s0, scale, sc); break;
-      default: hipLaunchKernelGGL(ntt_net_stage_kernel<4>, grid, blk, 0, st, first, dst, pw, log_n, s0, scale, sc); break;
+      case 1: hipLaunchKernelGGL(ntt_net_stage_kernel<1>, grid, blk, 0, st, first, dst, tlo, thi, log_n, s0, scale, sc); break;
+      case 2: hipLaunchKernelGGL(ntt_net_stage_kernel<2>, grid, blk, 0, st, first, dst, tlo, thi, log_n, s0, scale, sc); break;
+      case 3: hipLaunchKernelGGL(ntt_net_stage_kernel<3>, grid, blk, 0, st, first, dst, tlo, thi, log_n, s0, scale, sc); break;
+      default: hipLaunchKernelGGL(ntt_net_stage_kernel<4>, grid, blk, 0, st, first, dst, tlo, thi, log_n, s0, scale, sc); break;
     }
     e = hipGetLastError();
     s0 += q;

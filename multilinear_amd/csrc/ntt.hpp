@@ -67,10 +67,11 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
 // rocprof-style kernel label of pass p ("ntt_pass<8,0,0>")
 void ntt_pass_label(const NttTables& tb, uint32_t p, int zero_top, char* buf, size_t n);
 // The reference's radix-2 network for any generator (ntt.hip "general-generator
-// network"): pw[t] = w^t for t < N/2; zero_top as launch_ntt_passes; scratch
-// (N elements) is used when in == out; apply_scale multiplies the outputs by
-// scale (the inverse's n^-1).
-hipError_t launch_ntt_network(const fe* in, fe* out, fe* scratch, const fe* pw, uint32_t log_n,
+// network"): w^t = tlo[t mod 4096] * thi[t >> 12] for t < N/2; zero_top as
+// launch_ntt_passes; scratch (N elements) is used when in == out; apply_scale
+// multiplies the outputs by scale (the inverse's n^-1).
+hipError_t launch_ntt_network(const fe* in, fe* out, fe* scratch, const fe* tlo, const fe* thi,
+                              uint32_t log_n,
                               int zero_top, fe scale, bool apply_scale, hipStream_t st);
 hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st,
                             bool expand = false);

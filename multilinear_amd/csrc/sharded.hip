@@ -3,9 +3,10 @@
 // implementation is RCCL over xGMI (mlh_comm, librccl).  The reference has no
 // distributed API (its prover is single-threaded: src/ntt/mod.rs:69-173,
 // src/fri/mod.rs:19-145 and :261-285, sumcheck.rs:77-247); SURVEY.md 8(e)
-// prescribes the sharding, DESIGN.md §6 describes the layouts.  These are the
-// schedules of multilinear_amd/dist.py (the executable spec the CPU gloo tests
-// run with oracle rank-local ops), in C++ so a Rust caller binds them directly.
+// prescribes the sharding, DESIGN.md §6 describes the layouts.  This is the
+// one product implementation of the schedules (a Rust caller binds it
+// directly); tests/dist_spec.py restates them in Python as the executable spec
+// the CPU gloo tests run with oracle rank-local steps.
 //
 // Layout: a sharded vector of 2^log_n elements over P = 2^log_p ranks is
 // block-cyclic with block S = 2^log_s: local l of rank r is global
@@ -115,6 +116,13 @@ struct Bufs {
 
 void store_fe(uint8_t out[16], u128 v) { h_store(out, v); }
 
+// gen has order exactly 2^log_n (the cross-shard DFT needs a DFT generator)
+bool gen_has_order(u128 gen, uint32_t log_n) {
+  if (gen >= kModulus) return false;
+  if (log_n == 0) return gen == 1;
+  return h_pow(gen, (u128)1 << (log_n - 1)) == kModulus - 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -177,6 +185,8 @@ mlh_status mlh_sharded_ntt(mlh_ctx* ctx, const mlh_transport* t, const void* dev
     return inverse ? mlh_intt(ctx, dev_in, dev_out, log_n, gen) : mlh_ntt(ctx, dev_in, dev_out, log_n, gen);
   if (log_n < 2 * tp.p + 1 || log_n > 40)
     return fail(ctx, MLH_ERR_INVALID, "sharded NTT needs 2^log_n >= 2 P^2");
+  if (!gen_has_order(h_load(gen), log_n))  // before any local work or collective
+    return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != n");
   const uint64_t M = 1ull << (log_n - tp.p);
   uint8_t gp[16];
   store_fe(gp, h_pow(h_load(gen), (u128)tp.P));
@@ -196,6 +206,75 @@ mlh_status mlh_sharded_ntt(mlh_ctx* ctx, const mlh_transport* t, const void* dev
   return MLH_OK;
 }
 
+// `count` transforms, pipelined over two streams: stage A (the local NTT of a
+// forward transform, the cross-shard DFT of an inverse one) runs on the
+// context stream, stage B (the all-to-all, then the other local step) on the
+// context's side stream, so the exchange of transform i overlaps stage A of
+// transform i + 1.  Two staging buffers: stage A of i + 2 waits for stage B of
+// i to have sent its buffer.  On return the context stream is ordered after
+// every transform.  With a host-side transport the stages run in turn.
+mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const void* const* dev_in,
+                                 void* const* dev_out, uint32_t count, uint32_t log_n,
+                                 const uint8_t gen[16], int inverse) {
+  if (!ctx || (count && (!dev_in || !dev_out)) || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  MLH_TRY(check_transport(ctx, t));
+  for (uint32_t i = 0; i < count; ++i)
+    if (!dev_in[i] || !dev_out[i]) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  Tp tp(ctx, t);
+  if (tp.P == 1 || t->host_side) {
+    for (uint32_t i = 0; i < count; ++i)
+      MLH_TRY(mlh_sharded_ntt(ctx, t, dev_in[i], dev_out[i], log_n, gen, inverse));
+    return MLH_OK;
+  }
+  if (log_n < 2 * tp.p + 1 || log_n > 40)
+    return fail(ctx, MLH_ERR_INVALID, "sharded NTT needs 2^log_n >= 2 P^2");
+  if (!gen_has_order(h_load(gen), log_n)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != n");
+  if (!count) return MLH_OK;
+  if (!ctx->side) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  const uint64_t M = 1ull << (log_n - tp.p);
+  uint8_t gp[16];
+  store_fe(gp, h_pow(h_load(gen), (u128)tp.P));
+  Bufs b(ctx);
+  fe *z[2], *recv;
+  MLH_TRY(b.get(M * 16, &z[0]));
+  MLH_TRY(b.get(M * 16, &z[1]));
+  MLH_TRY(b.get(M * 16, &recv));
+  hipEvent_t a_done[2], b_done[2];
+  for (int k = 0; k < 2; ++k) {
+    a_done[k] = take_event(ctx);
+    b_done[k] = take_event(ctx);
+  }
+  struct Recycle {  // the events go back to the context's free list
+    mlh_ctx* c;
+    hipEvent_t* e;
+    ~Recycle() {
+      for (int k = 0; k < 4; ++k) c->ev_free.push_back(e[k]);
+    }
+  };
+  hipEvent_t evs[4] = {a_done[0], a_done[1], b_done[0], b_done[1]};
+  Recycle rec{ctx, evs};
+  hipStream_t main = ctx->stream, side = ctx->side;
+  HIP_TRY(ctx, hipEventRecord(b_done[1], main));  // the side stream starts after the caller's work
+  HIP_TRY(ctx, hipStreamWaitEvent(side, b_done[1], 0));
+  for (uint32_t i = 0; i < count; ++i) {
+    const int k = i & 1;
+    if (i >= 2) HIP_TRY(ctx, hipStreamWaitEvent(main, b_done[k], 0));  // z[k] was sent
+    if (!inverse) MLH_TRY(mlh_ntt(ctx, dev_in[i], z[k], log_n - tp.p, gp));
+    else MLH_TRY(mlh_shard_ntt_cross(ctx, dev_in[i], z[k], log_n, tp.p, tp.rank, gen, 1));
+    HIP_TRY(ctx, hipEventRecord(a_done[k], main));
+    HIP_TRY(ctx, hipStreamWaitEvent(side, a_done[k], 0));
+    {
+      StreamSwap sw(ctx, side);
+      MLH_TRY(tp.all_to_all(z[k], recv, M / tp.P * 16));
+      if (!inverse) MLH_TRY(mlh_shard_ntt_cross(ctx, recv, dev_out[i], log_n, tp.p, tp.rank, gen, 0));
+      else MLH_TRY(mlh_intt(ctx, recv, dev_out[i], log_n - tp.p, gp));
+    }
+    HIP_TRY(ctx, hipEventRecord(b_done[k], side));
+  }
+  HIP_TRY(ctx, hipStreamWaitEvent(main, b_done[(count - 1) & 1], 0));
+  return MLH_OK;
+}
+
 mlh_status mlh_sharded_reed_solomon(mlh_ctx* ctx, const mlh_transport* t, const void* dev_coeffs,
                                     uint32_t log_n, const uint8_t gen[16], void* dev_code) {
   if (!ctx || !dev_coeffs || !dev_code || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
@@ -205,6 +284,8 @@ mlh_status mlh_sharded_reed_solomon(mlh_ctx* ctx, const mlh_transport* t, const 
   const uint32_t log_c = log_n + MLH_LOG_BLOWUP;
   if (log_c < 2 * tp.p + 1 || log_c > 40)
     return fail(ctx, MLH_ERR_INVALID, "sharded RS needs 2^(log_n+1) >= 2 P^2");
+  if (!gen_has_order(h_load(gen), log_c))
+    return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != 2n");
   const uint64_t M2 = 1ull << (log_c - tp.p);  // local code length
   uint8_t gp[16];
   store_fe(gp, h_pow(h_load(gen), (u128)tp.P));
@@ -474,6 +555,32 @@ mlh_status mlh_sharded_fri_prove(mlh_ctx* ctx, const mlh_transport* t, const voi
   return MLH_OK;
 }
 
+// commit_rs_code of a block-layout codeword: local leaves and subtrees, one
+// all-gather of the subtree roots, the top levels on every rank.
+mlh_status mlh_sharded_commit_rs_code(mlh_ctx* ctx, const mlh_transport* t, const void* dev_code,
+                                      uint32_t log_code, uint8_t root_out[32]) {
+  if (!ctx || !dev_code || !root_out) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  MLH_TRY(check_transport(ctx, t));
+  Tp tp(ctx, t);
+  if (log_code < 1 || log_code > 40) return fail(ctx, MLH_ERR_INVALID, "log_code out of range");
+  if (tp.P == 1) {
+    const uint64_t bytes = mlh_merkle_layers_bytes(1ull << (log_code - 1));
+    PoolBuf tree(ctx);
+    MLH_TRY(tree.alloc(bytes));
+    return mlh_merkle_commit_pairs(ctx, dev_code, log_code, tree.p, root_out);
+  }
+  if (log_code < 2 * tp.p + 1) return fail(ctx, MLH_ERR_INVALID, "codeword too small for the world");
+  Bufs b(ctx);
+  ShardedFri F(ctx, tp, b);
+  SLayer L;
+  MLH_TRY(F.make_layer(static_cast<const fe*>(dev_code), log_code, true, &L));
+  MLH_TRY(F.commit(L));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 3584, L.root, 32, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(root_out, ctx->pinned + 3584, 32);
+  return MLH_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Sumcheck (sumcheck.rs:77-247) of cyclic-layout tables
 // ---------------------------------------------------------------------------
@@ -559,6 +666,12 @@ mlh_status mlh_sharded_sumcheck_prove(mlh_ctx* ctx, const mlh_transport* t, void
       log_local = tp.p;
       MLH_TRY(mlh_sumcheck_sums_dev(ctx, m, d, log_local, sums));
     }
+  }
+  // the last rounds folded pool copies: hand the fully folded m(r), d(r) back
+  // to entry 0 of the caller's tables (the reference's tables end at length 1)
+  if (m != dev_m) {
+    HIP_TRY(ctx, hipMemcpyAsync(dev_m, m, 16, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(dev_d, d, 16, hipMemcpyDeviceToDevice, ctx->stream));
   }
   std::vector<uint8_t> host(48ull * n);
   HIP_TRY(ctx, hipMemcpyAsync(host.data(), polys, 32ull * n, hipMemcpyDeviceToHost, ctx->stream));

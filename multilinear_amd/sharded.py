@@ -5,13 +5,17 @@ Transports (``mlh_transport``):
   * ``RcclComm`` -- the library's RCCL communicator (device-to-device over
     xGMI); the 128-byte ncclUniqueId travels over the caller's existing
     torch.distributed group.
-  * ``HostTransport`` -- collectives of a ``multilinear_amd.dist.Transport``
-    (torch.distributed, e.g. gloo) run as C callbacks on host copies; used by
-    the multi-process tests that share one GPU.
+  * ``HostTransport`` -- collectives of a ``Transport`` (torch.distributed,
+    e.g. gloo) run as C callbacks on host copies; used by the multi-process
+    tests that share one GPU and by the bench's gloo rehearsal.
 
-Layouts are those of ``multilinear_amd.dist`` (its Python schedule is the
-executable spec the CPU tests check against the oracle): cyclic in for
-NTT / RS / sumcheck, block 2^log_n / P^2 out of NTT / RS and into FRI.
+Layouts: a vector of n = 2^log_n elements over P = 2^p ranks is
+block-cyclic with block S = 2^log_s: local index l of rank r holds global index
+((l >> log_s) << (log_s + p)) | (r << log_s) | (l mod S).  Cyclic (S = 1) in
+for NTT / RS / sumcheck, block 2^log_n / P^2 out of NTT / RS and into FRI.
+The host helpers below shard / reassemble natural-order arrays in them.  The
+same schedules restated in Python (tests/dist_spec.py) are the executable
+spec the CPU gloo tests check against the oracle.
 """
 import ctypes
 
@@ -28,6 +32,99 @@ def _log2(n):
     if n < 1 or n & (n - 1):
         raise ValueError("size must be a power of two")
     return n.bit_length() - 1
+
+
+# ---------------------------------------------------------------------------
+# transport
+# ---------------------------------------------------------------------------
+
+class Transport:
+    """The collectives of the sharded path, on torch.distributed.
+
+    ``host_staged`` copies device tensors through host memory around each
+    collective (gloo with GPU buffers, e.g. several ranks sharing one GPU in
+    the tests); with ``nccl`` (RCCL) tensors go device to device over xGMI."""
+
+    def __init__(self, group=None, host_staged=False):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.host_staged = host_staged
+        if self.world & (self.world - 1) or self.world > 16:
+            raise ValueError("world size must be a power of two <= 16")
+
+    def _stage(self, t):
+        return t.cpu() if self.host_staged else t
+
+    def all_to_all(self, t):
+        """Chunk i of ``t`` (dim 0 split in world equal parts) goes to rank i;
+        chunk i of the result came from rank i."""
+        import torch
+
+        src = self._stage(t)
+        out = torch.empty_like(src)
+        self.dist.all_to_all_single(out, src.contiguous(), group=self.group)
+        return out.to(t.device) if self.host_staged else out
+
+    def all_gather(self, t):
+        """Concatenation over ranks (rank order) along dim 0."""
+        import torch
+
+        src = self._stage(t).contiguous()
+        out = torch.empty((self.world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype,
+                          device=src.device)
+        self.dist.all_gather_into_tensor(out, src, group=self.group)
+        return out.to(t.device) if self.host_staged else out
+
+    def gather_bytes(self, data: bytes):
+        """All-gather equal-length host byte strings -> list per rank."""
+        import torch
+
+        dev = "cpu" if self.host_staged or self.dist.get_backend(self.group) == "gloo" else \
+            "cuda:%d" % torch.cuda.current_device()
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev) if data else \
+            torch.zeros(0, dtype=torch.uint8, device=dev)
+        g = self.all_gather(t).cpu().numpy().tobytes()
+        n = len(data)
+        return [g[i * n:(i + 1) * n] for i in range(self.world)]
+
+
+# ---------------------------------------------------------------------------
+# layouts
+# ---------------------------------------------------------------------------
+
+def block_owner(i, log_s, log_p):
+    """(rank, local index) of global index i in the block-(2^log_s) layout."""
+    r = (i >> log_s) & ((1 << log_p) - 1)
+    l = ((i >> (log_s + log_p)) << log_s) | (i & ((1 << log_s) - 1))
+    return r, l
+
+
+def shard_cyclic(x, world, rank):
+    """Host helper: rank's part of a natural-order array in the cyclic layout."""
+    return np.ascontiguousarray(x[rank::world])
+
+
+def shard_blocks(x, world, rank, log_s):
+    """Host helper: rank's part of a natural-order array in the block layout."""
+    S = 1 << log_s
+    return np.ascontiguousarray(x.reshape(-1, world, S, *x.shape[1:])[:, rank].reshape(
+        -1, *x.shape[1:]))
+
+
+def unshard_blocks(parts, log_s):
+    """Host helper: natural order from all ranks' block-layout parts."""
+    S = 1 << log_s
+    P = len(parts)
+    st = np.stack([p.reshape(-1, S, *p.shape[1:]) for p in parts], axis=1)
+    return st.reshape(-1, *parts[0].shape[1:])
+
+
+def cross_log_s(log_n, log_p):
+    return log_n - 2 * log_p
 
 
 class RcclComm:
@@ -75,7 +172,7 @@ class RcclComm:
 
 
 class HostTransport:
-    """mlh_transport over a multilinear_amd.dist.Transport (torch.distributed):
+    """mlh_transport over a Transport (torch.distributed, host-staged):
     device buffers are copied to the host, exchanged, copied back."""
 
     def __init__(self, tp, device=0):
@@ -138,6 +235,21 @@ def ntt(x_local, log_n, gen, transport, inverse=False, device=0):
     return out
 
 
+def ntt_batch(xs_local, outs_local, log_n, gen, transport, inverse=False, device=0):
+    """mlh_sharded_ntt_batch: len(xs_local) sharded transforms, xs[i] -> outs[i],
+    the exchange of transform i overlapping the local step of i + 1 (enqueued;
+    the context stream is ordered after all of them on return)."""
+    ctx = context(device)
+    n = len(xs_local)
+    if len(outs_local) != n:
+        raise ValueError("one output per input")
+    ins = (ctypes.c_void_p * max(1, n))(*[ptr(x) for x in xs_local])
+    outs = (ctypes.c_void_p * max(1, n))(*[ptr(y) for y in outs_local])
+    check(lib().mlh_sharded_ntt_batch(ctx, _tp(transport), ins, outs, n, log_n, fe_bytes(gen),
+                                      1 if inverse else 0), ctx)
+    return outs_local
+
+
 def reed_solomon(coeffs_local, log_n, gen, transport, device=0):
     """Sharded reed_solomon of 2^log_n coefficients (cyclic) -> block-layout code."""
     ctx = context(device)
@@ -145,6 +257,15 @@ def reed_solomon(coeffs_local, log_n, gen, transport, device=0):
     check(lib().mlh_sharded_reed_solomon(ctx, _tp(transport), ptr(coeffs_local), log_n, fe_bytes(gen),
                                          ptr(out)), ctx)
     return out
+
+
+def commit_rs_code(code_local, log_code, transport, device=0):
+    """commit_rs_code + Merkle::commit of a block-layout codeword -> the root
+    (32 bytes, the same on every rank)."""
+    ctx = context(device)
+    root = (ctypes.c_uint8 * 32)()
+    check(lib().mlh_sharded_commit_rs_code(ctx, _tp(transport), ptr(code_local), log_code, root), ctx)
+    return bytes(root)
 
 
 def fri_prove(code_local, log_code, transcript, transport, gather_log=16, device=0):

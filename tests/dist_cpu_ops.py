@@ -1,14 +1,14 @@
-"""CPU stand-in for multilinear_amd.dist.HipOps (test infrastructure only).
+"""CPU stand-in for tests/dist_spec.HipOps (test infrastructure only).
 
 Lets the gloo world_size>1 CPU tests drive the real sharded orchestration
-(multilinear_amd/dist.py: layouts, all-to-all / all-gather exchanges, subtree
+(tests/dist_spec.py: layouts, all-to-all / all-gather exchanges, subtree
 root combination, query ownership) with every rank-local step computed by the
 oracle: C-oracle NTT / RS / Merkle, and the defining formulas of the
 cross-shard DFT and the index-mapped fold written out in Python ints."""
 import numpy as np
 import torch
 
-from multilinear_amd import dist as D
+from tests import dist_spec as D
 from oracle import coracle as C
 from oracle import field as F
 

@@ -1,4 +1,11 @@
-"""Sharded NTT, Reed-Solomon encoding and FRI prove: one process per GPU.
+"""Executable specification of the multi-GPU schedules (TEST INFRASTRUCTURE).
+
+The product implementation is C++ behind the C ABI (multilinear_amd/csrc/
+sharded.hip: mlh_sharded_*), which a Rust caller binds; this module states the
+same schedules in Python so that the CPU tests (tests/test_dist_cpu.py) can run
+them over gloo with world sizes 2/4/8 and oracle rank-local steps
+(tests/dist_cpu_ops.py), and the GPU tests with the C ABI's rank-local steps.
+Nothing in multilinear_amd/ or bench.py imports it.
 
 The reference (fr34za/multilinear) is single-node CPU code; its prover API is
 ``Polynomial::ntt`` / ``reed_solomon`` (src/ntt/mod.rs:69-108, src/fri/mod.rs:19-28)
@@ -36,8 +43,10 @@ import hashlib
 
 import numpy as np
 
-from . import _lib
-from .device import check, context, fe_bytes, lib, ptr
+from multilinear_amd import _lib
+from multilinear_amd.device import check, context, fe_bytes, lib, ptr
+from multilinear_amd.sharded import (Transport, block_owner, cross_log_s, shard_blocks,  # noqa: F401
+                                     shard_cyclic, unshard_blocks)
 
 M = 340282366920938463463374557953744961537
 LOG_BLOWUP = _lib.LOG_BLOWUP
@@ -48,64 +57,6 @@ def _log2(n):
     if n < 1 or n & (n - 1):
         raise ValueError("size must be a power of two")
     return n.bit_length() - 1
-
-
-# ---------------------------------------------------------------------------
-# transport
-# ---------------------------------------------------------------------------
-
-class Transport:
-    """The collectives of the sharded path, on torch.distributed.
-
-    ``host_staged`` copies device tensors through host memory around each
-    collective (gloo with GPU buffers, e.g. several ranks sharing one GPU in
-    the tests); with ``nccl`` (RCCL) tensors go device to device over xGMI."""
-
-    def __init__(self, group=None, host_staged=False):
-        import torch.distributed as dist
-
-        self.dist = dist
-        self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
-        self.host_staged = host_staged
-        if self.world & (self.world - 1) or self.world > 16:
-            raise ValueError("world size must be a power of two <= 16")
-
-    def _stage(self, t):
-        return t.cpu() if self.host_staged else t
-
-    def all_to_all(self, t):
-        """Chunk i of ``t`` (dim 0 split in world equal parts) goes to rank i;
-        chunk i of the result came from rank i."""
-        import torch
-
-        src = self._stage(t)
-        out = torch.empty_like(src)
-        self.dist.all_to_all_single(out, src.contiguous(), group=self.group)
-        return out.to(t.device) if self.host_staged else out
-
-    def all_gather(self, t):
-        """Concatenation over ranks (rank order) along dim 0."""
-        import torch
-
-        src = self._stage(t).contiguous()
-        out = torch.empty((self.world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype,
-                          device=src.device)
-        self.dist.all_gather_into_tensor(out, src, group=self.group)
-        return out.to(t.device) if self.host_staged else out
-
-    def gather_bytes(self, data: bytes):
-        """All-gather equal-length host byte strings -> list per rank."""
-        import torch
-
-        dev = "cpu" if self.host_staged or self.dist.get_backend(self.group) == "gloo" else \
-            "cuda:%d" % torch.cuda.current_device()
-        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev) if data else \
-            torch.zeros(0, dtype=torch.uint8, device=dev)
-        g = self.all_gather(t).cpu().numpy().tobytes()
-        n = len(data)
-        return [g[i * n:(i + 1) * n] for i in range(self.world)]
 
 
 # ---------------------------------------------------------------------------
@@ -261,7 +212,7 @@ class HipOps:
 
     # -- sumcheck (tables folded in place) --
     def eq_table(self, points):
-        from .polynomials import eq_table
+        from multilinear_amd.polynomials import eq_table
 
         return eq_table(points, self.device)
 
@@ -276,7 +227,7 @@ class HipOps:
         return int.from_bytes(b[:16], "little"), int.from_bytes(b[16:], "little")
 
     def const(self, v):
-        from .device import ints_to_limbs, to_device
+        from multilinear_amd.device import ints_to_limbs, to_device
 
         return to_device(ints_to_limbs([v]), self.device)
 
@@ -320,41 +271,6 @@ class HipOps:
 
 
 # ---------------------------------------------------------------------------
-# layouts
-# ---------------------------------------------------------------------------
-
-def block_owner(i, log_s, log_p):
-    """(rank, local index) of global index i in the block-(2^log_s) layout."""
-    r = (i >> log_s) & ((1 << log_p) - 1)
-    l = ((i >> (log_s + log_p)) << log_s) | (i & ((1 << log_s) - 1))
-    return r, l
-
-
-def shard_cyclic(x, world, rank):
-    """Host helper: rank's part of a natural-order array in the cyclic layout."""
-    return np.ascontiguousarray(x[rank::world])
-
-
-def shard_blocks(x, world, rank, log_s):
-    """Host helper: rank's part of a natural-order array in the block layout."""
-    S = 1 << log_s
-    return np.ascontiguousarray(x.reshape(-1, world, S, *x.shape[1:])[:, rank].reshape(
-        -1, *x.shape[1:]))
-
-
-def unshard_blocks(parts, log_s):
-    """Host helper: natural order from all ranks' block-layout parts."""
-    S = 1 << log_s
-    P = len(parts)
-    st = np.stack([p.reshape(-1, S, *p.shape[1:]) for p in parts], axis=1)
-    return st.reshape(-1, *parts[0].shape[1:])
-
-
-def cross_log_s(log_n, log_p):
-    return log_n - 2 * log_p
-
-
-# ---------------------------------------------------------------------------
 # sharded NTT / RS
 # ---------------------------------------------------------------------------
 
@@ -367,58 +283,6 @@ def ntt(x_local, log_n, gen, tp, ops):
     z = ops.ntt(x_local, pow(gen, P, M))
     recv = tp.all_to_all(z)
     return ops.cross(recv, log_n, _log2(P), tp.rank, gen, False)
-
-
-class NttPipeline:
-    """Sharded forward NTTs of a stream of independent vectors with the
-    all-to-all of vector i overlapping the local transform of vector i+1:
-    local NTTs and the cross-shard kernels run on the current (compute)
-    stream, the exchanges on a second stream, ordered by events.
-
-        pipe = NttPipeline(log_n, gen, tp, ops)
-        for x in xs: pipe.submit(x)        # returns finished outputs, in order
-        outs += pipe.drain()
-    """
-
-    def __init__(self, log_n, gen, tp, ops):
-        import torch
-
-        self.log_n, self.gen, self.tp, self.ops = log_n, gen, tp, ops
-        self.P = tp.world
-        self.comm = torch.cuda.Stream()
-        self.pending = None
-
-    def _finish(self):
-        import torch
-
-        recv, ev = self.pending
-        self.pending = None
-        comp = torch.cuda.current_stream()
-        comp.wait_event(ev)
-        recv.record_stream(comp)
-        return self.ops.cross(recv, self.log_n, _log2(self.P), self.tp.rank, self.gen, False)
-
-    def submit(self, x):
-        import torch
-
-        if self.P == 1:
-            return [self.ops.ntt(x, self.gen)]
-        comp = torch.cuda.current_stream()
-        z = self.ops.ntt(x, pow(self.gen, self.P, M))
-        ready = torch.cuda.Event()
-        ready.record(comp)
-        with torch.cuda.stream(self.comm):
-            self.comm.wait_event(ready)
-            z.record_stream(self.comm)
-            recv = self.tp.all_to_all(z)
-            done = torch.cuda.Event()
-            done.record(self.comm)
-        out = [self._finish()] if self.pending is not None else []
-        self.pending = (recv, done)
-        return out
-
-    def drain(self):
-        return [self._finish()] if self.pending is not None else []
 
 
 def intt(X_local, log_n, gen, tp, ops):
@@ -558,7 +422,7 @@ def fri_prove(code_local, log_code, transcript, tp, ops, gather_log=16):
     replays the absorbs into ``transcript`` and runs the query phase.
     Every rank returns the same proof; it equals the single-GPU proof of the
     natural-order codeword byte for byte."""
-    from .fri import FriProof
+    from multilinear_amd.fri import FriProof
 
     P, rank = tp.world, tp.rank
     log_p = _log2(P)

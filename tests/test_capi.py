@@ -52,6 +52,38 @@ def test_generators_match_oracle():
     assert lib.mlh_pow_2_generator(41, (ctypes.c_uint8 * 16)()) == 1
 
 
+def _gp_call(lib, table):
+    raw = b"".join(int(v).to_bytes(16, "little") for v in table)
+    buf = (ctypes.c_uint8 * max(16, len(raw))).from_buffer_copy(raw.ljust(16, b"\0"))
+    g, lg = (ctypes.c_uint8 * 16)(), ctypes.c_uint32()
+    st = lib.mlh_gen_pows_params(buf, len(table), g, ctypes.byref(lg))
+    return st, int.from_bytes(bytes(g), "little"), lg.value
+
+
+def test_gen_pows_shim_accepts_power_series_rejects_others():
+    """The Rust shim's mapping gen_pows: &[F] -> (gen_pows[1], log2 len) of the
+    _gp entry points (fri/mod.rs:79-114, :261): the reference's own table
+    (pow_2_generator_powers) maps to (g, log2 len); a table that is not that
+    power series -- which the reference would fold with, silently giving a
+    different proof -- is rejected with MLH_ERR_INVALID."""
+    lib = _lib.load()
+    for lg in (1, 2, 5, 10, 13):
+        tab = F.pow_2_generator_powers(lg)
+        assert _gp_call(lib, tab) == (0, tab[1], lg)
+    tab = F.pow_2_generator_powers(10)
+    bad = [list(tab) for _ in range(6)]
+    bad[0][0] = 2                                # gen_pows[0] != 1
+    bad[1][len(tab) - 1] = (tab[-1] + 1) % F.M   # last entry not g^-1
+    bad[2][512] = 1                              # gen_pows[len/2] != -1
+    bad[3][64] = (tab[64] * 3) % F.M             # gen_pows[2^j] != g^(2^j)
+    bad[4] = F.pow_2_generator_powers(11)[:1024]  # g of order 2^11, table of 2^10
+    bad[5][1] = F.M + 1                          # non-canonical g
+    for b in bad:
+        assert _gp_call(lib, b)[0] == 1, b[:3]
+    assert _gp_call(lib, tab[:768])[0] == 1      # not a power of two
+    assert _gp_call(lib, tab[:1])[0] == 1
+
+
 def test_transcript_matches_reference_semantics():
     from multilinear_amd.transcript import Transcript
 

@@ -1,4 +1,4 @@
-"""world_size 2 and 4 gloo tests of the sharded path (multilinear_amd/dist.py)
+"""world_size 2 and 4 gloo tests of the sharded path (tests/dist_spec.py)
 on CPU: the real orchestration (layouts, all-to-all, all-gather, subtree-root
 combination, query ownership) with rank-local steps from the oracle
 (tests/dist_cpu_ops.py).  Outputs must equal the single-process oracle's:
@@ -27,7 +27,7 @@ def _worker(rank, world, port, log_c, gather_log, q):
     os.environ["MASTER_PORT"] = str(port)
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from multilinear_amd import dist as D
+        from tests import dist_spec as D
         from multilinear_amd.transcript import Transcript
         from oracle import coracle as C
         from oracle import field as F
@@ -128,7 +128,7 @@ def _sc_worker(rank, world, port, n, q):
     os.environ["MASTER_PORT"] = str(port)
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from multilinear_amd import dist as D
+        from tests import dist_spec as D
         from multilinear_amd.transcript import Transcript
         from tests.dist_cpu_ops import CpuOps
 
@@ -196,7 +196,7 @@ def _commit_worker(rank, world, port, log_c, q):
     os.environ["MASTER_PORT"] = str(port)
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from multilinear_amd import dist as D
+        from tests import dist_spec as D
         from oracle import coracle as C
         from oracle import field as F
         from tests.dist_cpu_ops import CpuOps

@@ -1,11 +1,12 @@
-"""GPU tests of the sharded path (multilinear_amd/dist.py, libmlhip mlh_shard_*).
+"""GPU tests of the sharded building blocks (libmlhip mlh_shard_*).
 
 * In-process emulation of P ranks on one GPU: every rank-local HIP step runs
   through the C ABI, the all-to-all is done by slicing -- the sharded NTT /
   INTT / RS must equal the single-GPU transform bit for bit.
-* Real multi-process runs (2 and 4 processes sharing the one GPU, gloo with
-  host-staged buffers standing in for RCCL): the sharded FRI proof must equal
-  the single-GPU mlh_fri_prove proof byte for byte and pass the verifier.
+* The nccl (RCCL) backend at world 1 through the spec's Transport.
+The whole C++ schedules (mlh_sharded_*) are tested in test_sharded_capi_gpu.py
+(processes over gloo) and test_sharded_threads_gpu.py (P ranks as threads with
+device-ordered collectives, as RCCL orders them).
 """
 import os
 import socket
@@ -18,10 +19,8 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 from multilinear_amd import device as DV  # noqa: E402
-from multilinear_amd import dist as D  # noqa: E402
+from tests import dist_spec as D  # noqa: E402
 from multilinear_amd import ntt as MN  # noqa: E402
-from multilinear_amd.fri import FriProof  # noqa: E402
-from multilinear_amd.transcript import Transcript  # noqa: E402
 
 M = D.M
 
@@ -103,169 +102,6 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
-
-
-def _worker(rank, world, port, log_c, gather_log, q):
-    import torch.distributed as tdist
-
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    tdist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        torch.cuda.set_device(0)
-        tp, ops = D.Transport(host_staged=True), D.HipOps(0)
-        log_n = log_c - 1
-        coeffs = DV.random_limbs(1 << log_n, seed=11)
-        gen = MN.pow_2_generator(log_c)
-        local = DV.to_device(D.shard_cyclic(coeffs, world, rank))
-        enc = D.reed_solomon(local, log_n, gen, tp, ops)
-        proof = D.fri_prove(enc, log_c, Transcript(), tp, ops, gather_log=gather_log)
-        torch.cuda.synchronize()
-        res = {"commit": bytes(proof._commit), "q": bytes(proof._q), "idx": list(proof._idx),
-               "last": bytes(proof.c.last_elem), "lr": bytes(proof.c.last_random),
-               "ok": proof.verify()}
-        if rank == 0:  # the single-GPU proof of the natural-order codeword
-            from multilinear_amd import fri as MF
-
-            code = MF.reed_solomon(DV.to_device(coeffs), gen)
-            ref = FriProof.prove(code, Transcript())
-            res["ref"] = {"commit": bytes(ref._commit), "q": bytes(ref._q),
-                          "idx": list(ref._idx), "last": bytes(ref.c.last_elem),
-                          "lr": bytes(ref.c.last_random)}
-        q.put((rank, res))
-    except Exception:
-        import traceback
-
-        q.put((rank, {"error": traceback.format_exc()}))
-    finally:
-        tdist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world,log_c,gather_log", [(2, 16, 8), (4, 20, 12), (4, 12, 16)])
-def test_sharded_fri_prove_multiprocess(world, log_c, gather_log):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, log_c, gather_log, q))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    try:
-        res = dict(q.get(timeout=300) for _ in range(world))
-    finally:
-        for p in procs:
-            p.join(timeout=60)
-    for r in range(world):
-        assert "error" not in res[r], res[r].get("error")
-    ref = res[0].pop("ref")
-    for r in range(world):
-        assert res[r]["ok"], "rank %d proof rejected" % r
-        for key in ("commit", "q", "idx", "last", "lr"):
-            assert res[r][key] == ref[key], "rank %d: %s differs from single-GPU proof" % (r, key)
-
-
-def _sc_worker(rank, world, port, n, q):
-    import torch.distributed as tdist
-
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    tdist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        import random
-
-        from multilinear_amd import polynomials as MPL
-        from multilinear_amd import sumcheck as MS
-
-        torch.cuda.set_device(0)
-        tp, ops = D.Transport(host_staged=True), D.HipOps(0)
-        ev = DV.random_limbs(1 << n, seed=21)
-        rr = random.Random(4)
-        pts = [rr.randrange(M) for _ in range(n)]
-        m = DV.to_device(D.shard_cyclic(ev, world, rank))
-        d = D.eq_table(pts, tp, ops)
-        tr = Transcript()
-        polys, rs = D.sumcheck_prove(m, d, n, 777, tr, tp, ops)
-        res = {"polys": polys, "rs": rs, "lr": tr.random()}
-        if rank == 0:
-            x = DV.to_device(ev)
-            tab = MS.SumcheckTables(x.clone(), MPL.eq_table(pts))
-            t2 = Transcript()
-            rp, rr2 = tab.compute_sumcheck_polynomials(777, t2)
-            res["ref"] = {"polys": rp, "rs": rr2, "lr": t2.random()}
-        q.put((rank, res))
-    except Exception:
-        import traceback
-
-        q.put((rank, {"error": traceback.format_exc()}))
-    finally:
-        tdist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world,n", [(2, 18), (4, 20)])
-def test_sharded_sumcheck_multiprocess(world, n):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_sc_worker, args=(r, world, port, n, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    try:
-        res = dict(q.get(timeout=300) for _ in range(world))
-    finally:
-        for p in procs:
-            p.join(timeout=60)
-    for r in range(world):
-        assert "error" not in res[r], res[r].get("error")
-    ref = res[0].pop("ref")
-    for r in range(world):
-        assert [tuple(p) for p in res[r]["polys"]] == [tuple(p) for p in ref["polys"]]
-        assert res[r]["rs"] == ref["rs"] and res[r]["lr"] == ref["lr"]
-
-
-def _pipe_worker(rank, world, port, log_n, q):
-    import torch.distributed as tdist
-
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    tdist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        torch.cuda.set_device(0)
-        tp, ops = D.Transport(host_staged=True), D.HipOps(0)
-        gen = MN.pow_2_generator(log_n)
-        xs = [DV.to_device(D.shard_cyclic(DV.random_limbs(1 << log_n, seed=s), world, rank))
-              for s in range(4)]
-        pipe = D.NttPipeline(log_n, gen, tp, ops)
-        outs = []
-        for x in xs:
-            outs += pipe.submit(x)
-        outs += pipe.drain()
-        ref = [D.ntt(x, log_n, gen, tp, ops) for x in xs]
-        torch.cuda.synchronize()
-        q.put((rank, {"ok": all(torch.equal(a, b) for a, b in zip(outs, ref)) and len(outs) == 4}))
-    except Exception:
-        import traceback
-
-        q.put((rank, {"error": traceback.format_exc()}))
-    finally:
-        tdist.destroy_process_group()
-
-
-def test_ntt_pipeline_matches_sharded_ntt():
-    world, log_n = 2, 16
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, log_n, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    try:
-        res = dict(q.get(timeout=300) for _ in range(world))
-    finally:
-        for p in procs:
-            p.join(timeout=60)
-    for r in range(world):
-        assert "error" not in res[r], res[r].get("error")
-        assert res[r]["ok"]
 
 
 def _rccl_worker(port, q):

@@ -1,12 +1,17 @@
 """The multi-GPU C ABI (csrc/sharded.hip: mlh_sharded_*, mlh_comm_*).
 
 * 2 and 4 real processes sharing the one GPU, exchanges through
-  sharded.HostTransport (torch.distributed gloo as C callbacks): the sharded
-  NTT / INTT / RS outputs reassemble to the single-GPU transforms and to the C
-  oracle's (oracle/c/oracle.c: ntt / reed_solomon), the sharded
-  FRI proof equals the single-GPU mlh_fri_prove proof byte for byte (and
-  verifies), the sharded eq table + sumcheck give the single-GPU round
-  polynomials and challenges.
+  sharded.HostTransport (torch.distributed gloo as C callbacks), every result
+  compared with the ORACLE on the same inputs: the sharded NTT / INTT / RS
+  outputs reassemble to the C oracle's (oracle/c/oracle.c: ntt /
+  reed_solomon); the sharded FRI proof's commitments and last element equal
+  the C oracle's FriProverData::fold (orc_fri_commit_par) and, at codewords
+  the Python oracle proves in seconds, every query path equals
+  oracle/fri.py's FriProof::prove; the sharded eq table + sumcheck give the
+  round polynomials, challenges, final transcript and fully folded m(r), d(r)
+  of the reference round loop run on the C oracle (eq_table_par,
+  partial_sums_par, fold_par).  The single-GPU entry points are compared as
+  well (same bytes).
 * RCCL at world 1: an mlh_comm is created from a unique id and its transport
   callbacks (ncclAllToAll / ncclAllGather) move device buffers.
 The schedules are those of multilinear_amd/dist.py, whose Python version the
@@ -24,7 +29,7 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 from multilinear_amd import device as DV  # noqa: E402
-from multilinear_amd import dist as D  # noqa: E402
+from tests import dist_spec as D  # noqa: E402
 from multilinear_amd import sharded as S  # noqa: E402
 from oracle import coracle as C  # noqa: E402  (checker only)
 
@@ -80,8 +85,11 @@ def _worker(rank, world, port, cfg, q):
         pts = [rr.randrange(D.M) for _ in range(n)]
         d = S.eq_table(pts, ht)
         tr = Transcript()
-        polys, rs = S.sumcheck_prove(DV.to_device(D.shard_cyclic(ev, world, rank)), d, n, 777, tr, ht)
+        m_loc = DV.to_device(D.shard_cyclic(ev, world, rank))
+        polys, rs = S.sumcheck_prove(m_loc, d, n, 777, tr, ht)
         res["sc"] = (polys, rs, tr.random())
+        res["folded"] = (DV.from_device(m_loc[:1]).tobytes(), DV.from_device(d[:1]).tobytes())
+        res["queries"] = [pf.query(q) for q in range(MF.NUM_QUERIES)] if rank == 0 else None
         if rank == 0:  # single-GPU references
             ref = {"ntt": DV.from_device(MN.Polynomial(DV.to_device(x)).ntt(g).evals),
                    "code": DV.from_device(MF.reed_solomon(DV.to_device(coeffs), gc))}
@@ -141,6 +149,68 @@ def test_sharded_capi_multiprocess(world, cfg):
         assert res[r]["proof"][5], "rank %d proof rejected" % r
         assert res[r]["proof"][:5] == ref["proof"], "rank %d: proof differs from single GPU" % r
         assert res[r]["sc"] == ref["sc"], "rank %d: sumcheck differs from single GPU" % r
+    _check_against_oracle(res, world, cfg)
+
+
+def _check_against_oracle(res, world, cfg):
+    """The sharded results against the oracle (not only against single GPU)."""
+    import random
+
+    from oracle import field as F
+    from oracle import fri as OF
+    from oracle import polynomials as OPL
+    from oracle import transcript as OT
+
+    lc, n = cfg["log_code"], cfg["n_sc"]
+    coeffs = DV.random_limbs(1 << (lc - 1), seed=11)
+    code = C.reed_solomon(coeffs, lc - 1, F.pow_2_generator(lc))
+    roots, last, _, rc = C.fri_commit_par(code, lc)
+    assert rc == 0
+    for r in range(world):
+        commit, _, _, last_b, _, _ = res[r]["proof"]
+        assert [commit[32 * i:32 * i + 32] for i in range(len(roots))] == roots, \
+            "rank %d: FRI commitments differ from the C oracle" % r
+        assert int.from_bytes(last_b, "little") == last, "rank %d: last element differs" % r
+    if lc <= 16:  # the Python oracle's whole proof, query paths included
+        ints = [int.from_bytes(code[i].tobytes(), "little") for i in range(1 << lc)]
+        want = OF.FriProof.prove(ints, F.pow_2_generator_powers(lc), OT.Transcript())
+        commit, _, _, last_b, last_r, _ = res[0]["proof"]
+        assert commit == b"".join(want.commitments)
+        assert last_r == want.last_random
+        for q, gq in enumerate(res[0]["queries"]):
+            wq = want.queries[q]
+            assert len(gq) == len(wq)
+            for (gv, gs), (wv, wpath) in zip(gq, wq):
+                assert gv == wv
+                assert gs == [s for s, _ in wpath]
+    # sumcheck: the reference round loop on the C oracle, claim 777
+    ev = DV.random_limbs(1 << n, seed=21)
+    rr = random.Random(4)
+    pts = [rr.randrange(D.M) for _ in range(n)]
+    m = ev.copy()
+    d = C.eq_table_par(pts)
+    tr = OT.Transcript()
+    prev = 777
+    want_polys, want_rs = [], []
+    for k in range(n):
+        lh = n - k
+        s1, s2 = C.partial_sums_par(m, d, lh)
+        pol = OPL.interpolate([(prev - s1) % F.M, s1, s2])
+        for c in pol[1:]:
+            tr.absorb(F.to_bytes(c))
+        rch = tr.next_challenge()
+        prev = OPL.uni_evaluate(pol, rch)
+        want_polys.append(tuple(pol[1:]))
+        want_rs.append(rch)
+        C.fold_par(m, d, lh, rch)
+        m, d = m[: 1 << (lh - 1)], d[: 1 << (lh - 1)]
+    for r in range(world):
+        polys, rs, rnd = res[r]["sc"]
+        assert [tuple(p) for p in polys] == want_polys, "rank %d: round polynomials" % r
+        assert list(rs) == want_rs, "rank %d: challenges" % r
+        assert rnd == tr.random(), "rank %d: final transcript" % r
+        assert res[r]["folded"] == (m[0].tobytes(), d[0].tobytes()), \
+            "rank %d: the folded tables' m(r), d(r)" % r
 
 
 def _rccl_worker(port, q):

@@ -1,0 +1,279 @@
+"""The C++ multi-GPU schedules (csrc/sharded.hip: mlh_sharded_*) at P = 2..16
+ranks in ONE process on the one GPU, with collectives ordered on the device
+the way RCCL orders them -- no host drain (host_side = 0).
+
+Each rank is a thread with its own mlh_ctx and HIP stream.  The transport
+(``ThreadDeviceTransport``) enqueues the exchange on the stream the library
+passes, like ncclAllToAll / ncclAllGather: every rank records an event after
+the producer of its send buffer, each rank's stream waits for all senders'
+events and copies its chunks device to device, records a second event, and
+waits for every rank's second event before anything later on its stream may
+overwrite its send buffer.  The library never synchronises around these calls,
+so this runs the stream ordering of the RCCL path at P > 1 -- including the
+two-stream pipeline of mlh_sharded_ntt_batch -- which a host-side transport
+cannot.  Every result is compared with the oracle (C restatement
+oracle/c/oracle.c, and oracle/fri.py for whole proofs at small sizes).
+"""
+import ctypes
+import random
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from multilinear_amd import _lib  # noqa: E402
+from multilinear_amd import device as DV  # noqa: E402
+from multilinear_amd import sharded as S  # noqa: E402
+from multilinear_amd.fri import FriProof  # noqa: E402
+from multilinear_amd.transcript import Transcript  # noqa: E402
+from oracle import coracle as C  # noqa: E402  (checker only)
+from oracle import field as F  # noqa: E402
+from oracle import fri as OF  # noqa: E402
+from oracle import polynomials as OPL  # noqa: E402
+from oracle import transcript as OT  # noqa: E402
+
+_D2D = 3  # hipMemcpyDeviceToDevice
+
+
+def _hip():
+    h = ctypes.CDLL("libamdhip64.so")
+    h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    h.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+    h.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                 ctypes.c_void_p]
+    h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+    return h
+
+
+class ThreadDeviceTransport:
+    """P in-process ranks; collectives enqueued on the caller's stream."""
+
+    def __init__(self, P):
+        self.P = P
+        self.hip = _hip()
+        self.bar = threading.Barrier(P, timeout=120)
+        self.ready = [self._event() for _ in range(P)]
+        self.done = [self._event() for _ in range(P)]
+        self.send = [None] * P
+        self.error = []
+
+        def a2a(user, send, recv, per, stream):  # (void* arguments arrive as int or None)
+            me = user or 0
+            return self._run(me, send, stream, lambda s, src: self._copy(
+                (recv or 0) + s * per, (src or 0) + me * per, per, stream))
+
+        def ag(user, send, recv, nbytes, stream):
+            return self._run(user or 0, send, stream, lambda s, src: self._copy(
+                (recv or 0) + s * nbytes, src, nbytes, stream))
+
+        self._a2a = _lib.ALL_TO_ALL_FN(a2a)
+        self._ag = _lib.ALL_GATHER_FN(ag)
+        self.transports = [_Tp(_lib.TransportC(P, r, 0, ctypes.c_void_p(r), self._a2a, self._ag))
+                           for r in range(P)]
+
+    def _event(self):
+        e = ctypes.c_void_p()
+        assert self.hip.hipEventCreateWithFlags(ctypes.byref(e), 2) == 0  # hipEventDisableTiming
+        return e
+
+    def _copy(self, dst, src, n, stream):
+        if n:
+            assert self.hip.hipMemcpyAsync(dst, src, n, _D2D, stream) == 0
+
+    def _run(self, rank, send, stream, copy_from):
+        try:
+            self.send[rank] = send
+            assert self.hip.hipEventRecord(self.ready[rank], stream) == 0
+            self.bar.wait()
+            for s in range(self.P):
+                assert self.hip.hipStreamWaitEvent(stream, self.ready[s], 0) == 0
+                copy_from(s, self.send[s])
+            assert self.hip.hipEventRecord(self.done[rank], stream) == 0
+            self.bar.wait()
+            for s in range(self.P):  # senders' buffers stay untouched until all copied
+                assert self.hip.hipStreamWaitEvent(stream, self.done[s], 0) == 0
+            self.bar.wait()
+            return 0
+        except Exception as e:  # pragma: no cover - reported as MLH_ERR_COMM
+            self.error.append(repr(e))
+            self.bar.abort()
+            return 1
+
+
+class _Tp:
+    def __init__(self, c):
+        self.transport = c
+
+
+def _run_ranks(P, body):
+    """body(rank, ctx, stream_ptr, transport) in P threads; returns the results."""
+    tr = ThreadDeviceTransport(P)
+    out, errs = [None] * P, []
+    streams = [torch.cuda.Stream() for _ in range(P)]
+    ctxs = []
+    for r in range(P):
+        h = ctypes.c_void_p()
+        DV.check(DV.lib().mlh_context_create(0, ctypes.c_void_p(streams[r].cuda_stream), ctypes.byref(h)))
+        ctxs.append(h.value)
+
+    def run(r):
+        try:
+            with torch.cuda.stream(streams[r]):
+                out[r] = body(r, ctxs[r], streams[r], tr.transports[r])
+                streams[r].synchronize()
+        except Exception:
+            import traceback
+
+            errs.append(traceback.format_exc())
+            tr.bar.abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    torch.cuda.synchronize()
+    for c in ctxs:
+        DV.lib().mlh_context_destroy(c)
+    assert not tr.error, tr.error
+    assert not errs, errs[0]
+    return out
+
+
+def _tp(t):
+    return ctypes.byref(t.transport)
+
+
+def _gen(log_n):
+    return F.pow_2_generator(log_n)
+
+
+@pytest.mark.parametrize("P,log_n,count", [(2, 14, 3), (4, 16, 4), (8, 18, 3), (16, 12, 2)])
+def test_ntt_batch_pipelined_vs_c_oracle(P, log_n, count):
+    """mlh_sharded_ntt_batch (two streams, device-ordered exchanges): every
+    transform equals the C oracle's NTT; the inverse batch gives the inputs back."""
+    L = DV.lib()
+    xs = [DV.random_limbs(1 << log_n, seed=100 + i) for i in range(count)]
+    g = _gen(log_n)
+
+    def body(r, ctx, st, t):
+        ins = [DV.to_device(S.shard_cyclic(x, P, r)) for x in xs]
+        outs = [DV.empty(ins[0].shape[0]) for _ in range(count)]
+        back = [DV.empty(ins[0].shape[0]) for _ in range(count)]
+        pi = (ctypes.c_void_p * count)(*[i.data_ptr() for i in ins])
+        po = (ctypes.c_void_p * count)(*[o.data_ptr() for o in outs])
+        pb = (ctypes.c_void_p * count)(*[b.data_ptr() for b in back])
+        torch.cuda.current_stream().synchronize()
+        DV.check(L.mlh_sharded_ntt_batch(ctx, _tp(t), pi, po, count, log_n, DV.fe_bytes(g), 0), ctx)
+        DV.check(L.mlh_sharded_ntt_batch(ctx, _tp(t), po, pb, count, log_n, DV.fe_bytes(g), 1), ctx)
+        DV.check(L.mlh_synchronize(ctx), ctx)
+        return ([DV.from_device(o) for o in outs], [DV.from_device(b) for b in back],
+                [DV.from_device(i) for i in ins])
+
+    res = _run_ranks(P, body)
+    log_s = log_n - 2 * (P.bit_length() - 1)
+    for i, x in enumerate(xs):
+        want = C.ntt(x, log_n, g)
+        got = S.unshard_blocks([res[r][0][i] for r in range(P)], log_s)
+        assert np.array_equal(got, want), "transform %d" % i
+        for r in range(P):
+            assert np.array_equal(res[r][1][i], res[r][2][i]), "inverse of transform %d, rank %d" % (i, r)
+
+
+def _sumcheck_oracle(ev, pts, claim):
+    m, d = ev.copy(), C.eq_table_par(pts)
+    n = len(pts)
+    tr = OT.Transcript()
+    prev, polys, rs = claim, [], []
+    for k in range(n):
+        lh = n - k
+        s1, s2 = C.partial_sums_par(m, d, lh)
+        pol = OPL.interpolate([(prev - s1) % F.M, s1, s2])
+        for c in pol[1:]:
+            tr.absorb(F.to_bytes(c))
+        rch = tr.next_challenge()
+        prev = OPL.uni_evaluate(pol, rch)
+        polys.append(tuple(pol[1:]))
+        rs.append(rch)
+        C.fold_par(m, d, lh, rch)
+        m, d = m[: 1 << (lh - 1)], d[: 1 << (lh - 1)]
+    return polys, rs, tr.random(), m[0].tobytes(), d[0].tobytes()
+
+
+@pytest.mark.parametrize("P,log_code,gather_log,n_sc", [(2, 14, 8, 9), (4, 18, 12, 12),
+                                                         (8, 16, 10, 11), (16, 12, 16, 4)])
+def test_fri_and_sumcheck_device_ordered_vs_oracle(P, log_code, gather_log, n_sc):
+    """Sharded RS -> commit root -> FRI prove, and the sharded eq table +
+    sumcheck, through device-ordered collectives, against the oracle: RS code
+    and FRI commitments / last element from the C oracle, whole proof (every
+    query path) from oracle/fri.py at log_code <= 14, sumcheck round
+    polynomials, challenges, transcript and folded m(r), d(r) from the
+    reference round loop on the C oracle."""
+    L = DV.lib()
+    coeffs = DV.random_limbs(1 << (log_code - 1), seed=7)
+    gc = _gen(log_code)
+    ev = DV.random_limbs(1 << n_sc, seed=8)
+    rr = random.Random(9)
+    pts = [rr.randrange(F.M) for _ in range(n_sc)]
+    claim = 1234567
+
+    def body(r, ctx, st, t):
+        c_loc = DV.to_device(S.shard_cyclic(coeffs, P, r))
+        code = DV.empty(2 * c_loc.shape[0])
+        torch.cuda.current_stream().synchronize()
+        DV.check(L.mlh_sharded_reed_solomon(ctx, _tp(t), DV.ptr(c_loc), log_code - 1, DV.fe_bytes(gc),
+                                            DV.ptr(code)), ctx)
+        root = (ctypes.c_uint8 * 32)()
+        DV.check(L.mlh_sharded_commit_rs_code(ctx, _tp(t), DV.ptr(code), log_code, root), ctx)
+        pf = FriProof(log_code)
+        tr = Transcript()
+        DV.check(L.mlh_sharded_fri_prove(ctx, _tp(t), DV.ptr(code), log_code, gather_log, tr.h,
+                                         ctypes.byref(pf.c)), ctx)
+        m = DV.to_device(S.shard_cyclic(ev, P, r))
+        pb = b"".join(int(v).to_bytes(16, "little") for v in pts)
+        d = DV.empty(m.shape[0])
+        DV.check(L.mlh_sharded_eq_table(ctx, _tp(t), (ctypes.c_uint8 * len(pb)).from_buffer_copy(pb),
+                                        n_sc, DV.ptr(d)), ctx)
+        str_ = Transcript()
+        polys = (ctypes.c_uint8 * (32 * n_sc))()
+        rsb = (ctypes.c_uint8 * (16 * n_sc))()
+        DV.check(L.mlh_sharded_sumcheck_prove(ctx, _tp(t), DV.ptr(m), DV.ptr(d), n_sc,
+                                              DV.fe_bytes(claim), str_.h, polys, rsb), ctx)
+        DV.check(L.mlh_synchronize(ctx), ctx)
+        P_, R_ = bytes(polys), bytes(rsb)
+        sc = ([(int.from_bytes(P_[32 * k:32 * k + 16], "little"),
+                int.from_bytes(P_[32 * k + 16:32 * k + 32], "little")) for k in range(n_sc)],
+              [int.from_bytes(R_[16 * k:16 * k + 16], "little") for k in range(n_sc)],
+              str_.random(), DV.from_device(m[:1]).tobytes(), DV.from_device(d[:1]).tobytes())
+        return (DV.from_device(code), bytes(root), bytes(pf._commit), bytes(pf.c.last_elem),
+                bytes(pf.c.last_random), [pf.query(q) for q in range(_lib.NUM_QUERIES)],
+                pf.verify(), sc)
+
+    res = _run_ranks(P, body)
+    code_want = C.reed_solomon(coeffs, log_code - 1, gc)
+    log_s = log_code - 2 * (P.bit_length() - 1)
+    assert np.array_equal(S.unshard_blocks([res[r][0] for r in range(P)], log_s), code_want)
+    roots, last, _, rc = C.fri_commit_par(code_want, log_code)
+    assert rc == 0
+    want_sc = _sumcheck_oracle(ev, pts, claim)
+    for r in range(P):
+        _, root, commit, last_b, _, _, ok, sc = res[r]
+        assert root == roots[0], "rank %d: commit_rs_code root" % r
+        assert [commit[32 * i:32 * i + 32] for i in range(len(roots))] == roots, "rank %d" % r
+        assert int.from_bytes(last_b, "little") == last
+        assert ok, "rank %d: proof rejected by the verifier" % r
+        assert sc[0] == want_sc[0] and sc[1] == want_sc[1], "rank %d: sumcheck rounds" % r
+        assert sc[2:] == want_sc[2:], "rank %d: transcript / folded tables" % r
+        assert res[r][2:6] == res[0][2:6], "rank %d: proof differs from rank 0" % r
+    if log_code <= 14:
+        ints = [int.from_bytes(code_want[i].tobytes(), "little") for i in range(1 << log_code)]
+        want = OF.FriProof.prove(ints, F.pow_2_generator_powers(log_code), OT.Transcript())
+        assert res[0][2] == b"".join(want.commitments)
+        assert res[0][4] == want.last_random
+        for q, gq in enumerate(res[0][5]):
+            for (gv, gs), (wv, wpath) in zip(gq, want.queries[q]):
+                assert gv == wv and gs == [s for s, _ in wpath]
