@@ -167,10 +167,10 @@ def load_valu_profile():
              "ntt_pass_kernel<9, 0, 1, 8>": "config 3 RS LDE pass 0",
              "leaf_pairs_level2_kernel": "config 3 Merkle leaves + 2 levels",
              "fri_fold_leaves_kernel": "FRI fold + next-tree leaves",
-             "group_sums_eq_kernel": "config 4 sumcheck: corner sums of rounds 0-5 (HBM-streaming)",
-             "fold_group_eq_kernel<6, false>": "config 4 sumcheck: 6-level fold + next corner sums (HBM-streaming)",
-             "sumcheck_group_kernel": "config 4 sumcheck: 6 rounds' transcript chain (one lane)",
-             "sumcheck_eq_tail_kernel": "config 4 sumcheck: last 12 rounds (one LDS workgroup)"}
+             "corner_sums_lo_kernel": "config 4 sumcheck: corner sums of rounds 0-11 (HBM-streaming)",
+             "fold_group_eq_kernel<6, false>": "config 4 sumcheck: 6-level fold of the 2^24 table (HBM-streaming)",
+             "sumcheck_eq_tail_kernel": "config 4 sumcheck: 12 serial rounds (transcript wave + helper waves), "
+                                        "twice (head on the corner sums, tail on the folded table)"}
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu.json")), reverse=True)
     if not paths:
         return None

@@ -1506,6 +1506,26 @@ struct EqSumcheck {
   // last pass's fold leaves T_B (2^a entries) in m for the tail.
   mlh_status head_rounds(fe* prev, DevSha* dt, fe* polys, fe* rs) {
     if (!B) return MLH_OK;
+    if (B <= kEqLo && a == kEqLo && B >= 2) {
+      // B <= 12: one pass for the B-variable corner sums Y, all B rounds in one
+      // launch on Y (two corner groups), then the B-variable fold of the table
+      // as two eq-weighted passes (sumcheck.hip "grouped eq-factored rounds")
+      PoolBuf yb(ctx);
+      MLH_TRY(yb.alloc(16 * ((1ull << B) + 128)));
+      fe* Y = yb.as<fe>();
+      fe* wf = Y + (1ull << B);
+      const uint32_t JA = B < 6 ? B : 6, JB = B - JA;
+      HIP_TRY(ctx, launch_corner_sums_lo(src, B, a, lo, Y, ctx->stream));
+      HIP_TRY(ctx, launch_sumcheck_eq_head(Y, B, Hk(JA - 1), pts, c, prev, dt, polys, rs, wf,
+                                           ctx->stream, kw));
+      uint32_t nb = 0;
+      HIP_TRY(ctx, launch_fold_group_eq(src, 1ull << L, JA, 0, rs, wf, m, nullptr, lo, a, ctx->partials,
+                                        ctx->stream, &nb));
+      if (JB)
+        HIP_TRY(ctx, launch_fold_group_eq(m, 1ull << (L - JA), JB, 0, rs + JA, wf + 64, m, nullptr, lo,
+                                          a, ctx->partials, ctx->stream, &nb));
+      return MLH_OK;
+    }
     uint32_t nb = 0, k = 0, JT = B < kMaxGroup ? B : kMaxGroup;
     HIP_TRY(ctx, launch_group_sums_eq(src, 1ull << L, JT, Hk(JT - 1), lo, a, ctx->partials,
                                       ctx->stream, &nb));

@@ -87,6 +87,9 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 #ifndef MLH_LDS_PAD
 #define MLH_LDS_PAD 0  // extra dynamic LDS per pass workgroup (occupancy experiments)
 #endif
+#ifndef MLH_DIAG_TW  // diagnostics only (WRONG results): 1 = no TB, 2 = no TB and no TA loads
+#define MLH_DIAG_TW 0
+#endif
 #ifndef MLH_LDS_TW
 #define MLH_LDS_TW 1  // stage twiddles of the lane-dependent phases read from an LDS copy
 #endif
@@ -300,45 +303,73 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     for (int e = 0; e < EPT; ++e) x[e] = fe_load(&lds[pos[e] * kCols + c]);
     run_phase(S0_, Q_);
   };
+  // Two-table twiddle: TB[k][jh] has one jh for the tile's 8 columns (loga >=
+  // 3), so the 8 lanes of a row read the same entry: one row per thread is
+  // loaded and shared through the idle exchange tile.  TB is stored EXPANDED
+  // (the 4 limb-shifted multiples, as the stage twiddles), so its product is
+  // the 43-VALU expanded one (bfly_pp_v) instead of the 62-VALU full product.
+  // MLH_P0_EARLY_TB: its loads (and the first TA pair's) are issued before the
+  // last register phase, whose butterflies cover their latency; otherwise
+  // just before the epilogue's barriers.
+  constexpr int NTt = kCols * R / EPT;
+  constexpr int kTbPerThread = TW == 0 ? R / NTt : 1;
+  fe tbv[kTbPerThread][4];
+  const uint64_t jl = jrest & ((1ull << g.loga) - 1);
+  fe ta_c0, ta_c1;
+  auto load_tb = [&]() {
+    if constexpr (TW == 0 && MLH_DIAG_TW == 0) {
+      const uint64_t jh = jrest >> g.loga;
+      const uint32_t ltcols = g.lstride - g.loga;
+#pragma unroll
+      for (int e = 0; e < kTbPerThread; ++e) {
+        const fe* q = tb + ((((uint64_t)(e * NTt + tid) << ltcols) + jh) << 2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tbv[e][k] = fe_load(q + k);
+      }
+    }
+  };
+  // the first pair's inter-pass twiddles (the asm products below keep later
+  // loads from being hoisted, so each pair's are issued one pair ahead)
+  auto load_ta0 = [&](const uint32_t (&pf)[EPT]) {
+    if constexpr (!LAST && MLH_DIAG_TW == 2) {
+      ta_c0 = fe{{(uint32_t)jl | 1u, 7u, 9u, 3u}};
+      ta_c1 = fe{{(uint32_t)pf[1] | 1u, 5u, 9u, 3u}};
+    } else if constexpr (!LAST) {
+      ta_c0 = fe_load(ta + ((uint64_t)pf[0] << g.loga) + jl);
+      ta_c1 = fe_load(ta + ((uint64_t)pf[1] << g.loga) + jl);
+    }
+  };
+#ifndef MLH_P0_EARLY_TB
+#define MLH_P0_EARLY_TB 0
+#endif
+
+  constexpr bool kEarly = MLH_P0_EARLY_TB && TW == 0 && LOGR > 2 * LQ;
   if constexpr (LOGR > LQ) {
     constexpr int Q2 = (LOGR - LQ) < LQ ? (LOGR - LQ) : LQ;
     exchange_and_run(std::integral_constant<int, LQ>{}, std::integral_constant<int, Q2>{});
     if constexpr (LOGR > 2 * LQ) {
       constexpr int Q3 = LOGR - 2 * LQ;
       static_assert(Q3 <= LQ, "LOGR <= 3 * LQ");
+      if constexpr (kEarly) {
+        uint32_t pf[EPT];
+        positions(std::integral_constant<int, 2 * LQ>{}, std::integral_constant<int, Q3>{}, pf);
+        load_tb();
+        if (MLH_P0_EARLY_TB == 1) load_ta0(pf);  // 2: TB only
+      }
       exchange_and_run(std::integral_constant<int, 2 * LQ>{}, std::integral_constant<int, Q3>{});
     }
   }
 
   // ---- epilogue: inter-pass twiddle, store --------------------------------
-  // the first pair's inter-pass twiddles, issued before the epilogue's
-  // barriers so that their latency overlaps them (the asm products below keep
-  // later loads from being hoisted, so each pair's are issued one pair ahead)
-  const uint64_t jl = jrest & ((1ull << g.loga) - 1);
-  fe ta_c0, ta_c1;
-  if constexpr (!LAST) {
-    ta_c0 = fe_load(ta + ((uint64_t)pos[0] << g.loga) + jl);
-    ta_c1 = fe_load(ta + ((uint64_t)pos[1] << g.loga) + jl);
+  if constexpr (!kEarly) {
+    load_ta0(pos);
+    load_tb();
+  } else if (MLH_P0_EARLY_TB == 2) {
+    load_ta0(pos);
   }
-  // Two-table twiddle: TB[k][jh] has one jh for the tile's 8 columns (loga >=
-  // 3), so the 8 lanes of a row read the same entry: one row per thread is
-  // loaded (with the first pair's TA, its latency overlapping the barrier) and
-  // shared through the idle exchange tile.  TB is stored EXPANDED (the 4
-  // limb-shifted multiples, as the stage twiddles), so its product is the
-  // 43-VALU expanded one (bfly_pp_v) instead of the 62-VALU full product.
   if constexpr (TW == 0) {
-    constexpr int NT = kCols * R / EPT;
-    constexpr int kTbPerThread = R / NT;
     static_assert(4 * R <= R * kCols, "the expanded TB column fits the exchange tile");
-    const uint64_t jh = jrest >> g.loga;
-    const uint32_t ltcols = g.lstride - g.loga;
-    fe tbv[kTbPerThread][4];
-#pragma unroll
-    for (int e = 0; e < kTbPerThread; ++e) {
-      const fe* q = tb + ((((uint64_t)(e * NT + tid) << ltcols) + jh) << 2);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) tbv[e][k] = fe_load(q + k);
-    }
+    constexpr int NT = NTt;
     __syncthreads();  // every lane's reads of the exchange tile are done
 #pragma unroll
     for (int e = 0; e < kTbPerThread; ++e)
@@ -361,12 +392,12 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     for (int e = 0; e < EPT; e += 2) {
       uint64_t rare;
       const fe a0 = ta_c0, a1 = ta_c1;
-      if (e + 2 < EPT) {  // the next pair's, in flight during this pair's products
+      if (e + 2 < EPT && MLH_DIAG_TW < 2) {  // the next pair's, in flight during this pair's products
         ta_c0 = fe_load(ta + ((uint64_t)pos[e + 2] << g.loga) + jl);
         ta_c1 = fe_load(ta + ((uint64_t)pos[e + 3] << g.loga) + jl);
       }
       bfly_ff_v(x[e], a0, x[e + 1], a1, rare);
-      if constexpr (TW == 0) {
+      if constexpr (TW == 0 && MLH_DIAG_TW == 0) {
         const fe* b0 = lds + 4 * pos[e];
         const fe* b1 = lds + 4 * pos[e + 1];
         bfly_pp_v(x[e], b0[0], b0[1], b0[2], b0[3], x[e + 1], b1[0], b1[1], b1[2], b1[3], rare);

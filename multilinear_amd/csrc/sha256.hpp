@@ -17,12 +17,19 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) {
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 // a ^ b ^ c in one full-rate v_bitop3_b32 (truth table 0x96); hipcc emits two
 // v_xor_b32 for the Sigma/sigma functions otherwise.
+// Operands that are compile-time constants after unrolling (the constant words
+// of a 32-byte message's padded block, the IV in the first rounds) take the
+// plain expression instead, which folds (the bitop3 intrinsic does not), so
+// no instruction is spent on them.
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  if (__builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c)) return a ^ b ^ c;
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 // Maj(a, b, c) in one v_bitop3_b32 (table 0xE8: set where >= 2 inputs are);
 // left to itself hipcc emits xor + and + bitop3 per round.
 __device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+  if (__builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c))
+    return (a & b) | (c & (a | b));
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
 

@@ -272,7 +272,13 @@ fold_kernel(fe* m, fe* __restrict__ d, uint64_t S, fe r, const fe* __restrict__ 
 // 2^J corners x nbc blocks (block = c * nbc + bb, so partials[block] is
 // corner-major); a corner's nbc * 256 threads (a power of two >= 2^a) stride
 // over its Q entries, so a thread's i mod 2^a is fixed and lo is applied once.
-constexpr uint32_t kGroupHLds = 1024;  // group_sums_eq_kernel: H entries staged in LDS (16 KiB)
+constexpr uint32_t kGroupHLds = 1024;
+#ifndef MLH_GS_UNROLL
+#define MLH_GS_UNROLL 8  // group_sums_eq_kernel: table entries in flight per thread
+#endif
+#ifndef MLH_GS_NBC_CAP
+#define MLH_GS_NBC_CAP 16  // cap on group_sums_eq blocks per corner (fewer, longer blocks: measured faster)
+#endif  // group_sums_eq_kernel: H entries staged in LDS (16 KiB)
 __global__ void __launch_bounds__(kRedThreads)
 group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe* H,
                      const fe* __restrict__ lo, uint32_t a, uint32_t nbc,
@@ -295,13 +301,15 @@ group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe*
   const uint64_t stride = (uint64_t)nbc * blockDim.x;
   const uint64_t i0 = (uint64_t)bb * blockDim.x + threadIdx.x;
   uint64_t i = i0;
-  for (; i + stride < Q; i += 2 * stride) {  // two entries in flight per thread
-    const fe h0 = fe_load(H + (i >> a)), h1 = fe_load(H + ((i + stride) >> a));
-    const fe v0 = fe_load(Tc + i), v1 = fe_load(Tc + i + stride);
-    mulacc(s0, v0, h0);
-    mulacc(s1, v1, h1);
+  // MLH_GS_UNROLL entries in flight per thread (loads first, then the products)
+  for (; i + (MLH_GS_UNROLL - 1) * stride < Q; i += MLH_GS_UNROLL * stride) {
+    fe v[MLH_GS_UNROLL];
+#pragma unroll
+    for (int u = 0; u < MLH_GS_UNROLL; ++u) v[u] = fe_load(Tc + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < MLH_GS_UNROLL; ++u) mulacc((u & 1) ? s1 : s0, v[u], fe_load(H + ((i + u * stride) >> a)));
   }
-  if (i < Q) mulacc(s0, fe_load(Tc + i), fe_load(H + (i >> a)));
+  for (; i < Q; i += stride) mulacc(s0, fe_load(Tc + i), fe_load(H + (i >> a)));
   fe acc = fe_add(acc_reduce(s0), acc_reduce(s1));
   if (i0 < Q) acc = fe_mul_s(acc, fe_load(lo + (i0 & ((1ull << a) - 1))));
   fe z = fe_zero();
@@ -665,6 +673,7 @@ hipError_t launch_group_sums_eq(const fe* T, uint64_t S, uint32_t J, const fe* H
                                 uint32_t a, fe* partials, hipStream_t st, uint32_t* nb) {
   if (J < 1 || J > kMaxGroup || a < 8 || (S >> J) < (1ull << a)) return hipErrorInvalidValue;
   uint32_t nbc = group_blocks(S >> J, 1u << J);
+  if (MLH_GS_NBC_CAP && nbc > MLH_GS_NBC_CAP) nbc = MLH_GS_NBC_CAP;
   while ((uint64_t)nbc * kRedThreads < (1ull << a)) nbc *= 2;  // stride >= 2^a
   if ((nbc << J) > 2 * kMaxRedBlocks) return hipErrorInvalidValue;
   *nb = nbc;
@@ -866,24 +875,6 @@ __device__ __forceinline__ fe bcast_fe(const fe& x, int src) {
   for (int i = 0; i < 4; ++i) r.w[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.w[i], src);
   return r;
 }
-// x from the lane at the given DPP pattern (quad_perm / row_half_mirror).
-template <int CTRL>
-__device__ __forceinline__ fe dpp_fe(const fe& x) {
-  fe r;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    r.w[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.w[i], CTRL, 0xF, 0xF, true);
-  return r;
-}
-// Sum over each aligned group of n (2, 4 or 8) lanes, every lane of the group
-// ending with it: DPP butterflies (xor 1, xor 2 quad_perms, then the mirror
-// within 8 lanes, which pairs the two summed quads), no LDS crossbar.
-__device__ __forceinline__ fe group_sum_dpp(fe x, uint32_t n) {
-  if (n > 1) x = fe_add(x, dpp_fe<0xB1>(x));   // quad_perm [1,0,3,2]
-  if (n > 2) x = fe_add(x, dpp_fe<0x4E>(x));   // quad_perm [2,3,0,1]
-  if (n > 4) x = fe_add(x, dpp_fe<0x141>(x));  // row_half_mirror
-  return x;
-}
 __device__ __forceinline__ fe shfl_fe(const fe& x, int src) {
   fe r;
 #pragma unroll
@@ -891,316 +882,600 @@ __device__ __forceinline__ fe shfl_fe(const fe& x, int src) {
   return r;
 }
 
-// Wave 0 (all 64 lanes) runs rounds t0..t1-1 of a group of J eq-factored
-// rounds from its corner sums, lanes split by role: lanes 8..15 hold the
-// corner sums (lane 8 + c: X_c), lane 0 the claim and the round's
-// interpolation / transcript, lane 1 the eq scale c (v: lane 0 the claim,
-// lane 1 c, on entry and on exit).  Per round: step A (pqrst on every lane) =
-// corner weights + the previous round's claim p(r) (lane 0) and scale
-// c <- c (1 - p - r + 2 r p) (lane 1); a 3-level shuffle sum gives E0/E1;
-// step B (pqrst) = s1 = (c p) E1 on lane 0 and s2 = (c (3p - 1)) (2 E1 - E0) on
-// lane 1; lane 0 interpolates, absorbs and draws r.  p / r: the group's
-// points / challenges (r[u] for u < t0 known on entry; the rest filled in);
-// polys: round t0's slot; rs: round 0's r slot (lane 0 stores r_t at rs + t);
-// kw (or nullptr): per round t the padding-block K + W table at kw + 64 t
-// (eq_setup_kernel; used when round t's absorb leaves the buffer empty).
-__device__ __forceinline__ void eq_group_rounds(const fe& X, uint32_t J, uint32_t t0, uint32_t t1,
-                                                const fe (&p)[3], fe (&r)[3], fe& v, DevSha& s,
-                                                uint32_t* stage, fe* polys, fe* rs,
-                                                const uint32_t* kw) {
-  const uint32_t NC = 1u << J;
-  const uint32_t lane = threadIdx.x & 63;
-  const bool is0 = lane == 0, is1 = lane == 1;
-  const bool wl = lane >= 8 && lane < 8 + NC;  // corner-weight lane
-  const uint32_t cl = lane - 8;                // its corner
-  const fe one = fe_one();
-  // A corner lane's weight in round t is X_c times the J - 1 factors
-  // (c_u ? x_u : 1 - x_u), u != t, x_u = r_u (u < t) or p_u (u > t), kept in
-  // increasing u in F0, F1 (one when absent).  Going from round t to t + 1
-  // only slot t changes (p_{t+1}'s factor becomes r_t's), so after each
-  // challenge one factor is replaced instead of all being re-selected.
-  fe F0 = one, F1 = one;
-  {
-    uint32_t k = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < 3; ++u) {
-      if (u >= J || u == t0) continue;
-      const fe x = u < t0 ? r[u] : p[u];
-      const fe f = (cl >> (J - 1 - u)) & 1u ? x : fe_sub(one, x);
-      if (k == 0) F0 = f; else F1 = f;
-      ++k;
+// ---- serial rounds: a transcript wave and helper waves ----------------------
+// A round's Fiat-Shamir step is one lane's SHA-256 work (1.5 compressions per
+// round on average) and cannot be shortened; everything else is taken off
+// that chain.  Round t's polynomial (c1, c2) depends on the previous challenge
+// r_{t-1} only through quadratics: E_b(t) = A_b + r B_b (the only weight
+// factor or fold involving r_{t-1} is linear in it), the eq scale c_t = U + V r
+// and the claim p_{t-1}(r) = e0 + c1 r + c2 r^2, hence with
+//   X(r) = p_t c_t E1 = s1,  Y(r) = c_t ((3 p_t - 1)(2 E1 - E0) - 3 p_t E1) = s2 - 3 s1,
+//   c2 = (Y + claim) / 2,  c1 = 2 X - claim - c2,  e0' = claim - X
+// they are quadratics in r_{t-1} whose coefficients need r_{t-2} but not
+// r_{t-1}.  A helper wave (the "lead") builds round t's coefficients while
+// wave 0 runs the SHA-256 of round t-1; wave 0 only evaluates two quadratics
+// (two dependent products on two lanes), absorbs (c1, c2) and draws r_t.
+// Exchange through LDS: per round parity the four quadratics (c1, c2, e0', c),
+// the published challenges, and sequence counters (release / acquire at
+// workgroup scope).  A wait longer than kSpinLimit sleeps sets `fail` and gives
+// up instead of hanging the device (the outputs are then wrong, which the
+// tests catch).
+//
+// The lead works on corner sums (see "grouped eq-factored rounds"): lane c of
+// its wave is corner c of a group of J <= 6 variables (c_u = bit J-1-u), with
+// L_c = X_c prod_{challenged u} (c_u ? r_u : 1 - r_u) and the suffix products
+// Rs_u = prod_{u<v<J} (c_v ? p_v : 1 - p_v); round u's E_b sums L_c Rs_u over
+// c_u = b, split by c_{u-1} (whose factor is the one linear in r_{u-1}).
+struct CoopSync {
+  fe poly[2][12];    // round parity -> c1 | c2 | e0' | eq scale (k0, k1, k2) in r_{t-1}
+  fe rsh[64];        // r of each round of the launch (relative index)
+  fe red[4][2];      // per-wave partial sums
+  fe pg[16];         // the launch's points, by variable
+  fe xc[64];         // corner sums of the first group
+  fe rsuf[6][64];    // Rs of the first group (per corner lane; runtime-indexed: LDS)
+  fe rsufB[6][64];   // ... of the eq tail's second group
+  fe msplit[8][64];  // eq tail: its table folded over the first 3 variables
+  fe wsplit[8];      // ... with these weights
+  fe ab[2][4];       // round parity -> A0, B0, A1, B1 (corner wave -> coefficient wave)
+  uint32_t coef_seq, r_seq, hbar, mseq, fail, ab_seq;
+  // transcript wave: working state after round 7 of the last half-block
+  // challenge and the transcript length it belongs to (sha256_rounds_from)
+  uint32_t mid[8];
+  uint64_t mid_len;
+};
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+// Per-round timestamps of the cooperative kernels (tools/coop_bench.hip builds
+// this file with -DMLH_COOP_PROF; compiled out otherwise): [0][k] wave 0
+// starts waiting for round k's slot, [1][k] has it, [2][k] has absorbed,
+// [3][k] published r_k, [4][k] the lead published round k's slot, [5..8][k]
+// the lead's phases.
+#ifdef MLH_COOP_PROF
+__device__ uint64_t g_coop_ts[10][64];
+__device__ uint64_t g_coop_edge[4];  // kernel entry / roles start: s_memtime, wall_clock64
+#define MLH_COOP_EDGE(i)                                         \
+  do {                                                           \
+    if (threadIdx.x == 0) {                                      \
+      g_coop_edge[2 * (i)] = __builtin_amdgcn_s_memtime();       \
+      g_coop_edge[2 * (i) + 1] = wall_clock64();                 \
+    }                                                            \
+  } while (0)
+#define MLH_COOP_TS(e, k)                                                                    \
+  do {                                                                                       \
+    if ((threadIdx.x & 63) == 0 && (k) < 64) g_coop_ts[e][k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define MLH_COOP_TS(e, k) \
+  do {                    \
+  } while (0)
+#define MLH_COOP_EDGE(i) \
+  do {                   \
+  } while (0)
+#endif
+
+__device__ __forceinline__ void lds_publish(uint32_t* f, uint32_t v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(uint32_t* f, uint32_t v, uint32_t* fail) {
+  for (uint32_t n = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v;) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++n == kSpinLimit) {
+      *fail = 1;
+      break;
     }
   }
-  // step A operands, v = P + Q (R + S T): round t0 keeps the claim (lane 0)
-  // and the eq scale (lane 1) as given; corner lanes X F0 F1
-  fe P = is0 || is1 ? v : fe_zero(), Q = wl ? X : fe_zero(), R = fe_zero(), S = F0, T = F1;
-  for (uint32_t tt = t0;; ++tt) {
-    const int tb = 3 + 8 * (int)tt;
-    (void)tb;
-    v = pqrst(P, Q, R, S, T);
-    if (tt == t1) break;
-    MLH_TAIL_TS(tb);
-    const fe pv = tt == 0 ? p[0] : (tt == 1 ? p[1] : p[2]);  // wave-uniform
-    const bool bt = (cl >> (J - 1 - tt)) & 1u;
-    fe E0 = wl && !bt ? v : fe_zero(), E1 = wl && bt ? v : fe_zero();
-    E0 = group_sum_dpp(E0, NC);  // corner lanes 8..8+NC: an aligned group
-    E1 = group_sum_dpp(E1, NC);
-    MLH_TAIL_TS(tb + 1);
-    // step B: lane 0 s1 = E1 (c p), the others s2 = (2 E1 - E0)(c (3p - 1))
-    E0 = bcast_fe(E0, 8);
-    E1 = bcast_fe(E1, 8);
-    const fe cs = bcast_fe(v, 1);
-    const fe sB = fe_mul_s(fe_mul_s(cs, is0 ? pv : fe_sub(fe_add(fe_dbl(pv), pv), one)),
-                           is0 ? E1 : fe_sub(fe_dbl(E1), E0));
-    const fe s2 = bcast_fe(sB, 1);
-    MLH_TAIL_TS(tb + 2);
-    fe rr = fe_zero(), e0 = fe_zero(), c1 = fe_zero(), c2 = fe_zero();
-    if (is0) {
-      const fe s1 = sB;
-      e0 = fe_sub(v, s1);
-      c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
-      c1 = fe_sub(fe_sub(s1, e0), c2);
-      fe* po = polys + 2 * (tt - t0);
-      fe_store(po, c1);
-      fe_store(po + 1, c2);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// barrier of nw helper waves only (wave 0 never joins): a monotonic count
+__device__ __forceinline__ void helper_barrier(CoopSync& S, uint32_t nw, uint32_t& target) {
+  target += nw;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_add(&S.hbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  lds_wait_ge(&S.hbar, target, &S.fail);
+}
+
+// Wave 0: rounds 0..R-1 of the launch.  polys: round 0's (c1, c2) slot, rs:
+// round 0's r slot, kw (or nullptr): round 0's padding-block K + W table.
+__device__ void transcript_rounds(CoopSync& S, uint32_t R, DevSha& s, uint32_t* stage, fe* polys,
+                                  fe* rs, const uint32_t* kw) {
+  const uint32_t lane = threadIdx.x & 63;
+  fe r = fe_zero();
+  for (uint32_t k = 0; k < R; ++k) {
+    MLH_COOP_TS(0, k);
+    lds_wait_ge(&S.coef_seq, k + 1, &S.fail);
+    MLH_COOP_TS(1, k);
+    const fe* sl = S.poly[k & 1] + (lane == 1 ? 3 : 0);
+    const fe v = pqrst(sl[0], r, sl[1], sl[2], r);  // lane 0: c1, lane 1: c2
+    const fe c2 = bcast_fe(v, 1);
+    fe rr = fe_zero();
+    if (lane == 0) {
+      const fe c1 = v;
+      fe_store(polys + 2 * k, c1);
+      fe_store(polys + 2 * k + 1, c2);
       const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
-      MLH_TAIL_TS(tb + 3);
-      dsha_absorb<8>(s, w, stage);  // LE16(c1) || LE16(c2)
-      MLH_TAIL_TS(tb + 4);
-      rr = dsha_challenge_kw(s, kw ? kw + 64 * tt : nullptr);
-      MLH_TAIL_TS(tb + 5);
-      fe_store(rs + tt, rr);
+      // absorb LE16(c1) || LE16(c2) (sumcheck.rs:188-199), then r = next_challenge()
+      uint32_t* bw = reinterpret_cast<uint32_t*>(s.buf);
+      const uint32_t pos = (uint32_t)(s.len & 63);
+      if ((s.len & 3) == 0 && pos == 0) {
+        // half block: the challenge compresses the 32 bytes + padding; its
+        // rounds 0..7 are kept for the next absorb's compression
+#pragma unroll
+        for (int i = 0; i < 8; ++i) bw[i] = w[i];
+        s.len += 32;
+        const uint64_t bits = s.len * 8;
+        uint32_t blk[16], v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          blk[i] = bswap32(w[i]);
+          blk[8 + i] = 0;
+          v[i] = s.h[i];
+        }
+        blk[8] = 0x80000000u;
+        blk[14] = (uint32_t)(bits >> 32);
+        blk[15] = (uint32_t)bits;
+        MLH_COOP_TS(2, k);
+        sha256_rounds_from<0>(v, blk, S.mid);
+        S.mid_len = s.len;
+        fe o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o.w[i] = bswap32(s.h[i] + v[i]);
+        rr = canon_with_carry(o, 0u);
+      } else if ((s.len & 3) == 0 && pos == 32 && S.mid_len == s.len) {
+        // the block completes: its first 8 rounds were run by the last challenge
+        uint32_t blk[16], v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          blk[i] = bswap32(bw[i]);
+          blk[8 + i] = bswap32(w[i]);
+          v[i] = S.mid[i];
+        }
+        sha256_rounds_from<8>(v, blk, nullptr);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s.h[i] += v[i];
+        s.len += 32;
+        MLH_COOP_TS(2, k);
+        rr = dsha_challenge_kw(s, kw ? kw + 64 * k : nullptr);
+      } else {
+        dsha_absorb<8>(s, w, stage);
+        MLH_COOP_TS(2, k);
+        rr = dsha_challenge_kw(s, kw ? kw + 64 * k : nullptr);
+      }
+      fe_store(rs + k, rr);
+      S.rsh[k] = rr;
     }
-    rr = bcast_fe(rr, 0);
-    if (tt == 0) r[0] = rr; else if (tt == 1) r[1] = rr; else r[2] = rr;
-    // the next round's factor slot tt: r_t's in place of p_{t+1}'s
-    const fe f = bt ? rr : fe_sub(one, rr);
-    if (tt == 0) F0 = f; else if (tt == 1) F1 = f;
-    // step A of the next round: lane 0 the claim e0 + r (c1 + c2 r), lane 1
-    // the scale c ((1 - p) + r (2p - 1)), corner lanes X F0 F1
-    P = e0;  // zero off lane 0
-    Q = is0 ? rr : (is1 ? v : Q);
-    R = is0 ? c1 : (is1 ? fe_sub(one, pv) : fe_zero());
-    S = is0 ? c2 : (is1 ? rr : F0);
-    T = is0 ? rr : (is1 ? fe_sub(fe_dbl(pv), one) : F1);
-    MLH_TAIL_TS(tb + 7);
+    r = bcast_fe(rr, 0);
+    lds_publish(&S.r_seq, k + 1);
+    MLH_COOP_TS(3, k);
   }
 }
 
-// Rounds t0..t1-1 of a group of J eq-factored head rounds k..k+J-1 from the
+// Values of round t's four quadratics at r (lane j < 4 evaluates quadratic j).
+// (Cross-lane values move by v_readlane: an LDS round trip measured slower.)
+__device__ __forceinline__ void quad_eval(const fe* q, const fe& r, fe& c1, fe& c2, fe& e0, fe& cs) {
+  const uint32_t lane = threadIdx.x & 63;
+  const fe* k = q + 3 * (lane < 4 ? lane : 0);
+  const fe v = pqrst(k[0], r, k[1], k[2], r);
+  c1 = bcast_fe(v, 0);
+  c2 = bcast_fe(v, 1);
+  e0 = bcast_fe(v, 2);
+  cs = bcast_fe(v, 3);
+}
+// Round t's four quadratics in r_{t-1} into q (12 entries) from E_b = A_b +
+// r B_b, the claim quadratic (cl0, cl1, cl2) = (e0', c1, c2) of round t-1 and
+// its eq scale cs; p = p_t, pp = p_{t-1}.  first: round t is the launch's first
+// (cl0, cs constants; cl1 = cl2 = 0, B_b = 0).  Products on lanes, two deep.
+__device__ void quad_next(bool first, const fe& cl0, const fe& cl1, const fe& cl2, const fe& cs,
+                          const fe& A0, const fe& B0, const fe& A1, const fe& B1, const fe& p,
+                          const fe& pp, fe* q) {
+  const uint32_t lane = threadIdx.x & 63;
+  const fe one = fe_one();
+  const fe p3 = fe_add(fe_dbl(p), p), qq = fe_sub(p3, one);
+  const fe D0 = fe_sub(fe_dbl(A1), A0), D1 = fe_sub(fe_dbl(B1), B0);
+  // lanes 0..5: U = c (1 - pp), V = c (2 pp - 1), q D0, p A1, q D1, p B1
+  const fe a1 = lane < 2 ? cs : ((lane & 1) ? p : qq);
+  const fe b1 = lane == 0 ? fe_sub(one, pp)
+                          : (lane == 1 ? fe_sub(fe_dbl(pp), one)
+                                       : (lane == 2 ? D0 : (lane == 3 ? A1 : (lane == 4 ? D1 : B1))));
+  fe y = fe_mul_s(a1, b1);
+  if (first && lane < 2) y = lane == 0 ? cs : fe_zero();
+  const fe U = bcast_fe(y, 0), V = bcast_fe(y, 1), pA1 = bcast_fe(y, 3), pB1 = bcast_fe(y, 5);
+  const fe f0 = fe_sub(bcast_fe(y, 2), fe_add(fe_dbl(pA1), pA1));
+  const fe f1 = fe_sub(bcast_fe(y, 4), fe_add(fe_dbl(pB1), pB1));
+  // lanes 0..7: U f0, V f0, U f1, V f1, U h0, V h0, U h1, V h1 (h = p A1, p B1)
+  const uint32_t j = (lane >> 1) & 3;
+  const fe b2 = j == 0 ? f0 : (j == 1 ? f1 : (j == 2 ? pA1 : pB1));
+  const fe z = fe_mul_s((lane & 1) ? V : U, b2);
+  const fe Uf0 = bcast_fe(z, 0), Vf0 = bcast_fe(z, 1), Uf1 = bcast_fe(z, 2), Vf1 = bcast_fe(z, 3);
+  const fe Uh0 = bcast_fe(z, 4), Vh0 = bcast_fe(z, 5), Uh1 = bcast_fe(z, 6), Vh1 = bcast_fe(z, 7);
+  // lane k < 3: coefficient k of Y = (U+Vr)(f0+f1 r), X = (U+Vr)(h0+h1 r), the claim
+  const fe Yk = lane == 0 ? Uf0 : (lane == 1 ? fe_add(Uf1, Vf0) : Vf1);
+  const fe Xk = lane == 0 ? Uh0 : (lane == 1 ? fe_add(Uh1, Vh0) : Vh1);
+  const fe Ck = lane == 0 ? cl0 : (lane == 1 ? cl1 : cl2);
+  const fe c2 = fe_half(fe_add(Yk, Ck));
+  const fe c1 = fe_sub(fe_sub(fe_dbl(Xk), Ck), c2);
+  const fe e0 = fe_sub(Ck, Xk);
+  if (lane < 3) {
+    q[lane] = c1;
+    q[3 + lane] = c2;
+    q[6 + lane] = e0;
+    q[9 + lane] = lane == 0 ? U : (lane == 1 ? V : fe_zero());
+  }
+}
+
+// E_b split by the corner bit at position mt (and, me != 0, the bit at me):
+// returns the sums over lanes of x with (bit mt, bit me) = (b, e) as
+// S[2 b + e] (me = 0: S[0], S[2] only).
+__device__ __forceinline__ void bucket_sums(fe x, uint32_t mt, uint32_t me, fe (&Sb)[4]) {
+  for (uint32_t m = 1; m < 64; m <<= 1)
+    if (m != mt && m != me) x = fe_add(x, shfl_xor_fe(x, (int)m));
+  Sb[0] = bcast_fe(x, 0);
+  Sb[2] = bcast_fe(x, (int)mt);
+  if (me) {
+    Sb[1] = bcast_fe(x, (int)me);
+    Sb[3] = bcast_fe(x, (int)(mt | me));
+  }
+}
+
+// Suffix products Rs of a group (J variables, points pv) into rs[u][c]
+__device__ __forceinline__ void suffix_products(uint32_t J, const fe* pv, fe (*rs)[64]) {
+  const uint32_t c = threadIdx.x & 63;
+  const fe one = fe_one();
+  fe acc = one;
+  for (int u = (int)J - 1; u >= 0; --u) {
+    rs[u][c] = acc;
+    const fe x = pv[u];
+    acc = fe_mul_s(acc, (c >> (J - 1 - (uint32_t)u)) & 1u ? x : fe_sub(one, x));
+  }
+}
+
+// The helpers of rounds (variables) u0..vend-1 of the launch's corner groups
+// -- group A = variables [0, JA) with corner sums X = S.xc[c] (and Rs in
+// S.rsuf), group B = [JA, JA + JB) (eq tail with JB > 0: its corner sums come
+// from S.msplit folded with r_3, r_4 and split by r_5, Rs in S.rsufB).
+// Variable v is launch round v - u0; r_v for v < u0 are in rs_known.  Two
+// waves per round, in parallel once r_{t-2} is out: the corner wave updates
+// the corner weights and sums E_b = A_b + r B_b (S.ab), the coefficient wave
+// evaluates round t-1's quadratics at r_{t-2} and then builds round t's.
+//
+// Corner wave: writes (wout) group A's fold weights or (m_out) the fully
+// folded table entry sum_c W_c X_c.
+__device__ void corner_rounds(CoopSync& S, uint32_t JA, uint32_t JB, uint32_t u0, uint32_t vend,
+                              const fe* rs_known, fe* wout, fe* m_out, fe* wfold) {
+  const uint32_t c = threadIdx.x & 63;
+  const fe one = fe_one();
+  fe X = S.xc[c];
+  if (c >= (1u << JA)) X = fe_zero();
+  fe L = X, W = one, Xa = fe_zero(), Xb = fe_zero(), Xact = X;
+  auto gsel = [&](uint32_t v, const fe& x) -> fe {  // corner c's factor of variable v
+    const uint32_t J = v < JA ? JA : JB, u = v < JA ? v : v - JA;
+    return (c >> (J - 1 - u)) & 1u ? x : fe_sub(one, x);
+  };
+  for (uint32_t v = 0; v < u0; ++v) {
+    const fe g = gsel(v, fe_load(rs_known + v));
+    L = fe_mul_s(L, g);
+    W = fe_mul_s(W, g);
+  }
+  for (uint32_t v = u0; v < vend; ++v) {
+    const bool inB = v >= JA;
+    const uint32_t J = inB ? JB : JA, u = inB ? v - JA : v, t = v - u0;
+    const bool first = t == 0;
+    fe rv = fe_zero();
+    if (t >= 2) {
+      lds_wait_ge(&S.r_seq, t - 1, &S.fail);
+      rv = S.rsh[t - 2];
+    }
+    if (inB && u == 0) {  // group B's corner sums: fold the split table with r_3, r_4
+      lds_wait_ge(&S.mseq, 1, &S.fail);
+      const fe r3 = S.rsh[3 - u0];
+      fe n[2];
+#pragma unroll
+      for (uint32_t b5 = 0; b5 < 2; ++b5) {
+        const fe* M = &S.msplit[0][c];
+        const fe lo = lerp_s(M[64 * (0 | b5)], M[64 * (4 | b5)], r3);  // (b4 = 0; b3 = 0, 1)
+        const fe hi = lerp_s(M[64 * (2 | b5)], M[64 * (6 | b5)], r3);  // (b4 = 1)
+        n[b5] = lerp_s(lo, hi, rv);                                     // r_4
+      }
+      const bool live = c < (1u << JB);
+      Xa = live ? n[0] : fe_zero();
+      Xb = live ? fe_sub(n[1], n[0]) : fe_zero();
+      W = one;
+    } else if (inB && u == 1) {
+      L = fe_add(Xa, fe_mul_s(rv, Xb));  // the corner sums at r_5
+      Xact = L;
+    } else if (u >= 2 && v - 2 >= u0) {
+      const fe g = gsel(v - 2, rv);
+      L = fe_mul_s(L, g);
+      W = fe_mul_s(W, g);
+    }
+    MLH_COOP_TS(6, t);
+    const uint32_t mt = 1u << (J - 1 - u);
+    fe Sb[4];
+    fe A0, B0 = fe_zero(), A1, B1 = fe_zero();
+    if (inB && u == 0) {
+      const fe R0 = S.rsufB[0][c];
+      bucket_sums(fe_mul_s(Xa, R0), mt, 0, Sb);
+      A0 = Sb[0];
+      A1 = Sb[2];
+      bucket_sums(fe_mul_s(Xb, R0), mt, 0, Sb);
+      B0 = Sb[0];
+      B1 = Sb[2];
+    } else {
+      const fe x = fe_mul_s(L, inB ? S.rsufB[u][c] : S.rsuf[u][c]);
+      const uint32_t me = (first || u == 0) ? 0u : 1u << (J - u);
+      bucket_sums(x, mt, me, Sb);
+      A0 = Sb[0];
+      A1 = Sb[2];
+      if (me) {
+        B0 = fe_sub(Sb[1], Sb[0]);
+        B1 = fe_sub(Sb[3], Sb[2]);
+      }
+    }
+    if (c == 0) {
+      fe* ab = S.ab[t & 1];
+      ab[0] = A0;
+      ab[1] = B0;
+      ab[2] = A1;
+      ab[3] = B1;
+    }
+    lds_publish(&S.ab_seq, t + 1);
+    MLH_COOP_TS(7, t);
+  }
+  if (!wout && !m_out && !wfold) return;
+  // the last round's variables: r of the one before it, then its own
+  const uint32_t vl = vend - 1, tl = vl - u0, ul = vl >= JA ? vl - JA : vl;
+  fe rv = fe_zero();
+  if (tl >= 1) {
+    lds_wait_ge(&S.r_seq, tl, &S.fail);
+    rv = S.rsh[tl - 1];
+  }
+  if (vl >= JA && ul == 0)
+    Xact = fe_add(Xa, fe_mul_s(rv, Xb));  // a one-variable group B: m_6 at r_5
+  else if (ul >= 1 && vl - 1 >= u0)
+    W = fe_mul_s(W, gsel(vl - 1, rv));    // (the loop took the variables before)
+  lds_wait_ge(&S.r_seq, tl + 1, &S.fail);
+  W = fe_mul_s(W, gsel(vl, S.rsh[tl]));
+  if (wout && c < (1u << JA)) fe_store(wout + c, W);
+  if (wfold) {  // the fold weights of both groups: W_A at wfold[0..64), W_B at wfold[64..)
+    fe WA = W;
+    if (JB) {
+      WA = one;
+      for (uint32_t v = 0; v < JA; ++v) WA = fe_mul_s(WA, gsel(v, S.rsh[v - u0]));
+      if (c < (1u << JB)) fe_store(wfold + 64 + c, W);
+    }
+    if (c < (1u << JA)) fe_store(wfold + c, WA);
+  }
+  if (m_out) {  // sum over the last group's corners of W_c X_c
+    const uint32_t Jl = vl >= JA ? JB : JA;
+    fe x = c < (1u << Jl) ? fe_mul_s(W, Xact) : fe_zero();
+    for (int m = 32; m >= 1; m >>= 1) x = fe_add(x, shfl_xor_fe(x, m));
+    if (c == 0) fe_store(m_out, x);
+  }
+}
+
+// Coefficient wave: publishes round t's quadratics (S.poly, coef_seq); writes
+// the claim and eq scale after the last round (prev, cdev; d_out too).
+__device__ void coef_rounds(CoopSync& S, uint32_t u0, uint32_t vend, fe* prev, fe* cdev, fe* d_out) {
+  const uint32_t c = threadIdx.x & 63;
+  const fe one = fe_one();
+  const fe claim0 = fe_load(prev), cs0 = fe_load(cdev);
+  fe c1v = fe_zero(), c2v = fe_zero(), e0v = fe_zero(), csv = fe_zero();
+  for (uint32_t v = u0; v < vend; ++v) {
+    const uint32_t t = v - u0;
+    const bool first = t == 0;
+    fe rv = fe_zero();
+    if (t >= 2) {
+      lds_wait_ge(&S.r_seq, t - 1, &S.fail);
+      rv = S.rsh[t - 2];
+    }
+    MLH_COOP_TS(5, t);
+    if (!first) quad_eval(S.poly[(t - 1) & 1], rv, c1v, c2v, e0v, csv);  // round t-1's values
+    lds_wait_ge(&S.ab_seq, t + 1, &S.fail);
+    const fe* ab = S.ab[t & 1];
+    MLH_COOP_TS(8, t);
+    quad_next(first, first ? claim0 : e0v, c1v, c2v, first ? cs0 : csv, ab[0], ab[1], ab[2], ab[3],
+              S.pg[v], v ? S.pg[v - 1] : fe_zero(), S.poly[t & 1]);
+    lds_publish(&S.coef_seq, t + 1);
+    MLH_COOP_TS(4, t);
+  }
+  // the last round's values (at r of the variable before it), its challenge
+  const uint32_t vl = vend - 1, tl = vl - u0;
+  fe rv = fe_zero();
+  if (tl >= 1) {
+    lds_wait_ge(&S.r_seq, tl, &S.fail);
+    rv = S.rsh[tl - 1];
+  }
+  quad_eval(S.poly[tl & 1], rv, c1v, c2v, e0v, csv);
+  lds_wait_ge(&S.r_seq, tl + 1, &S.fail);
+  const fe r = S.rsh[tl];
+  const fe p = S.pg[vl];
+  const fe claim = pqrst(e0v, r, c1v, c2v, r);
+  const fe scale = fe_mul_s(csv, pqrst(fe_sub(one, p), r, fe_sub(fe_dbl(p), one), fe_zero(), fe_zero()));
+  if (c == 0) {
+    fe_store(prev, claim);
+    fe_store(cdev, scale);
+    if (d_out) fe_store(d_out, scale);
+  }
+}
+
+// Rounds t0..t1-1 of a group of J (+ J2) eq-factored head rounds k.. from the
 // corner sums (see "grouped eq-factored rounds"): the NC x nb partials are
-// summed 32 lanes per corner, then wave 0 runs eq_group_rounds.  pts, rs:
+// summed into the NC = 2^(J+J2) corner sums, then wave 0 runs the transcript
+// and wave 1 the coefficients (J2 > 0: all J + J2 rounds, t0 = 0).  pts, rs:
 // p_k.., r_k.. (rs[u] for u < t0 were written by earlier launches of this
-// group).
+// group); polys: round t0's slot; kw: round 0's padding table (or nullptr);
+// wout (when the launch ends the group): the fold weights of its challenges.
 __global__ void __launch_bounds__(kRedThreads)
 sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, uint32_t J2,
                       uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
                       const fe* __restrict__ pts, fe* cdev, const uint32_t* __restrict__ kw,
                       fe* wout) {
+  MLH_COOP_EDGE(0);
   __shared__ DevSha s;
   __shared__ uint32_t stage[8];
-  __shared__ fe slot[64];
-  MLH_TAIL_TS(0);
+  __shared__ fe slotY[64];
+  __shared__ CoopSync S;
   if (threadIdx.x < sizeof(DevSha) / 4)
     reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
+  if (threadIdx.x == 0) {
+    S.coef_seq = S.r_seq = S.hbar = S.mseq = S.fail = S.ab_seq = 0;
+    S.mid_len = ~0ull;
+  }
   const uint32_t JT = J + J2, NC = 1u << JT, G = kRedThreads >> JT;  // threads per corner
   const uint32_t GW = G < 64 ? G : 64;                                // ... within one wave
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave == 1 && lane < JT) S.pg[lane] = fe_load(pts + lane);
+  if (wave == 2) suffix_products(JT, pts, S.rsuf);  // the corner wave's, independent of the partials
   {
     const uint32_t c = threadIdx.x / G, j = threadIdx.x % G;
     fe acc = fe_zero();
 #pragma unroll 4
     for (uint32_t b = j; b < nb; b += G) acc = fe_add(acc, fe_load(partials + (uint64_t)c * nb + b));
-    MLH_TAIL_TS(1);
-    for (uint32_t m = GW / 2; m >= 1; m >>= 1) acc = fe_add(acc, shfl_xor_fe(acc, m));
-    if (threadIdx.x % GW == 0) slot[threadIdx.x / GW] = acc;
+    for (uint32_t m = GW / 2; m >= 1; m >>= 1) acc = fe_add(acc, shfl_xor_fe(acc, (int)m));
+    if (threadIdx.x % GW == 0) slotY[threadIdx.x / GW] = acc;
   }
   __syncthreads();
-  MLH_TAIL_TS(2);
-  if (threadIdx.x >= 64) return;
-  const uint32_t lane = threadIdx.x, per = G / GW;  // slots per corner
-  // lane c < NC: the corner sum Y_c
-  fe Y = fe_zero();
-  if (lane < NC)
-    for (uint32_t q = 0; q < per; ++q) Y = fe_add(Y, slot[lane * per + q]);
-  fe p[3], r[3];
-#pragma unroll
-  for (uint32_t u = 0; u < 3; ++u) {
-    p[u] = u < J ? fe_load(pts + u) : fe_zero();
-    r[u] = u < t0 ? fe_load(rs + u) : fe_zero();
+  MLH_COOP_EDGE(1);
+  const uint32_t tend = J2 ? JT : t1;
+  if (wave == 0) {
+    transcript_rounds(S, tend - t0, s, stage, polys, rs + t0, kw ? kw + 64 * t0 : nullptr);
+    if (lane == 0) *t = s;
+  } else if (wave == 1) {
+    coef_rounds(S, t0, tend, prev, cdev, nullptr);
+  } else if (wave == 2) {
+    fe X = fe_zero();
+    const uint32_t per = G / GW;  // slots per corner
+    if (lane < NC)
+      for (uint32_t q = 0; q < per; ++q) X = fe_add(X, slotY[lane * per + q]);
+    S.xc[lane] = X;
+    corner_rounds(S, JT, 0, t0, tend, rs, (wout && (J2 || t1 == J)) ? wout : nullptr, nullptr,
+                  nullptr);
   }
-  // lane 0: the claim; lane 1: the eq scale
-  fe v = lane == 0 ? fe_load(prev) : (lane == 1 ? fe_load(cdev) : fe_zero());
-  const fe one = fe_one();
-  // one group (J2 == 0): its corner sums; two chained groups over the corners
-  // c = (c_hi: J bits, c_lo: J2 bits): group 1's corner sums sum out c_lo with
-  // its eq weights, group 2's fold c_hi with group 1's challenges (see
-  // "grouped eq-factored rounds").  One loop body for both (code size: the
-  // one-lane transcript is instruction-fetch bound).
-  const uint32_t chi = lane >> J2, clo = lane & ((1u << J2) - 1);
-  fe w1 = fe_one();  // two groups: group 1's factor of the fold weight (lane = corner)
-  for (uint32_t g = 0; g < (J2 ? 2u : 1u); ++g) {
-    const uint32_t Jg = g ? J2 : J;
-    fe x = Y;
-    if (J2) {
-      fe pr[3];  // the summed-out variables' factors: group 2's points / group 1's challenges
-      if (g == 0) {
-#pragma unroll
-        for (uint32_t u = 0; u < 3; ++u) pr[u] = u < J2 ? fe_load(pts + J + u) : fe_zero();
-      } else {
-#pragma unroll
-        for (uint32_t u = 0; u < 3; ++u) pr[u] = r[u];
-      }
-      const uint32_t nb_ = g ? J : J2, bits = g ? chi : clo;
-#pragma unroll
-      for (uint32_t u = 0; u < 3; ++u)
-        if (u < nb_) x = fe_mul_s(x, (bits >> (nb_ - 1 - u)) & 1u ? pr[u] : fe_sub(one, pr[u]));
-      const uint32_t m0 = g ? 1u << J2 : 1u, m1 = g ? NC : 1u << J2;
-      for (uint32_t m = m0; m < m1; m <<= 1) x = fe_add(x, shfl_xor_fe(x, m));
-      if (g == 1) {
-        // group 1's factor of this lane's fold weight, while its r's are at hand
-#pragma unroll
-        for (uint32_t u = 0; u < 3; ++u)
-          if (u < J) w1 = fe_mul_s(w1, (chi >> (J - 1 - u)) & 1u ? r[u] : fe_sub(one, r[u]));
-#pragma unroll
-        for (uint32_t u = 0; u < 3; ++u) {
-          p[u] = u < J2 ? fe_load(pts + J + u) : fe_zero();
-          r[u] = fe_zero();
-        }
-      }
-    }
-    // group g's corner sum X_c to lane 8 + c (group 1 of two: from lane c << J2)
-    const uint32_t src = (g == 0 && J2) ? ((lane - 8) << J2) : (lane - 8);
-    const fe X = shfl_fe(x, src & 63);
-    eq_group_rounds(lane >= 8 && lane < 8 + (1u << Jg) ? X : fe_zero(), Jg, g ? 0 : t0,
-                    g ? Jg : t1, p, r, v, s, stage, g ? polys + 2 * J : polys, g ? rs + J : rs,
-                    kw ? (g ? kw + 64 * J : kw) : nullptr);
-  }
-  if (lane == 0) {
-    *t = s;
-    fe_store(prev, v);
-  }
-  if (lane == 1) fe_store(cdev, v);
-  // the eq weights of the finished group's challenges for the fold pass:
-  // w_c = prod_u (c_u ? r_u : 1 - r_u) over the J (+ J2) variables, lane c
-  if (wout && t1 == J && lane < NC) {
-    fe wc = w1;  // J2 == 0: r holds the group's challenges; else group 2's
-    const uint32_t nbits = J2 ? J2 : J, bits = J2 ? clo : chi;
-#pragma unroll
-    for (uint32_t u = 0; u < 3; ++u)
-      if (u < nbits) wc = fe_mul_s(wc, (bits >> (nbits - 1 - u)) & 1u ? r[u] : fe_sub(one, r[u]));
-    fe_store(wout + lane, wc);
-  }
-  MLH_TAIL_TS(63);
 }
 
 // The last a rounds of an eq-factored sumcheck (mlh_sumcheck_prove_eq) in ONE
 // workgroup: the 2^a-entry matrix table m and the suffix tables e_j =
 // eq(p_{B+j+1}..p_{L-1}) (2^(a-1-j) entries at offset 2^a - 2^(a-j), as H_k)
 // staged in LDS, delta = c eq(p_B..) never materialised.  The rounds go in
-// groups of up to 3 exactly as the HBM head groups: corner sums of the group
-// over m (all waves), the group's rounds on wave 0 (eq_group_rounds), a
-// J-level fold of m in LDS.  On load, m is Tin folded over Jin <= 3 pending
-// variables with rs_in (the last head group's fold, fused here).  Writes the
-// folded matrix m_out[0], the final delta c_L (eq of no points = 1) to
-// d_out[0], the claim and the transcript.
+// corner groups as the head's: group A = the first JA = min(a, 6) variables,
+// corner sums X_c = sum_{i<Q} m[c Q + i] e_{JA-1}[i] (Q = 2^(a-JA)); group B
+// = the rest (a > 6), whose table m_6 (Q entries, its own corner sums) is m
+// folded over group A.  Wave 0 runs the transcript, wave 1 the coefficients,
+// waves 2-3 fold m over group A's first 3 variables once r_0..r_2 are out,
+// keeping the next 3 split (S.msplit); the lead folds those with r_3, r_4 and
+// takes m_6 = N_0 + r_5 (N_1 - N_0) as linear in r_5.  On load, m is Tin
+// folded over Jin <= 3 pending variables with rs_in.  Writes the folded
+// matrix m_out[0], the final delta c_L (eq of no points = 1) to d_out[0], the
+// claim and the transcript.
 __global__ void __launch_bounds__(kRedThreads)
 sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_in, uint32_t a,
-                        const fe* __restrict__ ets, const fe* __restrict__ pts, fe* cdev, fe* prev,
+                        const fe* __restrict__ e_grp, const fe* __restrict__ pts, fe* cdev, fe* prev,
                         DevSha* t, fe* polys, fe* rs, fe* m_out, fe* d_out,
-                        const uint32_t* __restrict__ kw) {
+                        const uint32_t* __restrict__ kw, fe* wfold) {
+  MLH_COOP_EDGE(0);
   extern __shared__ fe eq_tail_lds[];
-  fe* lm = eq_tail_lds;                 // 2^a
-  fe* le = eq_tail_lds + (1u << a);     // 2^a - 1
+  const uint32_t JA = a < 6 ? a : 6, JB = a - JA, QA = 1u << (a - JA);
+  fe* lm = eq_tail_lds;                    // 2^a
+  fe* le = eq_tail_lds + (1u << a);        // e_{JA-1}: QA entries
   __shared__ DevSha s;
   __shared__ uint32_t stage[8];
-  __shared__ fe slot[kRedThreads / 32];
-  __shared__ fe r_sh[3];
+  __shared__ CoopSync S;
   if (threadIdx.x < sizeof(DevSha) / 4)
     reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
+  if (threadIdx.x == 0) {
+    S.coef_seq = S.r_seq = S.hbar = S.mseq = S.fail = S.ab_seq = 0;
+    S.mid_len = ~0ull;
+  }
+  if (threadIdx.x < a) S.pg[threadIdx.x] = fe_load(pts + threadIdx.x);
   const uint32_t S0 = 1u << a;
-  MLH_TAIL_TS(38);
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // the groups' suffix products (from the points in HBM) while the tables load
+  if (wave == 2) suffix_products(JA, pts, S.rsuf);
+  if (wave == 3 && JB) suffix_products(JB, pts + JA, S.rsufB);
   {
+    for (uint32_t x = threadIdx.x; x < QA; x += blockDim.x) le[x] = fe_load(e_grp + x);
     fe rin[3];
 #pragma unroll
     for (uint32_t u = 0; u < 3; ++u) rin[u] = u < Jin ? fe_load(rs_in + u) : fe_zero();
     if (Jin == 0) {  // plain copies, 8 per thread in flight at a time
       for (uint32_t x0 = 0; x0 < S0; x0 += 8 * kRedThreads) {
-        fe v[8], w[8];
+        fe v[8];
 #pragma unroll
         for (uint32_t u = 0; u < 8; ++u) {
           const uint32_t x = x0 + u * kRedThreads + threadIdx.x;
           v[u] = x < S0 ? fe_load(Tin + x) : fe_zero();
-          w[u] = x + 1 < S0 ? fe_load(ets + x) : fe_zero();
         }
 #pragma unroll
         for (uint32_t u = 0; u < 8; ++u) {
           const uint32_t x = x0 + u * kRedThreads + threadIdx.x;
           if (x < S0) lm[x] = v[u];
-          if (x + 1 < S0) le[x] = w[u];
         }
       }
     } else {
-      for (uint32_t x = threadIdx.x; x < S0; x += blockDim.x) {
-        lm[x] = fold_corners_n(Jin, Tin + x, S0, rin);
-        if (x + 1 < S0) le[x] = fe_load(ets + x);
-      }
+      for (uint32_t x = threadIdx.x; x < S0; x += blockDim.x) lm[x] = fold_corners_n(Jin, Tin + x, S0, rin);
     }
   }
-  MLH_TAIL_TS(39);
-  const uint32_t lane = threadIdx.x & 63;
-  fe v = fe_zero();  // wave 0: lane 0 the claim, lane 1 the eq scale
-  if (threadIdx.x == 0) v = fe_load(prev);
-  if (threadIdx.x == 1) v = fe_load(cdev);
   __syncthreads();
-  for (uint32_t j = 0; j < a;) {
-    const uint32_t J = a - j < 3 ? a - j : 3, NC = 1u << J, G = kRedThreads >> J;
-    const uint32_t S = S0 >> j, Q = S >> J;
-    const fe* e = le + (S0 - (S0 >> (j + J - 1)));  // e_{j+J-1}: Q entries
-    {  // corner sums of the group: 2^J corners x G threads
-      const uint32_t c = threadIdx.x / G, jj = threadIdx.x % G;
-      fe acc = fe_zero();
-      for (uint32_t i = jj; i < Q; i += G) acc = fe_add(acc, fe_mul_s(lm[c * Q + i], e[i]));
-#pragma unroll
-      for (int m = 16; m >= 1; m >>= 1) acc = fe_add(acc, shfl_xor_fe(acc, m));
-      if ((threadIdx.x & 31) == 0) slot[threadIdx.x >> 5] = acc;
+  // group A's corner sums: 2^JA corners x QA entries, G = 256 / 2^JA threads per corner
+  {
+    const uint32_t G = kRedThreads >> JA, c = threadIdx.x / G, j = threadIdx.x % G;
+    const fe* e = le;  // e_{JA-1}: QA entries
+    acc9 q;
+    acc_zero(q);
+    for (uint32_t i = j; i < QA; i += G) mulacc(q, lm[c * QA + i], e[i]);
+    fe x = acc_reduce(q);
+    for (uint32_t m = (G < 64 ? G : 64) / 2; m >= 1; m >>= 1) x = fe_add(x, shfl_xor_fe(x, (int)m));
+    if (G <= 64) {
+      if (j == 0) S.xc[c] = x;
+    } else {  // G = 128 or 256 (JA <= 1): 2 or 4 waves per corner
+      if (lane == 0) S.red[wave][0] = x;
     }
-    __syncthreads();
-    MLH_TAIL_TS(40 + 4 * (j / 3));
-    if (threadIdx.x < 64) {
-      fe X = fe_zero();
-      if (lane >= 8 && lane < 8 + NC)
-        for (uint32_t q = 0; q < G / 32; ++q) X = fe_add(X, slot[(lane - 8) * (G / 32) + q]);
-      fe p[3], r[3];
+  }
+  __syncthreads();
+  if ((kRedThreads >> JA) > 64 && threadIdx.x < (1u << JA)) {
+    const uint32_t per = (kRedThreads >> JA) / 64;
+    fe x = fe_zero();
+    for (uint32_t w = 0; w < per; ++w) x = fe_add(x, S.red[threadIdx.x * per + w][0]);
+    S.xc[threadIdx.x] = x;
+  }
+  __syncthreads();
+  MLH_COOP_EDGE(1);
+  if (wave == 0) {
+    transcript_rounds(S, a, s, stage, polys, rs, kw);
+    if (lane == 0) *t = s;
+  } else if (wave == 1) {
+    coef_rounds(S, 0, a, prev, cdev, d_out);
+  } else if (wave == 2) {
+    corner_rounds(S, JA, JB, 0, a, nullptr, nullptr, m_out, wfold);
+  } else if (JB) {
+    // wave 3: after r_0..r_2, M_d[x] = sum_{h<8} w_h m[(8 h + d) QA + x] (d: the bits of
+    // variables 3, 4, 5), w_h = prod_{u<3} (h_u ? r_u : 1 - r_u)
+    constexpr uint32_t NW = 1;
+    uint32_t bar = 0;
+    const uint32_t wid = threadIdx.x - 192;
+    lds_wait_ge(&S.r_seq, 3, &S.fail);
+    if (wid < 8) {
+      const fe one = fe_one();
+      fe w = one;
 #pragma unroll
       for (uint32_t u = 0; u < 3; ++u) {
-        p[u] = u < J ? fe_load(pts + j + u) : fe_zero();
-        r[u] = fe_zero();
+        const fe r = S.rsh[u];
+        w = fe_mul_s(w, (wid >> (2 - u)) & 1u ? r : fe_sub(one, r));
       }
-      eq_group_rounds(X, J, 0, J, p, r, v, s, stage, polys + 2 * j, rs + j,
-                      kw ? kw + 64 * j : nullptr);
-      if (lane == 0) {
-        r_sh[0] = r[0];
-        r_sh[1] = r[1];
-        r_sh[2] = r[2];
-      }
+      S.wsplit[wid] = w;
     }
-    __syncthreads();
-    MLH_TAIL_TS(41 + 4 * (j / 3));
-    // fold m over the group's J variables (in place: output x reads corner 0 at x)
-    const fe rr[3] = {r_sh[0], r_sh[1], r_sh[2]};
-    for (uint32_t x = threadIdx.x; x < Q; x += blockDim.x) lm[x] = fold_corners_n(J, lm + x, Q, rr);
-    __syncthreads();
-    MLH_TAIL_TS(42 + 4 * (j / 3));
-    j += J;
-  }
-  if (threadIdx.x == 0) {
-    *t = s;
-    fe_store(prev, v);
-    fe_store(m_out, lm[0]);
-  }
-  if (threadIdx.x == 1) {
-    fe_store(cdev, v);
-    fe_store(d_out, v);
+    helper_barrier(S, NW, bar);
+    for (uint32_t o = wid; o < 8 * QA; o += 64 * NW) {
+      const uint32_t d = o / QA, x = o % QA;
+      acc9 q;
+      acc_zero(q);
+#pragma unroll
+      for (uint32_t h = 0; h < 8; ++h) mulacc(q, S.wsplit[h], lm[(8 * h + d) * QA + x]);
+      S.msplit[d][x] = acc_reduce(q);
+    }
+    helper_barrier(S, NW, bar);
+    if (wid == 0) lds_publish(&S.mseq, 1);
   }
 }
 
@@ -1332,9 +1607,81 @@ hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
                                    const uint32_t* kw) {
   if (a == 0 || a > kTailLogMax || Jin > 3) return hipErrorInvalidValue;
-  const size_t lds = (2ull << a) * sizeof(fe);
+  const uint32_t JA = a < 6 ? a : 6, S0 = 1u << a;
+  const size_t lds = ((1ull << a) + (1ull << (a - JA))) * sizeof(fe);  // m + e_{JA-1}
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Tin, Jin, rs_in,
-                     a, ets, pts, c, prev, t, polys, rs, m_out, d_out, kw);
+                     a, ets + (S0 - (S0 >> (JA - 1))), pts, c, prev, t, polys, rs, m_out, d_out, kw,
+                     (fe*)nullptr);
+  return hipGetLastError();
+}
+
+// Y[c] = sum_{i < 2^a} T[c 2^a + i] lo[i], c < 2^B: a workgroup takes
+// MLH_CS_CPB consecutive corners (CPB * 2^a contiguous entries); a thread's
+// lo entries stay in registers across them, its table loads are issued 8 at a
+// time, and the CPB sums leave through one block reduction.
+#ifndef MLH_CS_CPB
+#define MLH_CS_CPB 1
+#endif
+__global__ void __launch_bounds__(kRedThreads)
+corner_sums_lo_kernel(const fe* __restrict__ T, uint32_t a, const fe* __restrict__ lo,
+                      fe* __restrict__ Y) {
+  constexpr int CPB = MLH_CS_CPB, PER = 16;  // 2^a = 4096 entries: 16 per thread
+  const uint64_t Q = 1ull << a;
+  const uint32_t c0 = blockIdx.x * CPB;
+  fe lv[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) lv[k] = fe_load(lo + threadIdx.x + k * kRedThreads);
+  fe acc[CPB];
+#pragma unroll
+  for (int q = 0; q < CPB; ++q) {
+    const fe* Tc = T + (uint64_t)(c0 + q) * Q + threadIdx.x;
+    acc9 s0;
+    acc_zero(s0);
+#pragma unroll
+    for (int k0 = 0; k0 < PER; k0 += 8) {
+      fe v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = fe_load(Tc + (k0 + k) * kRedThreads);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mulacc(s0, v[k], lv[k0 + k]);
+    }
+    acc[q] = acc_reduce(s0);
+  }
+  // one block reduction of the CPB sums
+  __shared__ fe part[kRedThreads / 64][CPB];
+#pragma unroll
+  for (int q = 0; q < CPB; ++q) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) acc[q] = fe_add(acc[q], shfl_xor_fe(acc[q], m));
+  }
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < CPB; ++q) part[threadIdx.x >> 6][q] = acc[q];
+  __syncthreads();
+  if (threadIdx.x < CPB) {
+    fe x = part[0][threadIdx.x];
+    for (int w = 1; w < kRedThreads / 64; ++w) x = fe_add(x, part[w][threadIdx.x]);
+    fe_store(Y + c0 + threadIdx.x, x);
+  }
+}
+
+hipError_t launch_corner_sums_lo(const fe* T, uint32_t B, uint32_t a, const fe* lo, fe* Y,
+                                 hipStream_t st) {
+  if (B > 12 || a != 12 || (1u << B) % MLH_CS_CPB) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(corner_sums_lo_kernel, dim3((1u << B) / MLH_CS_CPB), dim3(kRedThreads), 0, st, T,
+                     a, lo, Y);
+  return hipGetLastError();
+}
+
+hipError_t launch_sumcheck_eq_head(const fe* Y, uint32_t B, const fe* e_grp, const fe* pts, fe* c,
+                                   fe* prev, DevSha* t, fe* polys, fe* rs, fe* wfold,
+                                   hipStream_t st, const uint32_t* kw) {
+  if (B == 0 || B > kTailLogMax || !wfold) return hipErrorInvalidValue;
+  const uint32_t JA = B < 6 ? B : 6;
+  const size_t lds = ((1ull << B) + (1ull << (B - JA))) * sizeof(fe);
+  hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Y, 0u,
+                     (const fe*)nullptr, B, e_grp, pts, c, prev, t, polys, rs, (fe*)nullptr,
+                     (fe*)nullptr, kw, wfold);
   return hipGetLastError();
 }
 

@@ -60,6 +60,17 @@ hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
                                    const uint32_t* kw = nullptr);
+// The first B <= 12 rounds of an eq-factored sumcheck of 2^(B + a) entries in
+// one launch each for their corner sums and their rounds: Y[c] = sum_i T[c 2^a
+// + i] lo[i] (the B-variable corner sums, lo = eq of the last a points), then
+// the tail kernel's rounds on Y (e_grp = eq of the points after its first
+// group of min(B, 6), i.e. H_{min(B,6)-1}); wfold receives the fold weights
+// of the two groups (64 + 64), for two fold_group_eq passes over T.
+hipError_t launch_corner_sums_lo(const fe* T, uint32_t B, uint32_t a, const fe* lo, fe* Y,
+                                 hipStream_t st);
+hipError_t launch_sumcheck_eq_head(const fe* Y, uint32_t B, const fe* e_grp, const fe* pts, fe* c,
+                                   fe* prev, DevSha* t, fe* polys, fe* rs, fe* wfold,
+                                   hipStream_t st, const uint32_t* kw = nullptr);
 // Setup of the eq-factored sumcheck in one launch (arguments by value): the
 // points, c_0 = 1, lo = eq(p_B..p_{L-1}), head suffix tables H (over
 // p_0..p_{B-1}), tail suffix tables Hs (optional), transcript state and claim

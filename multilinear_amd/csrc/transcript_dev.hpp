@@ -227,6 +227,63 @@ __device__ __forceinline__ void sha256_compress_kw(Sha256State& st, const uint32
   st.h[7] += h;
 }
 
+// Rounds T0..63 of one compression on the working state v = (a..h), block w
+// (big-endian words; the schedule is extended in place); mid (T0 == 0,
+// optional) receives (a..h) after round 7.  Two compressions from the same
+// chaining value whose blocks share words 0..7 share rounds 0..7 exactly: the
+// transcript's challenge after a half-block absorb (block = the 32 absorbed
+// bytes || padding) and the next absorb's block-completing compression (block
+// = the same 32 bytes || the next 32) -- the second starts at round 8 from mid.
+template <int T0>
+__device__ __forceinline__ void sha256_rounds_from(uint32_t (&v)[8], uint32_t w[16], uint32_t* mid) {
+  constexpr uint32_t K[64] = MLH_SHA_K;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) pin_vgpr(w[i]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pin_vgpr(v[i]);
+  uint32_t a = v[0], b = v[1], c = v[2], d = v[3], e = v[4], f = v[5], g = v[6], h = v[7];
+#pragma unroll
+  for (int t = T0; t < 64; ++t) {
+    if (t >= 16) {
+      const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+      w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+    }
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + K[t] + w[t & 15];
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t t2 = S0 + maj3(a, b, c);
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+    if (t == 7 && mid) {
+      mid[0] = a;
+      mid[1] = b;
+      mid[2] = c;
+      mid[3] = d;
+      mid[4] = e;
+      mid[5] = f;
+      mid[6] = g;
+      mid[7] = h;
+    }
+  }
+  v[0] = a;
+  v[1] = b;
+  v[2] = c;
+  v[3] = d;
+  v[4] = e;
+  v[5] = f;
+  v[6] = g;
+  v[7] = h;
+}
+
 // Field128::from(u128) (field.rs:138-142): one conditional subtraction of M.
 // The u128 is LE over digest bytes 0..15, i.e. limb i = bswap(h[i]).
 __device__ inline fe dsha_challenge(const DevSha& s) {
