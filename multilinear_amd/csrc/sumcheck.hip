@@ -156,6 +156,102 @@ __device__ __forceinline__ fe acc_reduce(const acc9& a) {
   return fe_add(lo, fe_mul_s(fe{{a.w[8], 0u, 0u, 0u}}, k256));
 }
 
+// Column accumulator for the HBM-streaming sums: column k (weight 2^(32k))
+// holds a 64-bit sum c[k] of the products a_i b_j with i + j = k plus a count
+// h[k] of its wraps (weight 2^(32k+64)).  One product is v_mad_u64_u32 into
+// its column (carry-out to an SGPR pair) and one v_addc into the column's
+// count: 32 VALU per mulacc and no register moves, against ~52 VALU plus ~25
+// moves for acc9's carry-chained rows.  The 16 (mad, addc) pairs are issued
+// with the addc three slots behind its mad through 4 rotating SGPR pairs,
+// which covers gfx950's VALU-SGPR-write -> VALU-read wait states.
+// Value = sum_k (c[k] + h[k] 2^64) 2^(32k) < 2^288 for < 2^32 products.
+struct acccol {
+  uint64_t c[7];  // columns 0..6 (a_3 b_3's high word sits in c[6]'s top half)
+  uint32_t h[7];
+};
+__device__ __forceinline__ void acccol_zero(acccol& a) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    a.c[k] = 0;
+    a.h[k] = 0;
+  }
+}
+__device__ __forceinline__ void mulacc_col(acccol& s, const fe& x, const fe& y) {
+  uint64_t cc0, cc1, cc2, cc3;  // carry-out pairs, rotated (product n uses pair n % 4)
+  // one statement for all 16 products (columns 0..6 each get 1..4 products)
+  asm volatile(
+      "v_mad_u64_u32 %[C0], %[q0], %[x0], %[y0], %[C0]\n\t"  // n0  (0,0) col 0
+      "v_mad_u64_u32 %[C1], %[q1], %[x0], %[y1], %[C1]\n\t"  // n1  (0,1) col 1
+      "v_mad_u64_u32 %[C2], %[q2], %[x0], %[y2], %[C2]\n\t"  // n2  (0,2) col 2
+      "v_addc_co_u32_e64 %[H0], %[q0], %[H0], 0, %[q0]\n\t"
+      "v_mad_u64_u32 %[C3], %[q3], %[x0], %[y3], %[C3]\n\t"  // n3  (0,3) col 3
+      "v_addc_co_u32_e64 %[H1], %[q1], %[H1], 0, %[q1]\n\t"
+      "v_mad_u64_u32 %[C1], %[q0], %[x1], %[y0], %[C1]\n\t"  // n4  (1,0) col 1
+      "v_addc_co_u32_e64 %[H2], %[q2], %[H2], 0, %[q2]\n\t"
+      "v_mad_u64_u32 %[C2], %[q1], %[x1], %[y1], %[C2]\n\t"  // n5  (1,1) col 2
+      "v_addc_co_u32_e64 %[H3], %[q3], %[H3], 0, %[q3]\n\t"
+      "v_mad_u64_u32 %[C3], %[q2], %[x1], %[y2], %[C3]\n\t"  // n6  (1,2) col 3
+      "v_addc_co_u32_e64 %[H1], %[q0], %[H1], 0, %[q0]\n\t"
+      "v_mad_u64_u32 %[C4], %[q3], %[x1], %[y3], %[C4]\n\t"  // n7  (1,3) col 4
+      "v_addc_co_u32_e64 %[H2], %[q1], %[H2], 0, %[q1]\n\t"
+      "v_mad_u64_u32 %[C2], %[q0], %[x2], %[y0], %[C2]\n\t"  // n8  (2,0) col 2
+      "v_addc_co_u32_e64 %[H3], %[q2], %[H3], 0, %[q2]\n\t"
+      "v_mad_u64_u32 %[C3], %[q1], %[x2], %[y1], %[C3]\n\t"  // n9  (2,1) col 3
+      "v_addc_co_u32_e64 %[H4], %[q3], %[H4], 0, %[q3]\n\t"
+      "v_mad_u64_u32 %[C4], %[q2], %[x2], %[y2], %[C4]\n\t"  // n10 (2,2) col 4
+      "v_addc_co_u32_e64 %[H2], %[q0], %[H2], 0, %[q0]\n\t"
+      "v_mad_u64_u32 %[C5], %[q3], %[x2], %[y3], %[C5]\n\t"  // n11 (2,3) col 5
+      "v_addc_co_u32_e64 %[H3], %[q1], %[H3], 0, %[q1]\n\t"
+      "v_mad_u64_u32 %[C3], %[q0], %[x3], %[y0], %[C3]\n\t"  // n12 (3,0) col 3
+      "v_addc_co_u32_e64 %[H4], %[q2], %[H4], 0, %[q2]\n\t"
+      "v_mad_u64_u32 %[C4], %[q1], %[x3], %[y1], %[C4]\n\t"  // n13 (3,1) col 4
+      "v_addc_co_u32_e64 %[H5], %[q3], %[H5], 0, %[q3]\n\t"
+      "v_mad_u64_u32 %[C5], %[q2], %[x3], %[y2], %[C5]\n\t"  // n14 (3,2) col 5
+      "v_addc_co_u32_e64 %[H3], %[q0], %[H3], 0, %[q0]\n\t"
+      "v_mad_u64_u32 %[C6], %[q3], %[x3], %[y3], %[C6]\n\t"  // n15 (3,3) col 6
+      "v_addc_co_u32_e64 %[H4], %[q1], %[H4], 0, %[q1]\n\t"
+      "v_addc_co_u32_e64 %[H5], %[q2], %[H5], 0, %[q2]\n\t"
+      "v_addc_co_u32_e64 %[H6], %[q3], %[H6], 0, %[q3]"
+      : [C0] "+v"(s.c[0]), [C1] "+v"(s.c[1]), [C2] "+v"(s.c[2]), [C3] "+v"(s.c[3]),
+        [C4] "+v"(s.c[4]), [C5] "+v"(s.c[5]), [C6] "+v"(s.c[6]), [H0] "+v"(s.h[0]),
+        [H1] "+v"(s.h[1]), [H2] "+v"(s.h[2]), [H3] "+v"(s.h[3]), [H4] "+v"(s.h[4]),
+        [H5] "+v"(s.h[5]), [H6] "+v"(s.h[6]), [q0] "=&s"(cc0), [q1] "=&s"(cc1), [q2] "=&s"(cc2),
+        [q3] "=&s"(cc3)
+      : [x0] "v"(x.w[0]), [x1] "v"(x.w[1]), [x2] "v"(x.w[2]), [x3] "v"(x.w[3]), [y0] "v"(y.w[0]),
+        [y1] "v"(y.w[1]), [y2] "v"(y.w[2]), [y3] "v"(y.w[3]));
+}
+// Limbs of a column accumulator (< 2^288 by the bound above).
+__device__ __forceinline__ acc9 acccol_limbs(const acccol& s) {
+  acc9 r;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    uint64_t t = carry;
+    if (k < 7) t += (uint32_t)s.c[k];
+    if (k >= 1 && k <= 7) t += s.c[k - 1] >> 32;
+    if (k >= 2) t += s.h[k - 2];
+    r.w[k] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  return r;
+}
+
+// Accumulator of the HBM-streaming corner-sum kernels.
+#ifndef MLH_ACCCOL
+#define MLH_ACCCOL 1
+#endif
+#if MLH_ACCCOL
+using sacc = acccol;
+__device__ __forceinline__ void sacc_zero(sacc& a) { acccol_zero(a); }
+__device__ __forceinline__ void sacc_mac(sacc& a, const fe& x, const fe& y) { mulacc_col(a, x, y); }
+__device__ __forceinline__ fe sacc_reduce(const sacc& a) { return acc_reduce(acccol_limbs(a)); }
+#else
+using sacc = acc9;
+__device__ __forceinline__ void sacc_zero(sacc& a) { acc_zero(a); }
+__device__ __forceinline__ void sacc_mac(sacc& a, const fe& x, const fe& y) { mulacc(a, x, y); }
+__device__ __forceinline__ fe sacc_reduce(const sacc& a) { return acc_reduce(a); }
+#endif
+
 // Fold of 2^J values in registers (index MSB = the first variable) with
 // r[0..J-1]; v[0] ends with the folded value.
 template <int J>
@@ -295,9 +391,9 @@ group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe*
     __syncthreads();
     H = hs;
   }
-  acc9 s0, s1;  // unreduced (two for ILP); < 2^288 for < 2^32 products each
-  acc_zero(s0);
-  acc_zero(s1);
+  sacc s0, s1;  // unreduced (two for ILP); < 2^288 for < 2^32 products each
+  sacc_zero(s0);
+  sacc_zero(s1);
   const uint64_t stride = (uint64_t)nbc * blockDim.x;
   const uint64_t i0 = (uint64_t)bb * blockDim.x + threadIdx.x;
   uint64_t i = i0;
@@ -307,10 +403,10 @@ group_sums_eq_kernel(const fe* __restrict__ T, uint64_t S, uint32_t J, const fe*
 #pragma unroll
     for (int u = 0; u < MLH_GS_UNROLL; ++u) v[u] = fe_load(Tc + i + u * stride);
 #pragma unroll
-    for (int u = 0; u < MLH_GS_UNROLL; ++u) mulacc((u & 1) ? s1 : s0, v[u], fe_load(H + ((i + u * stride) >> a)));
+    for (int u = 0; u < MLH_GS_UNROLL; ++u) sacc_mac((u & 1) ? s1 : s0, v[u], fe_load(H + ((i + u * stride) >> a)));
   }
-  for (; i < Q; i += stride) mulacc(s0, fe_load(Tc + i), fe_load(H + (i >> a)));
-  fe acc = fe_add(acc_reduce(s0), acc_reduce(s1));
+  for (; i < Q; i += stride) sacc_mac(s0, fe_load(Tc + i), fe_load(H + (i >> a)));
+  fe acc = fe_add(sacc_reduce(s0), sacc_reduce(s1));
   if (i0 < Q) acc = fe_mul_s(acc, fe_load(lo + (i0 & ((1ull << a) - 1))));
   fe z = fe_zero();
   block_reduce2(acc, z);
@@ -364,7 +460,7 @@ fold_group_eq_kernel(const fe* Tin, uint64_t S, uint32_t JN, const fe* __restric
         v = lerp_s(hi ? o : v, hi ? v : o, r[JH + u]);
       }
     } else {
-      acc9 t;
+      acc9 t;  // (the column accumulator measured slower here: 24 registers per output)
       acc_zero(t);
 #pragma unroll
       for (int c0 = 0; c0 < (1 << J); c0 += 8) {  // 8 loads in flight at a time
@@ -1635,17 +1731,17 @@ corner_sums_lo_kernel(const fe* __restrict__ T, uint32_t a, const fe* __restrict
 #pragma unroll
   for (int q = 0; q < CPB; ++q) {
     const fe* Tc = T + (uint64_t)(c0 + q) * Q + threadIdx.x;
-    acc9 s0;
-    acc_zero(s0);
+    sacc s0;
+    sacc_zero(s0);
 #pragma unroll
     for (int k0 = 0; k0 < PER; k0 += 8) {
       fe v[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = fe_load(Tc + (k0 + k) * kRedThreads);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) mulacc(s0, v[k], lv[k0 + k]);
+      for (int k = 0; k < 8; ++k) sacc_mac(s0, v[k], lv[k0 + k]);
     }
-    acc[q] = acc_reduce(s0);
+    acc[q] = sacc_reduce(s0);
   }
   // one block reduction of the CPB sums
   __shared__ fe part[kRedThreads / 64][CPB];
@@ -1698,3 +1794,14 @@ hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, ui
 }
 
 }  // namespace mlh
+
+#ifdef MLH_COOP_PROF
+// Dev builds only (tools/coop_pipeline.py): the last cooperative launch's
+// per-round stamps (g_coop_ts, 10 x 64) and edges (g_coop_edge, 4).
+extern "C" int mlh_debug_coop_stamps(uint64_t* ts_out, uint64_t* edge_out) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(ts_out, HIP_SYMBOL(mlh::g_coop_ts), sizeof(uint64_t) * 640) != hipSuccess)
+    return 1;
+  return hipMemcpyFromSymbol(edge_out, HIP_SYMBOL(mlh::g_coop_edge), sizeof(uint64_t) * 4) != hipSuccess;
+}
+#endif
