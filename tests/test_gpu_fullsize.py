@@ -128,14 +128,16 @@ def test_config3_rs_2_25_and_fri_commit_vs_c_oracle():
 # ---- config 4: 24-variable sumcheck rounds (sumcheck.rs:77-247) ----
 
 @pytest.mark.slow
-@pytest.mark.parametrize("n", [17, 19, 20, 24])
-def test_config4_sumcheck_24_vars_vs_c_oracle(n):
+@pytest.mark.parametrize("n,label", [(17, b""), (19, b""), (20, b"abc"), (22, b"x" * 33), (24, b"")])
+def test_config4_sumcheck_24_vars_vs_c_oracle(n, label):
     """build_tables_for_pcs + compute_sumcheck_polynomials at 24 variables
     (the GPU keeps delta = eq(point) factored) against the reference round loop
     driven by the C oracle's eq table, partial sums and folds and the Python
     transcript: every round polynomial, every challenge, the final transcript.
-    n = 17 / 19 / 20 split the n - 12 eq-factored head rounds into groups
-    3+2 / 3+3+1 / 3+3+2 (one HBM pass per group), n = 24 into 3+3+3+3."""
+    n = 17 runs the head as separate launches (corner sums, 5 rounds, folds);
+    n = 19..24 (7..12 head rounds) the fused cooperative launch, whose second
+    head group has 1 / 2 / 4 / 6 variables; the 3- and 33-byte transcript
+    prefixes send every absorb through the device transcript's byte path."""
     Cq = _c()
     ev = D.random_limbs(1 << n, 2424)
     pts = _rand(n, 24)
@@ -143,6 +145,7 @@ def test_config4_sumcheck_24_vars_vs_c_oracle(n):
     d = Cq.eq_table_par(pts)
     total = Cq.dot_par(m, d, n)
     tr = OT.Transcript()
+    tr.absorb(label)
     prev = total
     want_polys, want_rs = [], []
     for k in range(n):
@@ -158,6 +161,7 @@ def test_config4_sumcheck_24_vars_vs_c_oracle(n):
         Cq.fold_par(m, d, lh, r)
         m, d = m[: 1 << (lh - 1)], d[: 1 << (lh - 1)]
     gtr = Transcript()
+    gtr.absorb(label)
     polys, rs = MS.SumcheckTables.build_tables_for_pcs(pts, D.to_device(ev)).compute_sumcheck_polynomials(
         total, gtr)
     assert rs == want_rs
