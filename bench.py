@@ -154,6 +154,21 @@ def load_valu(kernel):
     return None
 
 
+def load_sumcheck_pmc():
+    """(bytes per config-4 prove, source) from the newest committed
+    profiles/*_sumcheck_pmc.json (tools/sumcheck_pmc.py), or None."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sumcheck_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("bytes_per_prove"):
+            return d["bytes_per_prove"], os.path.basename(path)
+    return None
+
+
 def load_valu_profile():
     """Per-kernel VALU issue reading of every config's dominant kernels from the
     newest committed rocprofv3 VALU pass (profile-derived, not live): lane
@@ -542,11 +557,21 @@ def main():
         sc_ms = sum(sc_times[5:]) / 20 * 1e3  # the call synchronises; first 5 = warm-up
         del work
         result["sumcheck_ms"] = sc_ms
-        # algorithmic bytes of the factored rounds: round 0 reads the evaluations,
-        # each fold reads S and writes S/2 (the first fold reads the evaluations
-        # and writes a half-size table: no matrix clone)
-        sc_bytes = 16 * N + sum(24 * (N >> k) for k in range(log_n))
-        result["sumcheck_hbm_frac"] = sc_bytes / (sc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+        # HBM fraction of the prove, two ways: on SURVEY §8(d)'s
+        # algorithmic bytes of the reference schedule (per round: read matrix +
+        # delta, write both folded; plus the 2^24-entry eq table = 1.88 GB), and
+        # on the bytes the grouped eq-factored path actually moves, from the
+        # newest committed FETCH_SIZE / WRITE_SIZE passes (tools/sumcheck_pmc.py)
+        survey_bytes = sum(48 * (N >> k) for k in range(log_n)) + 16 * N
+        hf = {"survey_schedule": {"bytes": survey_bytes,
+                                  "frac": survey_bytes / (sc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                  "what": "SURVEY §8(d): sum over rounds of 2 S 16 B read + S 16 B "
+                                          "written, plus the 2^24-entry eq table"}}
+        pmc = load_sumcheck_pmc() if log_n == 24 else None
+        if pmc:
+            hf["measured"] = {"bytes": pmc[0], "frac": pmc[0] / (sc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                              "what": "rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per prove (%s)" % pmc[1]}
+        result["sumcheck_hbm_frac"] = hf
 
         # PCSProof::prove (multilinear_pcs.rs:90-136) on the 2^log_n evaluations:
         # Moebius + fused bit-reverse/RS (2^(log_n+1) code) + log_n interleaved

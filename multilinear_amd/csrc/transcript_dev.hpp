@@ -227,14 +227,14 @@ __device__ __forceinline__ void sha256_compress_kw(Sha256State& st, const uint32
   st.h[7] += h;
 }
 
-// Rounds T0..63 of one compression on the working state v = (a..h), block w
+// Rounds T0..T1-1 of one compression on the working state v = (a..h), block w
 // (big-endian words; the schedule is extended in place); mid (T0 == 0,
 // optional) receives (a..h) after round 7.  Two compressions from the same
 // chaining value whose blocks share words 0..7 share rounds 0..7 exactly: the
 // transcript's challenge after a half-block absorb (block = the 32 absorbed
 // bytes || padding) and the next absorb's block-completing compression (block
 // = the same 32 bytes || the next 32) -- the second starts at round 8 from mid.
-template <int T0>
+template <int T0, int T1 = 64>
 __device__ __forceinline__ void sha256_rounds_from(uint32_t (&v)[8], uint32_t w[16], uint32_t* mid) {
   constexpr uint32_t K[64] = MLH_SHA_K;
 #pragma unroll
@@ -243,7 +243,7 @@ __device__ __forceinline__ void sha256_rounds_from(uint32_t (&v)[8], uint32_t w[
   for (int i = 0; i < 8; ++i) pin_vgpr(v[i]);
   uint32_t a = v[0], b = v[1], c = v[2], d = v[3], e = v[4], f = v[5], g = v[6], h = v[7];
 #pragma unroll
-  for (int t = T0; t < 64; ++t) {
+  for (int t = T0; t < T1; ++t) {
     if (t >= 16) {
       const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
       const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);

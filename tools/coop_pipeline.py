@@ -36,11 +36,23 @@ us = lambda c: c / (ghz * 1e3)
 R = int(os.environ.get("R", "12"))
 print("clock %.2f GHz; entry -> roles %.2f us; roles -> last r %.2f us" %
       (ghz, us(ed[2] - ed[0]), us(T[3][R - 1] - ed[2])))
+print("prologue (wave 0, vs entry): loads+stores %.2f, first barrier %.2f, roles %.2f us" % (
+    us(T[9][10] - ed[0]), us(T[9][11] - ed[0]), us(ed[2] - ed[0])))
+print("round 0 helpers vs roles: corner ts6 %.2f ts7 %.2f; coef start %.2f got-ab %.2f slot %.2f" % (
+    us(T[6][0] - ed[2]), us(T[7][0] - ed[2]), us(T[5][0] - ed[2]), us(T[8][0] - ed[2]), us(T[4][0] - ed[2])))
 print("round   wait  eval+absorb  challenge  slot_ready(vs r_{k-2})")
 for k in range(R):
     lag = us(T[4][k] - T[3][k - 2]) if k >= 2 else 0.0
     print("%5d %6.2f %12.2f %10.2f %12.2f" % (k, us(T[1][k] - T[0][k]), us(T[2][k] - T[1][k]),
                                              us(T[3][k] - T[2][k]), lag))
+print("msplit published %.2f us after r_2; corner wave round-6 work done %.2f us after r_4" %
+      (us(T[9][0] - T[3][2]), us(T[6][6] - T[3][4])))
+print("wave 3: rehearsal done %.2f us after roles; fold levels (got r_u, done) vs roles: %s" % (
+    us(T[9][1] - ed[2]), " ".join("%.2f/%.2f" % (us(T[9][2 + 2 * u] - ed[2]), us(T[9][3 + 2 * u] - ed[2])) for u in range(3))))
+print("r_k published vs roles: %s" % " ".join("%.2f" % us(T[3][k] - ed[2]) for k in range(R)))
+print("corner wave: round  start->ts6(after transition/weights)  ts6->ts7(bucket+publish)")
+for k in range(2, R):
+    print("       %5d %8.2f %8.2f" % (k, us(T[6][k] - T[3][k - 2]), us(T[7][k] - T[6][k])))
 print("helper: round  eval  ->ab  ->slot")
 for k in range(1, R):
     print("       %5d %6.2f %6.2f %6.2f" % (k, us(T[8][k] - T[5][k]), 0.0, us(T[4][k] - T[8][k])))
