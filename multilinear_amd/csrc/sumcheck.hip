@@ -1547,26 +1547,31 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
   __shared__ DevSha s;
   __shared__ uint32_t stage[8];
   __shared__ CoopSync S;
-  if (threadIdx.x < sizeof(DevSha) / 4)
-    reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
-  if (threadIdx.x == 0) {
-    S.coef_seq = S.r_seq = S.hbar = S.mseq = S.fail = S.ab_seq = 0;
-    S.mid_len = ~0ull;
-  }
-  if (threadIdx.x < a) S.pg[threadIdx.x] = fe_load(pts + threadIdx.x);
   const uint32_t S0 = 1u << a;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // every HBM read of the prologue is issued before the first LDS store (a
+  // store of a loaded value waits for it): transcript state, points, and for
+  // plain copies the table (2^a / 256 <= 16 per thread) and e
+  const uint32_t sw = threadIdx.x < sizeof(DevSha) / 4 ? reinterpret_cast<const uint32_t*>(t)[threadIdx.x] : 0u;
+  const fe pgv = threadIdx.x < a ? fe_load(pts + threadIdx.x) : fe_zero();
+  constexpr uint32_t PER = (1u << kTailLogMax) / kRedThreads;
+  fe v[PER];
   if (Jin == 0) {
-    // plain copies: every HBM read of the prologue in flight at once (the
-    // table, 2^a / 256 <= 16 per thread, and e), then the groups' suffix
-    // products (their points' loads too), then the LDS stores
-    constexpr uint32_t PER = (1u << kTailLogMax) / kRedThreads;
-    fe v[PER];
 #pragma unroll
     for (uint32_t u = 0; u < PER; ++u) {
       const uint32_t x = u * kRedThreads + threadIdx.x;
       v[u] = x < S0 ? fe_load(Tin + x) : fe_zero();
     }
+  }
+  if (threadIdx.x < sizeof(DevSha) / 4) reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = sw;
+  if (threadIdx.x == 0) {
+    S.coef_seq = S.r_seq = S.hbar = S.mseq = S.fail = S.ab_seq = 0;
+    S.mid_len = ~0ull;
+  }
+  if (threadIdx.x < a) S.pg[threadIdx.x] = pgv;
+  if (Jin == 0) {
+    // plain copies: the groups' suffix products (their points' loads too),
+    // then the LDS stores
     const fe ev = threadIdx.x < QA ? fe_load(e_grp + threadIdx.x) : fe_zero();
     if (wave == 2) suffix_products(JA, pts, S.rsuf);
     if (wave == 3 && JB) suffix_products(JB, pts + JA, S.rsufB);
