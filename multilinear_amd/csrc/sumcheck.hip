@@ -1090,67 +1090,94 @@ __device__ void transcript_rounds(CoopSync& S, uint32_t R, DevSha& s, uint32_t* 
     const fe v = pqrst(sl[0], r, sl[1], sl[2], r);  // lane 0: c1, lane 1: c2
     const fe c2 = bcast_fe(v, 1);
     fe rr = fe_zero();
-    if (lane == 0) {
-      const fe c1 = v;
-      if (!dry) {
-        fe_store(polys + 2 * k, c1);
-        fe_store(polys + 2 * k + 1, c2);
-      }
-      const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
-      // absorb LE16(c1) || LE16(c2) (sumcheck.rs:188-199), then r = next_challenge()
-      uint32_t* bw = reinterpret_cast<uint32_t*>(s.buf);
-      const uint32_t pos = (uint32_t)(s.len & 63);
-      const bool half = (s.len & 3) == 0 && pos == 0;
-      if (half || ((s.len & 3) == 0 && pos == 32 && *mid_len == s.len)) {
-        // half: the challenge compresses the 32 bytes + padding, and its rounds
-        // 0..7 are kept for the next absorb's compression; else the block
-        // completes and its first 8 rounds were run by the last challenge.
-        // Both continue in ONE copy of rounds 8..63 (the rehearsal of one path
-        // brings the other's code into the instruction cache).
-        uint32_t blk[16], v[8];
-        if (half) {
+    // wave-uniform from here (lanes 0 and 1 run the compressions together,
+    // two-lane SHA-256: transcript_dev.hpp sha2l_*); LDS state written by lane 0
+    const fe c1 = bcast_fe(v, 0);
+    if (!dry && lane == 0) {
+      fe_store(polys + 2 * k, c1);
+      fe_store(polys + 2 * k + 1, c2);
+    }
+    const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
+    // absorb LE16(c1) || LE16(c2) (sumcheck.rs:188-199), then r = next_challenge()
+    uint32_t* bw = reinterpret_cast<uint32_t*>(s.buf);
+    const uint64_t len0 = s.len;
+    const uint32_t pos = (uint32_t)(len0 & 63);
+    const bool half = (len0 & 3) == 0 && pos == 0;
+    if (half || ((len0 & 3) == 0 && pos == 32 && *mid_len == len0)) {
+      // half: the challenge compresses the 32 bytes + padding, and its rounds
+      // 0..7 are kept for the next absorb's compression; else the block
+      // completes and its first 8 rounds were run by the last challenge.
+      // Both continue in ONE copy of rounds 8..63 (the rehearsal of one path
+      // brings the other's code into the instruction cache).
+      constexpr uint32_t K[64] = MLH_SHA_K;
+      uint32_t blk[16], st[8];
+      if (half) {
+        const uint64_t bits = (len0 + 32) * 8;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) bw[i] = w[i];
-          s.len += 32;
-          const uint64_t bits = s.len * 8;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            blk[i] = bswap32(w[i]);
-            blk[8 + i] = 0;
-            v[i] = s.h[i];
-          }
-          blk[8] = 0x80000000u;
-          blk[14] = (uint32_t)(bits >> 32);
-          blk[15] = (uint32_t)bits;
-          if (!dry) MLH_COOP_TS(2, k);
-          sha256_rounds_from<0, 8>(v, blk, mid);
-          *mid_len = s.len;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            blk[i] = bswap32(bw[i]);
-            blk[8 + i] = bswap32(w[i]);
-            v[i] = mid[i];
-          }
+        for (int i = 0; i < 8; ++i) {
+          blk[i] = bswap32(w[i]);
+          blk[8 + i] = 0;
+          st[i] = s.h[i];
         }
-        sha256_rounds_from<8>(v, blk, nullptr);
-        if (half) {
-          fe o;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) o.w[i] = bswap32(s.h[i] + v[i]);
-          rr = canon_with_carry(o, 0u);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) s.h[i] += v[i];
-          s.len += 32;
-          if (!dry) MLH_COOP_TS(2, k);
-          rr = dsha_challenge_kw(s, kw ? kw + 64 * k : nullptr);
-        }
+        blk[8] = 0x80000000u;
+        blk[14] = (uint32_t)(bits >> 32);
+        blk[15] = (uint32_t)bits;
       } else {
-        dsha_absorb<8>(s, w, stage);
-        if (!dry) MLH_COOP_TS(2, k);
-        rr = dsha_challenge_kw(s, kw ? kw + 64 * k : nullptr);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          blk[i] = bswap32(bw[i]);
+          blk[8 + i] = bswap32(w[i]);
+          st[i] = mid[i];
+        }
       }
+      auto kwf = [&](int t) -> uint32_t {
+        if (t >= 16) sha_sched(blk, t);
+        return K[t] + blk[t & 15];
+      };
+      Sha2L q;
+      if (half) {
+        if (!dry) MLH_COOP_TS(2, k);
+        sha2l_init(q, st);
+        sha2l_rounds<0, 8>(q, kwf);
+        sha2l_state(q, st);
+        if (lane == 0) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            bw[i] = w[i];
+            mid[i] = st[i];
+          }
+          s.len = len0 + 32;
+          *mid_len = len0 + 32;
+        }
+      }
+      sha2l_init(q, st);
+      sha2l_rounds<8, 64>(q, kwf);
+      uint32_t vv[8];
+      sha2l_state(q, vv);
+      if (half) {
+        fe o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o.w[i] = bswap32(s.h[i] + vv[i]);
+        rr = canon_with_carry(o, 0u);
+      } else {
+        uint32_t nh[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) nh[i] = s.h[i] + vv[i];
+        if (lane == 0) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) s.h[i] = nh[i];
+          s.len = len0 + 32;
+        }
+        if (!dry) MLH_COOP_TS(2, k);
+        rr = kw ? sha2l_pad_challenge(nh[0], nh[1], nh[2], nh[3], nh[4], nh[5], nh[6], nh[7], kw + 64 * k)
+                : dsha_challenge(s);
+      }
+    } else {
+      if (lane == 0) dsha_absorb<8>(s, w, stage);
+      if (!dry) MLH_COOP_TS(2, k);
+      if (lane == 0) rr = dsha_challenge_kw(s, kw ? kw + 64 * k : nullptr);
+    }
+    if (lane == 0) {
       if (!dry) {
         fe_store(rs + k, rr);
         S.rsh[k] = rr;
@@ -1165,24 +1192,31 @@ __device__ void transcript_rounds(CoopSync& S, uint32_t R, DevSha& s, uint32_t* 
   }
 }
 
-// An idle wave's rehearsal of transcript_rounds' round code (one half-block
-// round: the compression body is shared with the block-completing path) and
-// of the padding-block challenge, on a scratch copy of the state (see `dry`),
-// while the real rounds wait for round 0's coefficients.  Measured: the first
-// challenge 5.2 -> 2.9 us.
-__device__ void transcript_rehearsal(CoopSync& S, const DevSha& s, const uint32_t* kw) {
-  __shared__ DevSha sdry;
-  __shared__ uint32_t dmid[8];
-  __shared__ uint64_t dmid_len;
-  if ((threadIdx.x & 63) == 0) {
-    sdry = s;
-    sdry.len = 0;
-    dmid_len = ~0ull;
-  }
-  transcript_rounds(S, 1, sdry, nullptr, nullptr, nullptr, kw, true, dmid, &dmid_len);
-  if (kw && (threadIdx.x & 63) == 0) {  // the padding-block challenge (out of line)
-    sdry.len = 64;
-    sdry.h[1] ^= dsha_challenge_kw(sdry, kw).w[0];
+// Rehearsals that bring the transcript's code into the instruction cache
+// before the real rounds run it (on a cold CU the first pass through a
+// compression costs ~3 us more): round = one half-block round on a scratch
+// state (see `dry`; its compression body is shared with the block-completing
+// path), run by wave 0 itself while round 0's coefficients are being built;
+// otherwise the padding-block challenge, run by an idle wave.
+#ifndef MLH_REH
+#define MLH_REH 2  // 0: none; 1: wave 3 a round + the pad challenge; 2: wave 0 a round, wave 3 the pad
+#endif
+__device__ void transcript_rehearsal(CoopSync& S, const DevSha& s, const uint32_t* kw, bool round) {
+  if (round) {  // one half-block round on a scratch state
+    __shared__ DevSha sdry;
+    __shared__ uint32_t dmid[8];
+    __shared__ uint64_t dmid_len;
+    if ((threadIdx.x & 63) == 0) {
+      sdry = s;
+      sdry.len = 0;
+      dmid_len = ~0ull;
+    }
+    transcript_rounds(S, 1, sdry, nullptr, nullptr, nullptr, kw, true, dmid, &dmid_len);
+  } else if (kw) {  // the padding-block challenge (out of line, two lanes; result discarded)
+    __shared__ volatile uint32_t sink;  // (keeps the call: its result is discarded)
+    (void)sink;
+    const fe o = sha2l_pad_challenge(s.h[0], s.h[1], s.h[2], s.h[3], s.h[4], s.h[5], s.h[6], s.h[7], kw);
+    if ((threadIdx.x & 63) == 0) sink = o.w[0];
   }
 }
 
@@ -1497,13 +1531,15 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
   MLH_COOP_EDGE(1);
   const uint32_t tend = J2 ? JT : t1;
   if (wave == 0) {
+    if (MLH_REH == 2) transcript_rehearsal(S, s, kw ? kw + 64 * t0 : nullptr, true);
     transcript_rounds(S, tend - t0, s, stage, polys, rs + t0, kw ? kw + 64 * t0 : nullptr, false, S.mid,
                       &S.mid_len);
     if (lane == 0) *t = s;
   } else if (wave == 1) {
     coef_rounds(S, t0, tend, prev, cdev, nullptr, claim0, cs0);
   } else if (wave == 3) {
-    transcript_rehearsal(S, s, kw ? kw + 64 * t0 : nullptr);
+    if (MLH_REH == 1) transcript_rehearsal(S, s, kw ? kw + 64 * t0 : nullptr, true);
+    if (MLH_REH != 0) transcript_rehearsal(S, s, kw ? kw + 64 * t0 : nullptr, false);
   } else if (wave == 2) {
     fe X = fe_zero();
     const uint32_t per = G / GW;  // slots per corner
@@ -1619,6 +1655,7 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
   __syncthreads();
   MLH_COOP_EDGE(1);
   if (wave == 0) {
+    if (MLH_REH == 2) transcript_rehearsal(S, s, kw, true);
     transcript_rounds(S, a, s, stage, polys, rs, kw, false, S.mid, &S.mid_len);
     if (lane == 0) *t = s;
   } else if (wave == 1) {
@@ -1631,7 +1668,8 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
     // fold m in place over variables 0, 1, 2 as r_0, r_1, r_2 come out, so
     // that lm[d QA + x] (d: the bits of variables 3, 4, 5) is group B's split
     // table well before the corner wave's round-6 transition needs it.
-    transcript_rehearsal(S, s, kw);
+    if (MLH_REH == 1) transcript_rehearsal(S, s, kw, true);
+    if (MLH_REH != 0) transcript_rehearsal(S, s, kw, false);
     MLH_COOP_TS(9, 1);
     if (JB) {
       uint32_t n = 1u << a;

@@ -284,6 +284,101 @@ __device__ __forceinline__ void sha256_rounds_from(uint32_t (&v)[8], uint32_t w[
   v[7] = h;
 }
 
+// ---- two-lane SHA-256 rounds ------------------------------------------------
+// A one-lane compression issues ~14 VALU per round (6 v_alignbit, 4 v_bitop3,
+// 4 adds).  Lane pairs (2i, 2i+1) share a round in SIMT form: the even lane
+// holds (e, f, g, h) and the odd lane (a, b, c, d) of the working state, and
+// one instruction stream computes Sigma1(e) | Sigma0(a) (v_alignbit with
+// per-lane counts), Ch(e, f, g) | Maj(a, b, c) (= bfi(e, f, g) | bfi(a ^ c,
+// b, c)), T1 = h + Sigma1 + Ch + K + W | T2 = Sigma0 + Maj, and the new e |
+// new a = d + T1 | T1 + T2 through one quad_perm DPP exchange: 11 VALU per
+// round.  Every lane pair computes the same compression; inputs are
+// wave-uniform.
+struct Sha2L {
+  uint32_t r0, r1, r2, r3;  // even lane: e f g h; odd lane: a b c d
+  uint32_t m;               // odd lane ~0, even lane 0
+  uint32_t s1, s2, s3;      // the lane's Sigma rotation counts
+};
+__device__ __forceinline__ void sha2l_init(Sha2L& q, const uint32_t (&v)[8]) {
+  const bool odd = __lane_id() & 1u;
+  q.m = odd ? ~0u : 0u;
+  q.r0 = odd ? v[0] : v[4];
+  q.r1 = odd ? v[1] : v[5];
+  q.r2 = odd ? v[2] : v[6];
+  q.r3 = odd ? v[3] : v[7];
+  q.s1 = odd ? 2u : 6u;
+  q.s2 = odd ? 13u : 11u;
+  q.s3 = odd ? 22u : 25u;
+}
+// The working state a..h, wave-uniform (read from lanes 1 and 0).
+__device__ __forceinline__ void sha2l_state(const Sha2L& q, uint32_t (&v)[8]) {
+  v[0] = __builtin_amdgcn_readlane(q.r0, 1);
+  v[1] = __builtin_amdgcn_readlane(q.r1, 1);
+  v[2] = __builtin_amdgcn_readlane(q.r2, 1);
+  v[3] = __builtin_amdgcn_readlane(q.r3, 1);
+  v[4] = __builtin_amdgcn_readlane(q.r0, 0);
+  v[5] = __builtin_amdgcn_readlane(q.r1, 0);
+  v[6] = __builtin_amdgcn_readlane(q.r2, 0);
+  v[7] = __builtin_amdgcn_readlane(q.r3, 0);
+}
+// Rounds T0..T1-1; kwf(t) returns K[t] + W[t] (wave-uniform) and is called
+// once per t in increasing order (so it may extend the message schedule).
+template <int T0, int T1, class KWF>
+__device__ __forceinline__ void sha2l_rounds(Sha2L& q, KWF&& kwf) {
+  uint32_t x = (q.r3 + kwf(T0)) & ~q.m;  // even lane: h + K + W; odd lane: 0
+#pragma unroll
+  for (int t = T0; t < T1; ++t) {
+    const uint32_t sg = xor3(__builtin_amdgcn_alignbit(q.r0, q.r0, q.s1),
+                             __builtin_amdgcn_alignbit(q.r0, q.r0, q.s2),
+                             __builtin_amdgcn_alignbit(q.r0, q.r0, q.s3));
+    const uint32_t p = q.r0 ^ (q.r2 & q.m);       // e | a ^ c
+    const uint32_t f = (p & q.r1) | (~p & q.r2);  // Ch | Maj
+    const uint32_t u = sg + f + x;                // T1 | T2
+    const uint32_t y = (q.m & q.r3) | (~q.m & u); // T1 | d
+    if (t + 1 < T1) x = (q.r2 + kwf(t + 1)) & ~q.m;  // the next round's h + K + W
+    q.r3 = q.r2;
+    q.r2 = q.r1;
+    q.r1 = q.r0;
+    // pair swap (quad_perm [1,0,3,2]) folded into the add: d + T1 | T1 + T2
+    q.r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, 0xB1, 0xF, 0xF, true) + u;
+  }
+}
+// Message-schedule word t (t >= 16) in place in w[16].
+__device__ __forceinline__ uint32_t sha_sched(uint32_t* w, int t) {
+  const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+  const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+  const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+  return w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+}
+
+// next_challenge() after an absorb that ended on a block boundary (chaining
+// value h0..h7, wave-uniform): the padding-only block from its precomputed
+// K + W table, on two lanes; Field128::from of the digest's first 16 bytes.
+// Out of line, so a rehearsal of it warms the code the rounds run.
+__device__ __noinline__ fe sha2l_pad_challenge(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                               uint32_t h4, uint32_t h5, uint32_t h6, uint32_t h7,
+                                               const uint32_t* kw) {
+  const uint32_t h[8] = {h0, h1, h2, h3, h4, h5, h6, h7};
+  uint32_t k[64];
+#pragma unroll
+  for (int t = 0; t < 64; t += 4) {
+    const uint4 x = *reinterpret_cast<const uint4*>(kw + t);
+    k[t] = x.x;
+    k[t + 1] = x.y;
+    k[t + 2] = x.z;
+    k[t + 3] = x.w;
+  }
+  Sha2L q;
+  sha2l_init(q, h);
+  sha2l_rounds<0, 64>(q, [&](int t) -> uint32_t { return k[t]; });
+  uint32_t v[8];
+  sha2l_state(q, v);
+  fe o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o.w[i] = bswap32(h[i] + v[i]);
+  return canon_with_carry(o, 0u);
+}
+
 // Field128::from(u128) (field.rs:138-142): one conditional subtraction of M.
 // The u128 is LE over digest bytes 0..15, i.e. limb i = bswap(h[i]).
 __device__ inline fe dsha_challenge(const DevSha& s) {
