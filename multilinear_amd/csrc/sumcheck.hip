@@ -1654,6 +1654,9 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
   }
   __syncthreads();
   MLH_COOP_EDGE(1);
+#ifdef MLH_COOP_PROF
+  if (lane == 0) g_coop_ts[9][20 + wave] = __builtin_amdgcn_s_getreg(4 | (31 << 11));  // HW_ID: SIMD in bits 5:4
+#endif
   if (wave == 0) {
     if (MLH_REH == 2) transcript_rehearsal(S, s, kw, true);
     transcript_rounds(S, a, s, stage, polys, rs, kw, false, S.mid, &S.mid_len);

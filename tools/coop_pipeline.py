@@ -40,6 +40,8 @@ print("prologue (wave 0, vs entry): loads+stores %.2f, first barrier %.2f, roles
     us(T[9][10] - ed[0]), us(T[9][11] - ed[0]), us(ed[2] - ed[0])))
 print("round 0 helpers vs roles: corner ts6 %.2f ts7 %.2f; coef start %.2f got-ab %.2f slot %.2f" % (
     us(T[6][0] - ed[2]), us(T[7][0] - ed[2]), us(T[5][0] - ed[2]), us(T[8][0] - ed[2]), us(T[4][0] - ed[2])))
+print("HW_ID per wave: %s (SIMD = bits 5:4, CU = bits 11:8)" % " ".join(
+    "w%d:simd%d/cu%d" % (w, (T[9][20 + w] >> 4) & 3, (T[9][20 + w] >> 8) & 15) for w in range(4)))
 print("round   wait  eval+absorb  challenge  slot_ready(vs r_{k-2})")
 for k in range(R):
     lag = us(T[4][k] - T[3][k - 2]) if k >= 2 else 0.0
