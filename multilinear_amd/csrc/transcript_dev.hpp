@@ -351,6 +351,55 @@ __device__ __forceinline__ uint32_t sha_sched(uint32_t* w, int t) {
   return w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
 }
 
+// The working state a..h of each lane pair, on both lanes of the pair (one
+// DPP swap per word), for lane pairs that hash different messages.
+__device__ __forceinline__ void sha2l_state_pair(const Sha2L& q, uint32_t (&v)[8]) {
+  const bool odd = q.m != 0u;
+  const uint32_t o0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r0, 0xB1, 0xF, 0xF, true);
+  const uint32_t o1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r1, 0xB1, 0xF, 0xF, true);
+  const uint32_t o2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r2, 0xB1, 0xF, 0xF, true);
+  const uint32_t o3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r3, 0xB1, 0xF, 0xF, true);
+  v[0] = odd ? q.r0 : o0;
+  v[1] = odd ? q.r1 : o1;
+  v[2] = odd ? q.r2 : o2;
+  v[3] = odd ? q.r3 : o3;
+  v[4] = odd ? o0 : q.r0;
+  v[5] = odd ? o1 : q.r1;
+  v[6] = odd ? o2 : q.r2;
+  v[7] = odd ? o3 : q.r3;
+}
+// sha256_node (SHA-256 of the 64 bytes left || right) on a lane pair: both
+// lanes of the pair pass the same children and get the digest (~20 % less
+// latency than one lane: the latency-bound tree levels, where lanes idle).
+__device__ __forceinline__ Sha256State sha2l_node(const Sha256State& l, const Sha256State& r) {
+  constexpr uint32_t K[64] = MLH_SHA_K;
+  constexpr Pad64KW KW;
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    w[i] = l.h[i];
+    w[8 + i] = r.h[i];
+  }
+  const Sha256State iv = sha256_iv();
+  Sha2L q;
+  sha2l_init(q, iv.h);
+  sha2l_rounds<0, 64>(q, [&](int t) -> uint32_t {
+    if (t >= 16) sha_sched(w, t);
+    return K[t] + w[t & 15];
+  });
+  uint32_t v[8], h1[8];
+  sha2l_state_pair(q, v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h1[i] = iv.h[i] + v[i];
+  sha2l_init(q, h1);
+  sha2l_rounds<0, 64>(q, [&](int t) -> uint32_t { return KW.v[t]; });
+  sha2l_state_pair(q, v);
+  Sha256State o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o.h[i] = h1[i] + v[i];
+  return o;
+}
+
 // next_challenge() after an absorb that ended on a block boundary (chaining
 // value h0..h7, wave-uniform): the padding-only block from its precomputed
 // K + W table, on two lanes; Field128::from of the digest's first 16 bytes.

@@ -1,3 +1,5 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 120 python tools/coop_pipeline.py tools/variants/libPROF.so > gpurun_out/cp.log 2>&1; cat gpurun_out/cp.log
-timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/sc_kt -o run -- python3 tools/sumcheck_ab.py multilinear_amd/libmlhip.so > gpurun_out/sc_kt.log 2>&1; tail -3 gpurun_out/sc_kt.log
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "merkle or fri or commit or pcs" > gpurun_out/mk_test.log 2>&1 || { tail -30 gpurun_out/mk_test.log; exit 1; }
+tail -2 gpurun_out/mk_test.log
+timeout -k 10 300 python tools/prove_ab.py multilinear_amd/libmlhip.so tools/variants/libHEAD.so > gpurun_out/mk_ab.log 2>&1; cat gpurun_out/mk_ab.log
+timeout -k 10 300 python tools/commit_ab.py multilinear_amd/libmlhip.so tools/variants/libHEAD.so > gpurun_out/mk_cab.log 2>&1; tail -8 gpurun_out/mk_cab.log
