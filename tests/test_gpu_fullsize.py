@@ -128,16 +128,17 @@ def test_config3_rs_2_25_and_fri_commit_vs_c_oracle():
 # ---- config 4: 24-variable sumcheck rounds (sumcheck.rs:77-247) ----
 
 @pytest.mark.slow
-@pytest.mark.parametrize("n,label", [(17, b""), (19, b""), (20, b"abc"), (22, b"x" * 33), (24, b"")])
+@pytest.mark.parametrize("n,label", [(17, b""), (19, b""), (20, b"abc"), (21, b""), (22, b"x" * 33), (23, b"abc"), (24, b"")])
 def test_config4_sumcheck_24_vars_vs_c_oracle(n, label):
     """build_tables_for_pcs + compute_sumcheck_polynomials at 24 variables
     (the GPU keeps delta = eq(point) factored) against the reference round loop
     driven by the C oracle's eq table, partial sums and folds and the Python
     transcript: every round polynomial, every challenge, the final transcript.
-    n = 17 runs the head as separate launches (corner sums, 5 rounds, folds);
-    n = 19..24 (7..12 head rounds) the fused cooperative launch, whose second
-    head group has 1 / 2 / 4 / 6 variables; the 3- and 33-byte transcript
-    prefixes send every absorb through the device transcript's byte path."""
+    n = 17..24 has B = n - 12 = 5..12 head rounds: one corner-sum pass, ONE
+    serial launch on the 2^B corner sums (a group of min(B, 6) variables, then
+    B - 6 = 1..6 more for n >= 19) and the fold passes; the 3- and 33-byte
+    transcript prefixes send every absorb through the device transcript's
+    byte path."""
     Cq = _c()
     ev = D.random_limbs(1 << n, 2424)
     pts = _rand(n, 24)
