@@ -1070,6 +1070,30 @@ __device__ __forceinline__ void helper_barrier(CoopSync& S, uint32_t nw, uint32_
   lds_wait_ge(&S.hbar, target, &S.fail);
 }
 
+// The launch's padding-block K + W tables (64 words per round, <= 12 rounds)
+// copied to LDS in the prologue: the challenge after a block-completing absorb
+// reads round k's table as its first operand, and from HBM that read's latency
+// (~0.5 us) sat on the serial chain every other round.
+// The loads are issued with the prologue's other HBM reads, the LDS stores
+// after them (a store of a loaded value waits for the load).
+constexpr uint32_t kPadKwLds = 12 * 64, kPadKwPer = kPadKwLds / kRedThreads;
+struct PadKw {
+  uint32_t v[kPadKwPer];
+};
+__device__ __forceinline__ PadKw pad_kw_load(const uint32_t* __restrict__ kw, uint32_t n) {
+  PadKw p;
+#pragma unroll
+  for (uint32_t u = 0; u < kPadKwPer; ++u) {
+    const uint32_t i = u * kRedThreads + threadIdx.x;
+    p.v[u] = kw && i < n ? kw[i] : 0u;
+  }
+  return p;
+}
+__device__ __forceinline__ void pad_kw_store(const PadKw& p, uint32_t* kwl) {
+#pragma unroll
+  for (uint32_t u = 0; u < kPadKwPer; ++u) kwl[u * kRedThreads + threadIdx.x] = p.v[u];
+}
+
 // Wave 0: rounds 0..R-1 of the launch.  polys: round 0's (c1, c2) slot, rs:
 // round 0's r slot, kw (or nullptr): round 0's padding-block K + W table.
 //
@@ -1130,8 +1154,9 @@ __device__ void transcript_rounds(CoopSync& S, uint32_t R, DevSha& s, uint32_t* 
           st[i] = mid[i];
         }
       }
+      const Sched2L sc = sched2l_init();
       auto kwf = [&](int t) -> uint32_t {
-        if (t >= 16) sha_sched(blk, t);
+        if (t >= 16) sha2l_sched(blk, t, sc);
         return K[t] + blk[t & 15];
       };
       Sha2L q;
@@ -1508,6 +1533,10 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
   __shared__ uint32_t stage[8];
   __shared__ fe slotY[64];
   __shared__ CoopSync S;
+  __shared__ uint32_t kwl[kPadKwLds];
+  const uint32_t tend = J2 ? J + J2 : t1;
+  const uint32_t* kwx = kw ? kwl : nullptr;  // the launch's pad K + W tables, in LDS
+  const PadKw pkw = pad_kw_load(kw ? kw + 64 * t0 : nullptr, 64 * (tend - t0));
   if (threadIdx.x < sizeof(DevSha) / 4)
     reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
   if (threadIdx.x == 0) {
@@ -1527,19 +1556,18 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
     for (uint32_t m = GW / 2; m >= 1; m >>= 1) acc = fe_add(acc, shfl_xor_fe(acc, (int)m));
     if (threadIdx.x % GW == 0) slotY[threadIdx.x / GW] = acc;
   }
+  pad_kw_store(pkw, kwl);
   __syncthreads();
   MLH_COOP_EDGE(1);
-  const uint32_t tend = J2 ? JT : t1;
   if (wave == 0) {
-    if (MLH_REH == 2) transcript_rehearsal(S, s, kw ? kw + 64 * t0 : nullptr, true);
-    transcript_rounds(S, tend - t0, s, stage, polys, rs + t0, kw ? kw + 64 * t0 : nullptr, false, S.mid,
-                      &S.mid_len);
+    if (MLH_REH == 2) transcript_rehearsal(S, s, kwx, true);
+    transcript_rounds(S, tend - t0, s, stage, polys, rs + t0, kwx, false, S.mid, &S.mid_len);
     if (lane == 0) *t = s;
   } else if (wave == 1) {
     coef_rounds(S, t0, tend, prev, cdev, nullptr, claim0, cs0);
   } else if (wave == 3) {
-    if (MLH_REH == 1) transcript_rehearsal(S, s, kw ? kw + 64 * t0 : nullptr, true);
-    if (MLH_REH != 0) transcript_rehearsal(S, s, kw ? kw + 64 * t0 : nullptr, false);
+    if (MLH_REH == 1) transcript_rehearsal(S, s, kwx, true);
+    if (MLH_REH != 0) transcript_rehearsal(S, s, kwx, false);
   } else if (wave == 2) {
     fe X = fe_zero();
     const uint32_t per = G / GW;  // slots per corner
@@ -1583,6 +1611,8 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
   __shared__ DevSha s;
   __shared__ uint32_t stage[8];
   __shared__ CoopSync S;
+  __shared__ uint32_t kwl[kPadKwLds];
+  const uint32_t* kwx = kw ? kwl : nullptr;  // the launch's pad K + W tables, in LDS
   const uint32_t S0 = 1u << a;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // every HBM read of the prologue is issued before the first LDS store (a
@@ -1590,6 +1620,7 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
   // plain copies the table (2^a / 256 <= 16 per thread) and e
   const uint32_t sw = threadIdx.x < sizeof(DevSha) / 4 ? reinterpret_cast<const uint32_t*>(t)[threadIdx.x] : 0u;
   const fe pgv = threadIdx.x < a ? fe_load(pts + threadIdx.x) : fe_zero();
+  const PadKw pkw = pad_kw_load(kw, 64 * a);
   constexpr uint32_t PER = (1u << kTailLogMax) / kRedThreads;
   fe v[PER];
   if (Jin == 0) {
@@ -1605,6 +1636,7 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
     S.mid_len = ~0ull;
   }
   if (threadIdx.x < a) S.pg[threadIdx.x] = pgv;
+  pad_kw_store(pkw, kwl);
   if (Jin == 0) {
     // plain copies: the groups' suffix products (their points' loads too),
     // then the LDS stores
@@ -1658,8 +1690,8 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
   if (lane == 0) g_coop_ts[9][20 + wave] = __builtin_amdgcn_s_getreg(4 | (31 << 11));  // HW_ID: SIMD in bits 5:4
 #endif
   if (wave == 0) {
-    if (MLH_REH == 2) transcript_rehearsal(S, s, kw, true);
-    transcript_rounds(S, a, s, stage, polys, rs, kw, false, S.mid, &S.mid_len);
+    if (MLH_REH == 2) transcript_rehearsal(S, s, kwx, true);
+    transcript_rounds(S, a, s, stage, polys, rs, kwx, false, S.mid, &S.mid_len);
     if (lane == 0) *t = s;
   } else if (wave == 1) {
     coef_rounds(S, 0, a, prev, cdev, d_out, claim0, cs0);
@@ -1671,8 +1703,8 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
     // fold m in place over variables 0, 1, 2 as r_0, r_1, r_2 come out, so
     // that lm[d QA + x] (d: the bits of variables 3, 4, 5) is group B's split
     // table well before the corner wave's round-6 transition needs it.
-    if (MLH_REH == 1) transcript_rehearsal(S, s, kw, true);
-    if (MLH_REH != 0) transcript_rehearsal(S, s, kw, false);
+    if (MLH_REH == 1) transcript_rehearsal(S, s, kwx, true);
+    if (MLH_REH != 0) transcript_rehearsal(S, s, kwx, false);
     MLH_COOP_TS(9, 1);
     if (JB) {
       uint32_t n = 1u << a;

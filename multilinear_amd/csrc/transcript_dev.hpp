@@ -302,6 +302,9 @@ struct Sha2L {
 __device__ __forceinline__ void sha2l_init(Sha2L& q, const uint32_t (&v)[8]) {
   const bool odd = __lane_id() & 1u;
   q.m = odd ? ~0u : 0u;
+  // opaque to the compiler: p = r0 ^ (r2 & m) stays one v_bitop3 (as a select
+  // of constants it lowers to v_cndmask + v_xor)
+  asm("" : "+v"(q.m));
   q.r0 = odd ? v[0] : v[4];
   q.r1 = odd ? v[1] : v[5];
   q.r2 = odd ? v[2] : v[6];
@@ -351,6 +354,34 @@ __device__ __forceinline__ uint32_t sha_sched(uint32_t* w, int t) {
   return w[t & 15] = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
 }
 
+// Message-schedule word t (t >= 16) in place in w[16] on a lane pair whose two
+// lanes hold the same w: the even lane computes sigma0(w[t-15]) and the odd
+// lane sigma1(w[t-2]) in one instruction stream (per-lane v_alignbit and
+// v_lshrrev counts) and one quad_perm DPP add sums them: 7 VALU per word
+// instead of the one-lane 10.
+struct Sched2L {
+  uint32_t m;           // odd lane ~0, even lane 0
+  uint32_t c1, c2, c3;  // even: 7, 18, 3 (sigma0); odd: 17, 19, 10 (sigma1)
+};
+__device__ __forceinline__ Sched2L sched2l_init() {
+  const bool odd = __lane_id() & 1u;
+  Sched2L c;
+  c.m = odd ? ~0u : 0u;
+  asm("" : "+v"(c.m));
+  c.c1 = odd ? 17u : 7u;
+  c.c2 = odd ? 19u : 18u;
+  c.c3 = odd ? 10u : 3u;
+  return c;
+}
+__device__ __forceinline__ uint32_t sha2l_sched(uint32_t* w, int t, const Sched2L& c) {
+  const uint32_t x = (w[(t - 2) & 15] & c.m) | (w[(t - 15) & 15] & ~c.m);
+  const uint32_t sg = xor3(__builtin_amdgcn_alignbit(x, x, c.c1), __builtin_amdgcn_alignbit(x, x, c.c2),
+                           x >> c.c3);
+  uint32_t both = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sg, 0xB1, 0xF, 0xF, true) + sg;
+  asm("" : "+v"(both));  // one v_add_u32_dpp (else: v_mov_dpp + a reassociated add)
+  return w[t & 15] = both + w[(t - 7) & 15] + w[t & 15];
+}
+
 // The working state a..h of each lane pair, on both lanes of the pair (one
 // DPP swap per word), for lane pairs that hash different messages.
 __device__ __forceinline__ void sha2l_state_pair(const Sha2L& q, uint32_t (&v)[8]) {
@@ -383,8 +414,9 @@ __device__ __forceinline__ Sha256State sha2l_node(const Sha256State& l, const Sh
   const Sha256State iv = sha256_iv();
   Sha2L q;
   sha2l_init(q, iv.h);
+  const Sched2L sc = sched2l_init();
   sha2l_rounds<0, 64>(q, [&](int t) -> uint32_t {
-    if (t >= 16) sha_sched(w, t);
+    if (t >= 16) sha2l_sched(w, t, sc);
     return K[t] + w[t & 15];
   });
   uint32_t v[8], h1[8];

@@ -1,4 +1,5 @@
-// Dev check: two-lane SHA-256 rounds (transcript_dev.hpp sha2l_*) against the
+// Dev check: two-lane SHA-256 rounds and message schedule (transcript_dev.hpp
+// sha2l_*, sha2l_sched) against the
 // one-lane sha256_rounds_from / sha256_compress_kw on random states and blocks:
 // a full compression, the 0..8 + 8..64 split with the mid-state, and a
 // padding-only block from a precomputed K + W table.  One wave per test case.
@@ -36,8 +37,9 @@ __global__ void chk(const uint32_t* states, const uint32_t* blocks, const uint32
   // two lanes: 0..8, mid, 8..64
   Sha2L q;
   sha2l_init(q, v0);
+  const Sched2L sc = sched2l_init();
   auto kwf = [&](int t) -> uint32_t {
-    if (t >= 16) sha_sched(w, t);
+    if (t >= 16) sha2l_sched(w, t, sc);
     return K[t] + w[t & 15];
   };
   sha2l_rounds<0, 8>(q, kwf);
