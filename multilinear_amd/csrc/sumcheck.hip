@@ -28,6 +28,28 @@
 namespace mlh {
 
 constexpr int kRedThreads = 256;
+// The 2^24-table sweeps of the eq-factored prove (corner_sums_lo_kernel and
+// the 6-level fold_group_eq_kernel) read through a raw buffer load with the
+// nontemporal policy (`nt`): the sweep then does not flush the L2 of the code
+// and tables of the one-workgroup eq-tail launches between sweeps, which
+// otherwise start cold (their instruction fetches from HBM).  Measured per
+// prove: eq-tail launches 76 -> 67 us each, the 6-level fold +2 us, the corner
+// sums +5 us (a plain global load with the same hint: fold +8 us; the sc0 /
+// sc1 policies: no effect on the eq tail).  base: uniform; idx < 2^28.
+#ifndef MLH_SWEEP_AUX
+#define MLH_SWEEP_AUX 2  // cache-policy word of the buffer load (gfx950: sc0 1, nt 2, sc1 16); < 0: plain load
+#endif
+__device__ __forceinline__ fe sweep_load(const fe* base, uint32_t idx) {
+#if MLH_SWEEP_AUX < 0
+  return fe_load(base + idx);
+#else
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<fe*>(base), 0, (int)0xFFFFFFFFu, 0x00020000);
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, idx * 16u, 0, MLH_SWEEP_AUX);
+  return fe{{v.x, v.y, v.z, v.w}};
+#endif
+}
 constexpr uint32_t kTailLogMax = 12;  // sumcheck_tail_kernel: 2 x 2^12 x 16 B = 128 KiB LDS
 
 // Phase timestamps of sumcheck_tail_kernel (tools/tail_bench.hip builds this
@@ -447,41 +469,52 @@ fold_group_eq_kernel(const fe* Tin, uint64_t S, uint32_t JN, const fe* __restric
   fe acc = fe_zero();
   const uint64_t stride = ((uint64_t)nbc * blockDim.x) >> J2;
   const uint64_t i0 = ((uint64_t)bb * blockDim.x + threadIdx.x) >> J2;
-  for (uint64_t i = i0; i < Qp; i += stride) {
-    const uint64_t x = (uint64_t)co * Qp + i;
-    fe v;
-    if constexpr (SPLIT) {
-      v = fold_corners<JH>(Tin + (uint64_t)l * Sp + x, Sp << J2, r);
+  // BUF: the !SPLIT loads through sweep_load (32-bit byte offsets: S <= 2^28)
+  auto run = [&](auto BUF_) {
+    constexpr bool BUF = decltype(BUF_)::value;
+    for (uint64_t i = i0; i < Qp; i += stride) {
+      const uint64_t x = (uint64_t)co * Qp + i;
+      fe v;
+      if constexpr (SPLIT) {
+        v = fold_corners<JH>(Tin + (uint64_t)l * Sp + x, Sp << J2, r);
 #pragma unroll
-      for (int u = 0; u < J2; ++u) {
-        const uint32_t m = 1u << (J2 - 1 - u);
-        const fe o = shfl_xor_fe(v, m);
-        const bool hi = l & m;
-        v = lerp_s(hi ? o : v, hi ? v : o, r[JH + u]);
+        for (int u = 0; u < J2; ++u) {
+          const uint32_t m = 1u << (J2 - 1 - u);
+          const fe o = shfl_xor_fe(v, m);
+          const bool hi = l & m;
+          v = lerp_s(hi ? o : v, hi ? v : o, r[JH + u]);
+        }
+      } else {
+        acc9 t;  // (the column accumulator measured slower here: 24 registers per output)
+        acc_zero(t);
+#pragma unroll
+        for (int c0 = 0; c0 < (1 << J); c0 += 8) {  // 8 loads in flight at a time
+          fe tv[8];
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            if (c0 + c < (1 << J)) {
+              const uint64_t ix = (uint64_t)(c0 + c) * Sp + x;
+              tv[c] = BUF ? sweep_load(Tin, (uint32_t)ix) : fe_load(Tin + ix);
+            }
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            if (c0 + c < (1 << J)) mulacc(t, tv[c], wsh[c0 + c]);
+        }
+        v = acc_reduce(t);
       }
-    } else {
-      acc9 t;  // (the column accumulator measured slower here: 24 registers per output)
-      acc_zero(t);
-#pragma unroll
-      for (int c0 = 0; c0 < (1 << J); c0 += 8) {  // 8 loads in flight at a time
-        fe tv[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-          if (c0 + c < (1 << J)) tv[c] = fe_load(Tin + (uint64_t)(c0 + c) * Sp + x);
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-          if (c0 + c < (1 << J)) mulacc(t, tv[c], wsh[c0 + c]);
+      if (l == 0) {
+        fe_store(Tout + x, v);
+        // e(i) = H[i >> a] lo[i mod 2^a] in full: one output per 2^J inputs
+        if (JN)
+          acc = fe_add(acc, fe_mul_s(v, fe_mul_s(fe_load(H + (i >> a)),
+                                                 fe_load(lo + (i & ((1ull << a) - 1))))));
       }
-      v = acc_reduce(t);
     }
-    if (l == 0) {
-      fe_store(Tout + x, v);
-      // e(i) = H[i >> a] lo[i mod 2^a] in full: one output per 2^J inputs
-      if (JN)
-        acc = fe_add(acc, fe_mul_s(v, fe_mul_s(fe_load(H + (i >> a)),
-                                               fe_load(lo + (i & ((1ull << a) - 1))))));
-    }
-  }
+  };
+  if (!SPLIT && S <= (1ull << 28))
+    run(std::true_type{});
+  else
+    run(std::false_type{});
   if (JN) {
     fe z = fe_zero();
     block_reduce2(acc, z);
@@ -1878,14 +1911,14 @@ corner_sums_lo_kernel(const fe* __restrict__ T, uint32_t a, const fe* __restrict
   fe acc[CPB];
 #pragma unroll
   for (int q = 0; q < CPB; ++q) {
-    const fe* Tc = T + (uint64_t)(c0 + q) * Q + threadIdx.x;
+    const fe* Tc = T + (uint64_t)(c0 + q) * Q;
     sacc s0;
     sacc_zero(s0);
 #pragma unroll
     for (int k0 = 0; k0 < PER; k0 += 8) {
       fe v[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = fe_load(Tc + (k0 + k) * kRedThreads);
+      for (int k = 0; k < 8; ++k) v[k] = sweep_load(Tc, threadIdx.x + (k0 + k) * kRedThreads);
 #pragma unroll
       for (int k = 0; k < 8; ++k) sacc_mac(s0, v[k], lv[k0 + k]);
     }

@@ -13,6 +13,7 @@
 #endif
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -113,7 +114,13 @@ int main() {
     CHECK(hipMemcpy(kw, hkw.data(), hkw.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(partials, hp.data(), hp.size() * sizeof(fe), hipMemcpyHostToDevice));
     CHECK(hipMemcpy(pts, hpts.data(), JT * sizeof(fe), hipMemcpyHostToDevice));
+    // FLUSH=1: stream 1 GiB through the L2s before each launch (as the folds
+    // before the tail launch of a prove do), so the kernel's code comes from HBM
+    const char* fl = getenv("FLUSH");
+    void* junk = nullptr;
+    if (fl && *fl == '1') CHECK(hipMalloc(&junk, 1ull << 30));
     for (int rep = 0; rep < 5; ++rep) {
+      if (junk) CHECK(hipMemsetAsync(junk, rep, 1ull << 30, 0));
       const fe one{{1, 0, 0, 0}}, cl = rand_fe();
       CHECK(hipMemcpy(cdev, &one, sizeof(fe), hipMemcpyHostToDevice));
       CHECK(hipMemcpy(prev, &cl, sizeof(fe), hipMemcpyHostToDevice));
@@ -167,7 +174,13 @@ int main() {
     CHECK(hipMemcpy(m, hm.data(), S0 * sizeof(fe), hipMemcpyHostToDevice));
     CHECK(hipMemcpy(e, he.data(), (S0 - 1) * sizeof(fe), hipMemcpyHostToDevice));
     CHECK(hipMemcpy(pts, hpts.data(), a * sizeof(fe), hipMemcpyHostToDevice));
+    // FLUSH=1: stream 1 GiB through the L2s before each launch (as the folds
+    // before the tail launch of a prove do), so the kernel's code comes from HBM
+    const char* fl = getenv("FLUSH");
+    void* junk = nullptr;
+    if (fl && *fl == '1') CHECK(hipMalloc(&junk, 1ull << 30));
     for (int rep = 0; rep < 5; ++rep) {
+      if (junk) CHECK(hipMemsetAsync(junk, rep, 1ull << 30, 0));
       const fe one{{1, 0, 0, 0}}, cl = rand_fe();
       CHECK(hipMemcpy(cdev, &one, sizeof(fe), hipMemcpyHostToDevice));
       CHECK(hipMemcpy(prev, &cl, sizeof(fe), hipMemcpyHostToDevice));
