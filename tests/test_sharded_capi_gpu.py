@@ -14,8 +14,8 @@
   well (same bytes).
 * RCCL at world 1: an mlh_comm is created from a unique id and its transport
   callbacks (ncclAllToAll / ncclAllGather) move device buffers.
-The schedules are those of multilinear_amd/dist.py, whose Python version the
-CPU tests (tests/test_dist_cpu.py) check against the oracle over gloo.
+The C++ schedules follow the executable CPU spec tests/dist_spec.py, which
+tests/test_dist_cpu.py checks against the oracle over gloo.
 """
 import ctypes
 import os
