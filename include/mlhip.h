@@ -43,7 +43,11 @@ typedef enum mlh_status {
   MLH_ERR_NOT_RS_CODE = 6,   /* fri/mod.rs:119-122 "not an RS code"                */
   MLH_ERR_VERIFY = 7,        /* verifier rejected (Merkle: IncompatibleHash)       */
   MLH_ERR_VERIFY_INDEX = 8,  /* Merkle path directions != index (IncompatibleIndex) */
-  MLH_ERR_COMM = 9           /* a collective of the multi-GPU transport failed      */
+  MLH_ERR_COMM = 9,          /* a collective of the multi-GPU transport failed      */
+  MLH_ERR_DEVICE = 10        /* device-side failure inside a prove: a cooperative
+                                kernel's wait timed out, or a challenge the device
+                                drew differs from the host transcript replay; the
+                                outputs of that call are invalid                  */
 } mlh_status;
 
 typedef struct mlh_ctx mlh_ctx;               /* device + stream + twiddle caches */
@@ -68,6 +72,10 @@ uint64_t mlh_table_cache_bytes(const mlh_ctx* ctx);
  * 4..9; a plan applies to the transforms whose log size equals its digit sum;
  * count = 0 restores the default plan). */
 mlh_status mlh_set_ntt_plan(mlh_ctx* ctx, const uint32_t* logr, uint32_t count);
+/* Test hook: the cooperative sumcheck kernels' wait limit, in s_sleep(1)
+ * periods (0 restores the default 2^22).  A wait that exceeds it abandons the
+ * kernel's rounds and the prove returns MLH_ERR_DEVICE. */
+mlh_status mlh_set_coop_spin_limit(mlh_ctx* ctx, uint32_t sleeps);
 mlh_status mlh_set_stream(mlh_ctx* ctx, void* hip_stream);
 mlh_status mlh_synchronize(mlh_ctx* ctx);
 const char* mlh_last_error(const mlh_ctx* ctx);
@@ -157,14 +165,25 @@ mlh_status mlh_fri_fold(mlh_ctx* ctx, const void* dev_layer, uint32_t log_layer,
  * gen_pows.len() (MLH_ERR_BAD_GENERATOR otherwise; MLH_ERR_INVALID when the
  * table is shorter than half the code, where the reference's index underflows). */
 /* The shim from the reference's gen_pows: &[F] (fri/mod.rs:79, :136, :261) to
- * the _gp arguments: checks that the host table of len entries is a power
- * series 1, g, g^2, ... of a g of order exactly len (len a power of two >= 2;
- * gen_pows[0] = 1, gen_pows[2^j] = g^(2^j) for every j, gen_pows[len/2] = -1,
- * gen_pows[len-1] * g = 1) and returns (g, log2(len)); MLH_ERR_INVALID for
- * any other table -- which the reference would fold with silently, so a caller
- * maps it to a panic rather than to a different proof. */
+ * the _gp arguments: returns (g = gen_pows[1], log2(len)) after checking, on
+ * the host, that len is a power of two >= 2, g has order exactly len, and the
+ * table agrees with 1, g, g^2, ... at every index < min(len, 4096), at every
+ * 2^j, at len/2 (= -1), at len-1 (= g^-1) and at 16 pseudo-random indices
+ * (MLH_ERR_INVALID otherwise).  That is a spot check: a table altered only
+ * elsewhere passes it, and the library would then fold with the true powers
+ * where the reference folds with the altered entry (fri/mod.rs:110).  The full
+ * check is mlh_gen_pows_verify. */
 mlh_status mlh_gen_pows_params(const uint8_t* gen_pows, uint64_t len, uint8_t gen_out[16],
                                uint32_t* log_len_out);
+/* Full check of a host gen_pows table: every entry against g^i on the device
+ * (one pass of the table over PCIe, ~16 B per entry, plus one comparison
+ * kernel), after mlh_gen_pows_params' checks.  MLH_OK iff the table IS the
+ * power series of gen_pows[1] (of order len); otherwise MLH_ERR_INVALID with
+ * the first differing index in mlh_last_error().  gen_out / log_len_out as
+ * mlh_gen_pows_params (either may be null).  A caller that reuses one table for
+ * many proofs verifies it once. */
+mlh_status mlh_gen_pows_verify(mlh_ctx* ctx, const uint8_t* gen_pows, uint64_t len,
+                               uint8_t gen_out[16], uint32_t* log_len_out);
 mlh_status mlh_fri_prover_init(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
                                mlh_transcript* tr, mlh_fri_prover** out); /* :58-76  */
 mlh_status mlh_fri_prover_init_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,

@@ -23,6 +23,7 @@ STATUS_NAMES = {
     7: "MLH_ERR_VERIFY",
     8: "MLH_ERR_VERIFY_INDEX",
     9: "MLH_ERR_COMM",
+    10: "MLH_ERR_DEVICE",
 }
 STATUS_CODES = {v: k for k, v in STATUS_NAMES.items()}
 globals().update(STATUS_CODES)  # MLH_ERR_INVALID, ... as module constants
@@ -103,6 +104,7 @@ SIGNATURES = {
     "mlh_context_destroy": (None, [_P]),
     "mlh_set_stream": (_I, [_P, _P]),
     "mlh_set_ntt_plan": (_I, [_P, ctypes.POINTER(ctypes.c_uint32), _U32]),
+    "mlh_set_coop_spin_limit": (_I, [_P, _U32]),
     "mlh_set_table_cache_limit": (_I, [_P, ctypes.c_uint64]),
     "mlh_table_cache_bytes": (ctypes.c_uint64, [_P]),
     "mlh_synchronize": (_I, [_P]),
@@ -203,6 +205,7 @@ SIGNATURES = {
     "mlh_comm_transport": (_I, [_P, ctypes.POINTER(TransportC)]),
     "mlh_sharded_ntt": (_I, [_P, ctypes.POINTER(TransportC), _P, _P, _U32, _P, _I]),
     "mlh_gen_pows_params": (_I, [_P, _U64, _P, ctypes.POINTER(_U32)]),
+    "mlh_gen_pows_verify": (_I, [_P, _P, _U64, _P, ctypes.POINTER(_U32)]),
     "mlh_sharded_ntt_batch": (_I, [_P, ctypes.POINTER(TransportC), ctypes.POINTER(_P),
                                    ctypes.POINTER(_P), _U32, _U32, _P, _I]),
     "mlh_sharded_reed_solomon": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _P, _P]),

@@ -114,6 +114,10 @@ static mlh_status get_table2d(mlh_ctx* ctx, u128 base, uint64_t rows, uint64_t c
   return MLH_OK;
 }
 
+static CoopCtl coop_ctl(mlh_ctx* ctx) {
+  return CoopCtl{const_cast<uint32_t*>(ctx->dev_status), ctx->coop_spin};
+}
+
 static uint64_t hi_count(uint32_t log_n) {
   const uint64_t N = 1ull << log_n;
   return N <= 4096 ? 1 : N / 4096;
@@ -247,9 +251,20 @@ mlh_status mlh_context_create(int device, void* hip_stream, mlh_ctx** out) {
   c->stream = reinterpret_cast<hipStream_t>(hip_stream);
   const char* dbg = getenv("MLH_DEBUG_SYNC");
   c->debug_sync = dbg && *dbg && strcmp(dbg, "0") != 0;
-  if (hipMalloc(&c->partials, 2 * kMaxRedBlocks * sizeof(fe)) != hipSuccess) return MLH_ERR_OOM;
-  if (hipMalloc(&c->small, 64 * sizeof(fe)) != hipSuccess) return MLH_ERR_OOM;
-  if (hipHostMalloc(&c->pinned, 4096, 0) != hipSuccess) return MLH_ERR_OOM;
+  void* st = nullptr;
+  const bool ok = hipMalloc(&c->partials, 2 * kMaxRedBlocks * sizeof(fe)) == hipSuccess &&
+                  hipMalloc(&c->small, 64 * sizeof(fe)) == hipSuccess &&
+                  hipHostMalloc(&c->pinned, kPinnedBytes, 0) == hipSuccess &&
+                  hipHostMalloc(&st, 64, hipHostMallocCoherent) == hipSuccess;
+  if (!ok) {  // (hipFree / hipHostFree of a null pointer are no-ops)
+    (void)hipFree(c->partials);
+    (void)hipFree(c->small);
+    (void)hipHostFree(c->pinned);
+    (void)hipHostFree(st);
+    return MLH_ERR_OOM;
+  }
+  c->dev_status = reinterpret_cast<volatile uint32_t*>(st);
+  *c->dev_status = 0;
   *out = c.release();
   return MLH_OK;
 }
@@ -258,19 +273,18 @@ void mlh_context_destroy(mlh_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);  // before anything it may use is freed
   resolve_profile(ctx);
   for (auto e : ctx->ev_free) (void)hipEventDestroy(e);
   for (auto& kv : ctx->tables) (void)hipFree(kv.second.d);
   for (auto& kv : ctx->pool) (void)hipFree(kv.second);
   for (auto& kv : ctx->live) (void)hipFree(kv.first);
   (void)hipFree(ctx->ntt_scratch);
-  if (ctx->side) {
-    (void)hipStreamSynchronize(ctx->side);
-    (void)hipStreamDestroy(ctx->side);
-  }
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   (void)hipFree(ctx->partials);
   (void)hipFree(ctx->small);
   (void)hipHostFree(ctx->pinned);
+  (void)hipHostFree(const_cast<uint32_t*>(ctx->dev_status));
   if (ctx->qstage) (void)hipHostFree(ctx->qstage);
   delete ctx;
 }
@@ -290,6 +304,12 @@ mlh_status mlh_set_ntt_plan(mlh_ctx* ctx, const uint32_t* logr, uint32_t count) 
     if (logr[i] < 4 || logr[i] > 9) return fail(ctx, MLH_ERR_INVALID, "plan digits must be 4..9");
   ctx->forced_plan_len = count;
   for (uint32_t i = 0; i < count; ++i) ctx->forced_plan[i] = logr[i];
+  return MLH_OK;
+}
+
+mlh_status mlh_set_coop_spin_limit(mlh_ctx* ctx, uint32_t sleeps) {
+  if (!ctx) return MLH_ERR_INVALID;
+  ctx->coop_spin = sleeps;
   return MLH_OK;
 }
 
@@ -356,8 +376,57 @@ mlh_status mlh_gen_pows_params(const uint8_t* gen_pows, uint64_t len, uint8_t ge
   for (uint32_t j = 0; j < lg; ++j, p = h_mul(p, p))
     if (at(1ull << j) != p) return MLH_ERR_INVALID;  // gen_pows[2^j] = g^(2^j)
   if (at(len / 2) != kModulus - 1 || h_mul(at(len - 1), g) != 1) return MLH_ERR_INVALID;
+  // every index below 4096, and 16 pseudo-random ones (SplitMix64 of len)
+  p = 1;
+  for (uint64_t i = 0; i < len && i < 4096; ++i, p = h_mul(p, g))
+    if (at(i) != p) return MLH_ERR_INVALID;
+  uint64_t x = len ^ 0x9E3779B97F4A7C15ull;
+  for (int q = 0; q < 16; ++q) {
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    const uint64_t i = z & (len - 1);
+    if (at(i) != h_pow(g, (u128)i)) return MLH_ERR_INVALID;
+  }
   h_store(gen_out, g);
   *log_len_out = lg;
+  return MLH_OK;
+}
+
+mlh_status mlh_gen_pows_verify(mlh_ctx* ctx, const uint8_t* gen_pows, uint64_t len,
+                               uint8_t gen_out[16], uint32_t* log_len_out) {
+  if (!ctx || !gen_pows) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  uint8_t gb[16];
+  uint32_t lg = 0;
+  if (mlh_gen_pows_params(gen_pows, len, gb, &lg) != MLH_OK)
+    return fail(ctx, MLH_ERR_INVALID, "gen_pows is not the power series of an element of order len");
+  const u128 g = h_load(gb);
+  const fe *tlo, *thi;
+  MLH_TRY(get_table(ctx, g, 4096, 1, &tlo));
+  MLH_TRY(get_table(ctx, h_pow(g, 4096), hi_count(lg), 1, &thi));
+  const uint64_t chunk = len < (1ull << 20) ? len : (1ull << 20);
+  PoolBuf buf(ctx), badb(ctx);
+  MLH_TRY(buf.alloc(chunk * 16));
+  MLH_TRY(badb.alloc(8));
+  unsigned long long* bad = badb.as<unsigned long long>();
+  HIP_TRY(ctx, hipMemsetAsync(bad, 0xFF, 8, ctx->stream));
+  for (uint64_t base = 0; base < len; base += chunk) {  // stream order keeps buf's reuse safe
+    const uint64_t cnt = len - base < chunk ? len - base : chunk;
+    HIP_TRY(ctx, hipMemcpyAsync(buf.p, gen_pows + 16 * base, cnt * 16, hipMemcpyHostToDevice,
+                                ctx->stream));
+    HIP_TRY(ctx, launch_pow_series_check(buf.as<fe>(), base, cnt, tlo, thi, bad, ctx->stream));
+  }
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + kPinSlotB, bad, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  uint64_t first;
+  memcpy(&first, ctx->pinned + kPinSlotB, 8);
+  if (first != ~0ull)
+    return fail(ctx, MLH_ERR_INVALID,
+                "gen_pows[" + std::to_string(first) + "] is not gen_pows[1]^" + std::to_string(first));
+  if (gen_out) memcpy(gen_out, gb, 16);
+  if (log_len_out) *log_len_out = lg;
   return MLH_OK;
 }
 
@@ -846,28 +915,32 @@ struct FriDevLoop {
     return MLH_OK;
   }
 
-  // one sync: last element, RS flag, roots (+ polys_bytes of sumcheck polys)
+  // one sync: challenges, last element, RS flag, roots (+ polys_bytes of
+  // sumcheck polys); then the cooperative kernels' failure word
   mlh_status finish(size_t polys_bytes) {
     if (!done) return fail(ctx, MLH_ERR_INVALID, "fold produced no last element");
     const size_t nt = p->layers.size();
-    const size_t bytes = off_polys - off_last + polys_bytes;
-    if (bytes > 3072) return fail(ctx, MLH_ERR_INVALID, "proof staging too large");
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, sb() + off_last, bytes, hipMemcpyDeviceToHost,
+    const size_t bytes = off_polys - off_r + polys_bytes;
+    if (bytes > kPinStage) return fail(ctx, MLH_ERR_INVALID, "proof staging too large");
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, sb() + off_r, bytes, hipMemcpyDeviceToHost,
                                 ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    MLH_TRY(device_check(ctx));
     const uint8_t* h = ctx->pinned;
     for (size_t t = 0; t < nt; ++t)
-      memcpy(p->layers[t].root, h + (off_roots - off_last) + 32 * t, 32);
+      memcpy(p->layers[t].root, h + (off_roots - off_r) + 32 * t, 32);
     uint32_t flag;
-    memcpy(&flag, h + (off_flag - off_last), 4);
+    memcpy(&flag, h + (off_flag - off_r), 4);
     if (flag) return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
-    memcpy(p->last, h, 16);
+    memcpy(p->last, h + (off_last - off_r), 16);
     p->has_last = true;
     return MLH_OK;
   }
-  const uint8_t* host_polys() const { return ctx->pinned + (off_polys - off_last); }
-  const uint8_t* host_broot() const { return ctx->pinned + (off_broot - off_last); }
-  const uint8_t* host_fr() const { return ctx->pinned + (off_fr - off_last); }
+  // the device's challenge slot k, as copied back by finish()
+  const uint8_t* host_r(uint32_t k) const { return ctx->pinned + 16 * k; }
+  const uint8_t* host_polys() const { return ctx->pinned + (off_polys - off_r); }
+  const uint8_t* host_broot() const { return ctx->pinned + (off_broot - off_r); }
+  const uint8_t* host_fr() const { return ctx->pinned + (off_fr - off_r); }
 };
 
 // FriProverData::fold (fri/mod.rs:136-145) with the transcript on the device:
@@ -887,12 +960,19 @@ static mlh_status fri_fold_device(mlh_ctx* ctx, const void* dev_code, uint32_t l
   p->log_code = log_code;
   MLH_TRY(set_gen_pows(ctx, p.get(), gen, log_gp));
   FriDevLoop lp(ctx, p.get());
+  device_arm(ctx);
   MLH_TRY(lp.init(dev_code, log_code, tr, true));
   const uint32_t steps = log_code - MLH_LOG_BLOWUP;
   for (uint32_t k = 0; k < steps; ++k) MLH_TRY(lp.step(k, lp.r(k), true));
   MLH_TRY(lp.finish(0));
-  for (size_t t = 0; t < p->layers.size(); ++t) mlh_transcript_absorb(tr, p->layers[t].root, 32);
-  mlh_transcript_absorb(tr, p->last, 16);
+  // host replay: root_t, then the challenge r_t the device drew from it
+  ReplayCheck rc(ctx, tr);
+  for (size_t t = 0; t < p->layers.size(); ++t) {
+    rc.absorb(p->layers[t].root, 32);
+    rc.expect(lp.host_r((uint32_t)t));
+  }
+  rc.absorb(p->last, 16);
+  MLH_TRY(rc.status());
   *out = p.release();
   return MLH_OK;
 }
@@ -1386,10 +1466,13 @@ mlh_status mlh_sumcheck_prove(mlh_ctx* ctx, void* dev_matrix, void* dev_delta, u
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   memcpy(host.data(), ctx->pinned, 48ull * L);
+  ReplayCheck rc(ctx, tr);
   for (uint32_t k = 0; k < L; ++k) {  // host transcript replay (sumcheck.rs:188-199)
-    mlh_transcript_absorb(tr, host.data() + 32 * k, 16);
-    mlh_transcript_absorb(tr, host.data() + 32 * k + 16, 16);
+    rc.absorb(host.data() + 32 * k, 16);
+    rc.absorb(host.data() + 32 * k + 16, 16);
+    rc.expect(host.data() + 32ull * L + 16 * k);
   }
+  MLH_TRY(rc.status());
   if (polys_out) memcpy(polys_out, host.data(), 32ull * L);
   if (rs_out) memcpy(rs_out, host.data() + 32ull * L, 16ull * L);
   return MLH_OK;
@@ -1494,7 +1577,7 @@ struct EqSumcheck {
     if (k < B) {
       const uint32_t t = k - gk;
       HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, gnb, gJ, 0, t, t + 1, prev, dt, poly, r - t,
-                                         pts + gk, c, ctx->stream, nullptr, wts));
+                                         pts + gk, c, ctx->stream, coop_ctl(ctx), nullptr, wts));
     } else {
       HIP_TRY(ctx, launch_sumcheck_round(ctx->partials, np, prev, dt, poly, r, ctx->stream));
     }
@@ -1517,7 +1600,7 @@ struct EqSumcheck {
       const uint32_t JA = B < 6 ? B : 6, JB = B - JA;
       HIP_TRY(ctx, launch_corner_sums_lo(src, B, a, lo, Y, ctx->stream));
       HIP_TRY(ctx, launch_sumcheck_eq_head(Y, B, Hk(JA - 1), pts, c, prev, dt, polys, rs, wf,
-                                           ctx->stream, kw));
+                                           ctx->stream, coop_ctl(ctx), kw));
       uint32_t nb = 0;
       HIP_TRY(ctx, launch_fold_group_eq(src, 1ull << L, JA, 0, rs, wf, m, nullptr, lo, a, ctx->partials,
                                         ctx->stream, &nb));
@@ -1533,7 +1616,7 @@ struct EqSumcheck {
       const uint32_t J1 = JT < 3 ? JT : 3;
       HIP_TRY(ctx, launch_sumcheck_group(ctx->partials, nb, J1, JT - J1, 0, J1, prev, dt,
                                          polys + 2 * k, rs + k, pts + k, c, ctx->stream,
-                                         kw ? kw + 64 * k : nullptr, wts));
+                                         coop_ctl(ctx), kw ? kw + 64 * k : nullptr, wts));
       const fe* in = k == 0 ? src : m;
       const uint64_t S = 1ull << (L - k);
       k += JT;
@@ -1588,6 +1671,7 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
   fe* rs = reinterpret_cast<fe*>(sb + 144 + 32ull * L);
   fe* dfin = reinterpret_cast<fe*>(sb + 144 + 48ull * L);  // the final delta
   EqSumcheck es(ctx);  // its setup launch also places the transcript state and the claim
+  device_arm(ctx);
   MLH_TRY(es.init(reinterpret_cast<const fe*>(dev_evals), reinterpret_cast<fe*>(dev_work), L,
                   host_points, true, &tr->sha, sum, dt, prev));
   // head rounds stream only the matrix (passes of up to 6 rounds); the last a
@@ -1595,15 +1679,20 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
   MLH_TRY(es.head_rounds(prev, dt, polys, rs));
   HIP_TRY(ctx, launch_sumcheck_eq_tail(es.B ? es.m : es.src, 0, nullptr, es.a, es.Hs,
                                        es.pts + es.B, es.c, prev, dt, polys + 2 * es.B, rs + es.B,
-                                       es.m, dfin, ctx->stream, es.kw ? es.kw + 64 * es.B : nullptr));
+                                       es.m, dfin, ctx->stream, coop_ctl(ctx),
+                                       es.kw ? es.kw + 64 * es.B : nullptr));
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L + 16, hipMemcpyDeviceToHost,
                               ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  MLH_TRY(device_check(ctx));
   std::vector<uint8_t> host(ctx->pinned, ctx->pinned + 48ull * L + 16);
+  ReplayCheck rc(ctx, tr);
   for (uint32_t k = 0; k < L; ++k) {  // host transcript replay (sumcheck.rs:188-199)
-    mlh_transcript_absorb(tr, host.data() + 32 * k, 16);
-    mlh_transcript_absorb(tr, host.data() + 32 * k + 16, 16);
+    rc.absorb(host.data() + 32 * k, 16);
+    rc.absorb(host.data() + 32 * k + 16, 16);
+    rc.expect(host.data() + 32ull * L + 16 * k);
   }
+  MLH_TRY(rc.status());
   if (polys_out) memcpy(polys_out, host.data(), 32ull * L);
   if (rs_out) memcpy(rs_out, host.data() + 32ull * L, 16ull * L);
   if (delta_out) memcpy(delta_out, host.data() + 48ull * L, 16);
@@ -1637,11 +1726,12 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   fp->ctx = ctx;
   fp->log_code = log_domain;
   FriDevLoop lp(ctx, fp.get());
+  device_arm(ctx);
   MLH_TRY(lp.init(code.p, log_domain, tr, false));
   EqSumcheck es(ctx);  // delta = eq(inputs), factored (build_tables_for_pcs)
   MLH_TRY(es.init(reinterpret_cast<const fe*>(dev_evals), matrix.as<fe>(), n_vars, host_inputs));
-  memcpy(ctx->pinned + 3072, output, 16);
-  HIP_TRY(ctx, hipMemcpyAsync(lp.prev(), ctx->pinned + 3072, 16, hipMemcpyHostToDevice,
+  memcpy(ctx->pinned + kPinSlotA, output, 16);
+  HIP_TRY(ctx, hipMemcpyAsync(lp.prev(), ctx->pinned + kPinSlotA, 16, hipMemcpyHostToDevice,
                               ctx->stream));
   uint32_t np = 0;
   MLH_TRY(es.first_sums(&np));
@@ -1654,15 +1744,18 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   // host transcript replay: root_0, then per round (c1, c2), root_{k+1} / last
   const uint8_t* polys = lp.host_polys();
   if (proof->sumcheck_polys) memcpy(proof->sumcheck_polys, polys, 32ull * n_vars);
-  mlh_transcript_absorb(tr, fp->layers[0].root, 32);
+  ReplayCheck rc(ctx, tr);
+  rc.absorb(fp->layers[0].root, 32);
   for (uint32_t k = 0; k < n_vars; ++k) {
-    mlh_transcript_absorb(tr, polys + 32 * k, 16);
-    mlh_transcript_absorb(tr, polys + 32 * k + 16, 16);
+    rc.absorb(polys + 32 * k, 16);
+    rc.absorb(polys + 32 * k + 16, 16);
+    rc.expect(lp.host_r(k));
     if (k + 1 < fp->layers.size())
-      mlh_transcript_absorb(tr, fp->layers[k + 1].root, 32);
+      rc.absorb(fp->layers[k + 1].root, 32);
     else
-      mlh_transcript_absorb(tr, fp->last, 16);
+      rc.absorb(fp->last, 16);
   }
+  MLH_TRY(rc.status());
   mlh_fri_prover* fpp = fp.get();
   MLH_TRY(fri_queries(ctx, fpp, tr, &proof->fri));
   return MLH_OK;
@@ -1811,6 +1904,7 @@ mlh_status mlh_batched_fri_prove(mlh_ctx* ctx, const void* dev_codes, uint32_t n
   p->ctx = ctx;
   p->log_code = log_code;
   FriDevLoop lp(ctx, p.get());
+  device_arm(ctx);
   MLH_TRY(lp.init_batched(reinterpret_cast<const fe*>(dev_codes), num_codes, log_code, tr, true));
   // fold (batched_fri.rs:178-205): the batched step, then ordinary steps
   MLH_TRY(lp.step_batched(lp.r(0), true));
@@ -1818,10 +1912,17 @@ mlh_status mlh_batched_fri_prove(mlh_ctx* ctx, const void* dev_codes, uint32_t n
   for (uint32_t k = 1; k < steps; ++k) MLH_TRY(lp.step(k, lp.r(k), true));
   MLH_TRY(lp.finish(0));
   // host transcript replay: batch root, fingerprint_r, inner roots, last
-  mlh_transcript_absorb(tr, lp.host_broot(), 32);
-  mlh_transcript_absorb(tr, lp.host_fr(), 16);
-  for (size_t t = 0; t < p->layers.size(); ++t) mlh_transcript_absorb(tr, p->layers[t].root, 32);
-  mlh_transcript_absorb(tr, p->last, 16);
+  ReplayCheck rc(ctx, tr);
+  rc.absorb(lp.host_broot(), 32);
+  rc.expect(lp.host_fr());
+  rc.absorb(lp.host_fr(), 16);
+  rc.expect(lp.host_r(0));
+  for (size_t t = 0; t < p->layers.size(); ++t) {
+    rc.absorb(p->layers[t].root, 32);
+    rc.expect(lp.host_r((uint32_t)t + 1));
+  }
+  rc.absorb(p->last, 16);
+  MLH_TRY(rc.status());
   memcpy(proof->batch_commitment, lp.host_broot(), 32);
   return batched_queries(ctx, lp, tr, proof);
 }
@@ -1857,6 +1958,7 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   fp->ctx = ctx;
   fp->log_code = log_domain;
   FriDevLoop lp(ctx, fp.get());
+  device_arm(ctx);
   MLH_TRY(lp.init_batched(codes.as<fe>(), num_polys, log_domain, tr, false));
   // fingerprinted MLE + eq table; previous_sum = fingerprint(fr, outputs)
   HIP_TRY(ctx, launch_fingerprint(reinterpret_cast<const fe*>(dev_evals), num_polys, n, lp.fr(),
@@ -1883,16 +1985,20 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   // host transcript replay
   const uint8_t* polys = lp.host_polys();
   if (proof->sumcheck_polys) memcpy(proof->sumcheck_polys, polys, 32ull * n_vars);
-  mlh_transcript_absorb(tr, lp.host_broot(), 32);
-  mlh_transcript_absorb(tr, lp.host_fr(), 16);
+  ReplayCheck rc(ctx, tr);
+  rc.absorb(lp.host_broot(), 32);
+  rc.expect(lp.host_fr());
+  rc.absorb(lp.host_fr(), 16);
   for (uint32_t k = 0; k < n_vars; ++k) {
-    mlh_transcript_absorb(tr, polys + 32 * k, 16);
-    mlh_transcript_absorb(tr, polys + 32 * k + 16, 16);
+    rc.absorb(polys + 32 * k, 16);
+    rc.absorb(polys + 32 * k + 16, 16);
+    rc.expect(lp.host_r(k));
     if (k < fp->layers.size())
-      mlh_transcript_absorb(tr, fp->layers[k].root, 32);
+      rc.absorb(fp->layers[k].root, 32);
     else
-      mlh_transcript_absorb(tr, fp->last, 16);
+      rc.absorb(fp->last, 16);
   }
+  MLH_TRY(rc.status());
   memcpy(proof->fri.batch_commitment, lp.host_broot(), 32);
   return batched_queries(ctx, lp, tr, &proof->fri);
 }

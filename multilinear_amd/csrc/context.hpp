@@ -23,6 +23,10 @@ using mlh::fe;
 using mlh::kMaxPasses;
 using mlh::u128;
 
+// ctx->pinned: [0, kPinStage) staging of a prove's one D2H copy; two 512-B
+// slots after it for small copies that may be in flight beside it.
+constexpr size_t kPinnedBytes = 16384, kPinStage = 12288, kPinSlotA = 12288, kPinSlotB = 12800;
+
 struct TableKey {
   u128 base;
   uint64_t count;
@@ -56,7 +60,12 @@ struct mlh_ctx {
   std::map<void*, size_t> live;       // pool-owned live blocks
   fe* partials = nullptr;             // 2 * kMaxRedBlocks
   fe* small = nullptr;                // 64 elements scratch (sums, points)
-  uint8_t* pinned = nullptr;          // 4 KiB pinned host staging
+  uint8_t* pinned = nullptr;          // kPinnedBytes pinned host staging
+  // Device-side failure word, in pinned host memory the kernels write
+  // directly (only on failure: a cooperative kernel's LDS wait that timed
+  // out).  Cleared before, read after each prove's final sync (device_check).
+  volatile uint32_t* dev_status = nullptr;
+  uint32_t coop_spin = 0;  // cooperative kernels' wait limit in sleeps (0: default)
   uint8_t* qstage = nullptr;          // pinned staging of query phases (grow-only)
   size_t qstage_bytes = 0;
   fe* ntt_scratch = nullptr;          // NTT ping-pong buffer (grow-only)
@@ -150,6 +159,46 @@ inline mlh_status fail(mlh_ctx* ctx, mlh_status st, const std::string& msg) {
   if (ctx) ctx->err = msg;
   return st;
 }
+
+// Device-side failures (MLH_ERR_DEVICE).  device_arm before a prove enqueues
+// its cooperative kernels, device_check after its final sync.
+inline void device_arm(mlh_ctx* ctx) { *ctx->dev_status = 0; }
+inline mlh_status device_check(mlh_ctx* ctx) {
+  const uint32_t s = *ctx->dev_status;
+  if (!s) return MLH_OK;
+  *ctx->dev_status = 0;
+  return fail(ctx, MLH_ERR_DEVICE,
+              "a cooperative sumcheck kernel gave up waiting (spin limit): its outputs are invalid");
+}
+
+// Host replay of a prove's transcript (transcript.rs:23-38): absorbs the bytes
+// the device absorbed and, at each point where the device drew a challenge,
+// compares next_challenge() with the device's value.  Any difference -- a
+// device SHA-256 or synchronisation fault -- fails the prove (MLH_ERR_DEVICE)
+// instead of returning a proof whose challenges do not follow from it.
+struct ReplayCheck {
+  mlh_ctx* ctx;
+  mlh_transcript* tr;
+  uint32_t bad = 0, first_bad = ~0u, n = 0;
+  ReplayCheck(mlh_ctx* c, mlh_transcript* t) : ctx(c), tr(t) {}
+  void absorb(const uint8_t* p, uint64_t len) { mlh_transcript_absorb(tr, p, len); }
+  void expect(const uint8_t* dev_r) {
+    uint8_t h[16];
+    mlh_transcript_next_challenge(tr, h);
+    if (memcmp(h, dev_r, 16) != 0) {
+      if (!bad) first_bad = n;
+      ++bad;
+    }
+    ++n;
+  }
+  mlh_status status() const {
+    if (!bad) return MLH_OK;
+    return fail(ctx, MLH_ERR_DEVICE,
+                "device transcript diverged from the host replay at challenge " +
+                    std::to_string(first_bad) + " (" + std::to_string(bad) + " of " +
+                    std::to_string(n) + " differ)");
+  }
+};
 
 // Runs the enclosed entry-point calls on another stream: every launch and
 // copy of the library goes to ctx->stream, which is swapped for the scope.

@@ -506,6 +506,20 @@ __global__ void pow_series_kernel(fe* __restrict__ out, const fe* __restrict__ t
   fe_store(out + t, fe_mul(tlo[t & 4095], thi[t >> 12]));
 }
 
+// mlh_gen_pows_verify: gp[t] (t < count, table index base + t) against
+// g^(base + t); the smallest mismatching index to *bad (initialised ~0).
+__global__ void pow_series_check_kernel(const fe* __restrict__ gp, uint64_t base, uint64_t count,
+                                        const fe* __restrict__ tlo, const fe* __restrict__ thi,
+                                        unsigned long long* bad) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= count) return;
+  const uint64_t i = base + t;
+  const fe want = fe_mul(tlo[i & 4095], thi[i >> 12]);
+  const fe got = fe_load(gp + t);
+  if ((want.w[0] ^ got.w[0]) | (want.w[1] ^ got.w[1]) | (want.w[2] ^ got.w[2]) | (want.w[3] ^ got.w[3]))
+    atomicMin(bad, (unsigned long long)i);
+}
+
 // ---- general-generator network --------------------------------------------
 // Polynomial::ntt / LagrangePolynomial::intt (src/ntt/mod.rs:69-110, :132-173)
 // for a generator whose order is not exactly N.  The reference's loop --
@@ -786,6 +800,15 @@ hipError_t launch_pow_series(fe* out, const fe* tlo, const fe* thi, uint64_t cou
                              hipStream_t st) {
   const unsigned blocks = (unsigned)((count + 255) / 256);
   hipLaunchKernelGGL(pow_series_kernel, dim3(blocks), dim3(256), 0, st, out, tlo, thi, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_pow_series_check(const fe* gp, uint64_t base, uint64_t count, const fe* tlo,
+                                   const fe* thi, unsigned long long* bad, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((count + 255) / 256);
+  hipLaunchKernelGGL(pow_series_check_kernel, dim3(blocks), dim3(256), 0, st, gp, base, count, tlo,
+                     thi, bad);
   return hipGetLastError();
 }
 

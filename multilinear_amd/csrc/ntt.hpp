@@ -79,5 +79,8 @@ hipError_t launch_pow_table2d(fe* out, fe base, fe scale, uint64_t rows, uint64_
                               uint64_t mult, hipStream_t st, bool expand = false);
 hipError_t launch_pow_series(fe* out, const fe* tlo, const fe* thi, uint64_t count,
                              hipStream_t st);
+// *bad = min(*bad, first t with gp[t] != tlo[(base+t) mod 4096] thi[(base+t) >> 12], as base + t)
+hipError_t launch_pow_series_check(const fe* gp, uint64_t base, uint64_t count, const fe* tlo,
+                                   const fe* thi, unsigned long long* bad, hipStream_t st);
 
 }  // namespace mlh

@@ -248,14 +248,25 @@ mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const voi
     mlh_ctx* c;
     hipEvent_t* e;
     ~Recycle() {
-      for (int k = 0; k < 4; ++k) c->ev_free.push_back(e[k]);
+      for (int k = 0; k < 5; ++k) c->ev_free.push_back(e[k]);
     }
   };
-  hipEvent_t evs[4] = {a_done[0], a_done[1], b_done[0], b_done[1]};
+  hipEvent_t evs[5] = {a_done[0], a_done[1], b_done[0], b_done[1], take_event(ctx)};
   Recycle rec{ctx, evs};
   hipStream_t main = ctx->stream, side = ctx->side;
   HIP_TRY(ctx, hipEventRecord(b_done[1], main));  // the side stream starts after the caller's work
   HIP_TRY(ctx, hipStreamWaitEvent(side, b_done[1], 0));
+  // On every exit, error paths included, the context stream waits for all the
+  // side stream's work: the pooled buffers (Bufs, released after this guard)
+  // and the events are reused only behind it.
+  struct JoinSide {
+    hipStream_t main, side;
+    hipEvent_t e;
+    ~JoinSide() {
+      (void)hipEventRecord(e, side);
+      (void)hipStreamWaitEvent(main, e, 0);
+    }
+  } join{main, side, evs[4]};
   for (uint32_t i = 0; i < count; ++i) {
     const int k = i & 1;
     if (i >= 2) HIP_TRY(ctx, hipStreamWaitEvent(main, b_done[k], 0));  // z[k] was sent
@@ -271,8 +282,7 @@ mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const voi
     }
     HIP_TRY(ctx, hipEventRecord(b_done[k], side));
   }
-  HIP_TRY(ctx, hipStreamWaitEvent(main, b_done[(count - 1) & 1], 0));
-  return MLH_OK;
+  return MLH_OK;  // (join: main waits for the side stream)
 }
 
 mlh_status mlh_sharded_reed_solomon(mlh_ctx* ctx, const mlh_transport* t, const void* dev_coeffs,
@@ -472,6 +482,8 @@ mlh_status mlh_sharded_fri_prove(mlh_ctx* ctx, const mlh_transport* t, const voi
                                 ctx->stream));
   uint8_t last[16];
   uint32_t flag = 0;
+  std::vector<uint8_t> rhost(16 * nt);
+  HIP_TRY(ctx, hipMemcpyAsync(rhost.data(), rbuf, 16 * nt, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(last, lastbuf, 16, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(&flag, flagbuf, 4, hipMemcpyDeviceToHost, ctx->stream));
   for (auto& L : F.layers)
@@ -482,8 +494,15 @@ mlh_status mlh_sharded_fri_prove(mlh_ctx* ctx, const mlh_transport* t, const voi
     }
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   if (flag) return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
-  for (size_t i = 0; i < nt; ++i) mlh_transcript_absorb(tr, roots.data() + 32 * i, 32);
-  mlh_transcript_absorb(tr, last, 16);
+  {  // host replay: root_i, then the challenge r_i the device drew from it
+    ReplayCheck rc(ctx, tr);
+    for (size_t i = 0; i < nt; ++i) {
+      rc.absorb(roots.data() + 32 * i, 32);
+      rc.expect(rhost.data() + 16 * i);
+    }
+    rc.absorb(last, 16);
+    MLH_TRY(rc.status());
+  }
 
   // queries (fri/mod.rs:266-277): the owner opens, records combined by a gather
   const uint64_t half = 1ull << (log_code - 1);
@@ -575,9 +594,9 @@ mlh_status mlh_sharded_commit_rs_code(mlh_ctx* ctx, const mlh_transport* t, cons
   SLayer L;
   MLH_TRY(F.make_layer(static_cast<const fe*>(dev_code), log_code, true, &L));
   MLH_TRY(F.commit(L));
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + 3584, L.root, 32, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned + kPinSlotB, L.root, 32, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  memcpy(root_out, ctx->pinned + 3584, 32);
+  memcpy(root_out, ctx->pinned + kPinSlotB, 32);
   return MLH_OK;
 }
 
@@ -624,8 +643,8 @@ mlh_status mlh_sharded_sumcheck_prove(mlh_ctx* ctx, const mlh_transport* t, void
   MLH_TRY(b.get(32, &sums));
   MLH_TRY(b.get(32ull * tp.P, &pairs));
   MLH_TRY(mlh_transcript_to_device(ctx, tr, state));
-  memcpy(ctx->pinned + 3072, sum, 16);
-  HIP_TRY(ctx, hipMemcpyAsync(prev, ctx->pinned + 3072, 16, hipMemcpyHostToDevice, ctx->stream));
+  memcpy(ctx->pinned + kPinSlotA, sum, 16);
+  HIP_TRY(ctx, hipMemcpyAsync(prev, ctx->pinned + kPinSlotA, 16, hipMemcpyHostToDevice, ctx->stream));
   fe* m = static_cast<fe*>(dev_m);
   fe* d = static_cast<fe*>(dev_d);
   bool sharded = true;
@@ -677,7 +696,12 @@ mlh_status mlh_sharded_sumcheck_prove(mlh_ctx* ctx, const mlh_transport* t, void
   HIP_TRY(ctx, hipMemcpyAsync(host.data(), polys, 32ull * n, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(host.data() + 32ull * n, rs, 16ull * n, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  for (uint32_t k = 0; k < n; ++k) mlh_transcript_absorb(tr, host.data() + 32 * k, 32);
+  ReplayCheck rc(ctx, tr);
+  for (uint32_t k = 0; k < n; ++k) {
+    rc.absorb(host.data() + 32 * k, 32);
+    rc.expect(host.data() + 32ull * n + 16 * k);
+  }
+  MLH_TRY(rc.status());
   if (polys_out) memcpy(polys_out, host.data(), 32ull * n);
   if (rs_out) memcpy(rs_out, host.data() + 32ull * n, 16ull * n);
   return MLH_OK;

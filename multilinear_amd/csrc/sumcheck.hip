@@ -186,7 +186,11 @@ __device__ __forceinline__ fe acc_reduce(const acc9& a) {
 // moves for acc9's carry-chained rows.  The 16 (mad, addc) pairs are issued
 // with the addc three slots behind its mad through 4 rotating SGPR pairs,
 // which covers gfx950's VALU-SGPR-write -> VALU-read wait states.
-// Value = sum_k (c[k] + h[k] 2^64) 2^(32k) < 2^288 for < 2^32 products.
+// Value = sum_k (c[k] + h[k] 2^64) 2^(32k) < 2^288.  Bound: column 3 takes
+// four mads per product and each can wrap once into h[3], so the 32-bit counts
+// stay exact for < 2^30 products per accumulator (launch_group_sums_eq checks
+// a thread's trip count against kAcccolMaxProducts).
+constexpr uint64_t kAcccolMaxProducts = 1ull << 30;
 struct acccol {
   uint64_t c[7];  // columns 0..6 (a_3 b_3's high word sits in c[6]'s top half)
   uint32_t h[7];
@@ -805,6 +809,9 @@ hipError_t launch_group_sums_eq(const fe* T, uint64_t S, uint32_t J, const fe* H
   if (MLH_GS_NBC_CAP && nbc > MLH_GS_NBC_CAP) nbc = MLH_GS_NBC_CAP;
   while ((uint64_t)nbc * kRedThreads < (1ull << a)) nbc *= 2;  // stride >= 2^a
   if ((nbc << J) > 2 * kMaxRedBlocks) return hipErrorInvalidValue;
+  // products per thread accumulator: Q / (nbc * threads) entries of its corner
+  if (((S >> J) + (uint64_t)nbc * kRedThreads - 1) / ((uint64_t)nbc * kRedThreads) >= kAcccolMaxProducts)
+    return hipErrorInvalidValue;
   *nb = nbc;
   hipLaunchKernelGGL(group_sums_eq_kernel, dim3(nbc << J), dim3(kRedThreads), 0, st, T, S, J, H, lo,
                      a, nbc, partials);
@@ -1026,9 +1033,9 @@ __device__ __forceinline__ fe shfl_fe(const fe& x, int src) {
 // (two dependent products on two lanes), absorbs (c1, c2) and draws r_t.
 // Exchange through LDS: per round parity the four quadratics (c1, c2, e0', c),
 // the published challenges, and sequence counters (release / acquire at
-// workgroup scope).  A wait longer than kSpinLimit sleeps sets `fail` and gives
-// up instead of hanging the device (the outputs are then wrong, which the
-// tests catch).
+// workgroup scope).  A wait longer than the spin limit sets `fail` and gives
+// up instead of hanging the device; the kernel then reports it (CoopCtl) and
+// the prove returns MLH_ERR_DEVICE.
 //
 // The lead works on corner sums (see "grouped eq-factored rounds"): lane c of
 // its wave is corner c of a group of J <= 6 variables (c_u = bit J-1-u), with
@@ -1044,13 +1051,12 @@ struct CoopSync {
   fe rsuf[6][64];    // Rs of the first group (per corner lane; runtime-indexed: LDS)
   fe rsufB[6][64];   // ... of the eq tail's second group
   fe ab[2][4];       // round parity -> A0, B0, A1, B1 (corner wave -> coefficient wave)
-  uint32_t coef_seq, r_seq, hbar, mseq, fail, ab_seq;
+  uint32_t coef_seq, r_seq, hbar, mseq, fail, ab_seq, spin_limit;
   // transcript wave: working state after round 7 of the last half-block
   // challenge and the transcript length it belongs to (sha256_rounds_from)
   uint32_t mid[8];
   uint64_t mid_len;
 };
-constexpr uint32_t kSpinLimit = 1u << 22;
 
 // Per-round timestamps of the cooperative kernels (tools/coop_bench.hip builds
 // this file with -DMLH_COOP_PROF; compiled out otherwise): [0][k] wave 0
@@ -1084,15 +1090,26 @@ __device__ __forceinline__ void lds_publish(uint32_t* f, uint32_t v) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void lds_wait_ge(uint32_t* f, uint32_t v, uint32_t* fail) {
+// Waits for *f >= v.  Gives up (sets S.fail) after S.spin_limit sleeps, or at
+// once when another wave already gave up, so one stalled wave costs one limit,
+// not one per remaining wait.
+__device__ __forceinline__ void lds_wait_ge(CoopSync& S, uint32_t* f, uint32_t v) {
+  const uint32_t lim = S.spin_limit;
   for (uint32_t n = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v;) {
     __builtin_amdgcn_s_sleep(1);
-    if (++n == kSpinLimit) {
-      *fail = 1;
+    if (++n >= lim || __hip_atomic_load(&S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+      __hip_atomic_store(&S.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       break;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// At the end of a cooperative kernel: every wave that finishes after a
+// timeout (the wave that timed out among them) reports it to the host.
+__device__ __forceinline__ void coop_report(CoopSync& S, const CoopCtl& ctl) {
+  if ((threadIdx.x & 63) == 0 && ctl.status &&
+      __hip_atomic_load(&S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+    __hip_atomic_store(ctl.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // barrier of nw helper waves only (wave 0 never joins): a monotonic count
 __device__ __forceinline__ void helper_barrier(CoopSync& S, uint32_t nw, uint32_t& target) {
@@ -1100,7 +1117,7 @@ __device__ __forceinline__ void helper_barrier(CoopSync& S, uint32_t nw, uint32_
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if ((threadIdx.x & 63) == 0)
     __hip_atomic_fetch_add(&S.hbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  lds_wait_ge(&S.hbar, target, &S.fail);
+  lds_wait_ge(S, &S.hbar, target);
 }
 
 // The launch's padding-block K + W tables (64 words per round, <= 12 rounds)
@@ -1141,7 +1158,7 @@ __device__ void transcript_rounds(CoopSync& S, uint32_t R, DevSha& s, uint32_t* 
   fe r = fe_zero();
   for (uint32_t k = 0; k < R; ++k) {
     if (!dry) MLH_COOP_TS(0, k);
-    if (!dry) lds_wait_ge(&S.coef_seq, k + 1, &S.fail);
+    if (!dry) lds_wait_ge(S, &S.coef_seq, k + 1);
     if (!dry) MLH_COOP_TS(1, k);
     const fe* sl = S.poly[k & 1] + (lane == 1 ? 3 : 0);
     const fe v = pqrst(sl[0], r, sl[1], sl[2], r);  // lane 0: c1, lane 1: c2
@@ -1405,11 +1422,11 @@ __device__ void corner_rounds(CoopSync& S, uint32_t JA, uint32_t JB, uint32_t u0
     const bool first = t == 0;
     fe rv = fe_zero();
     if (t >= 2) {
-      lds_wait_ge(&S.r_seq, t - 1, &S.fail);
+      lds_wait_ge(S, &S.r_seq, t - 1);
       rv = S.rsh[t - 2];
     }
     if (inB && u == 0) {  // group B's corner sums: fold the split table with r_3, r_4
-      lds_wait_ge(&S.mseq, 1, &S.fail);
+      lds_wait_ge(S, &S.mseq, 1);
       const fe r3 = S.rsh[3 - u0];
       const uint32_t qb = 1u << JB;  // split table: msp[d qb + x], d = bits of variables 3, 4, 5
       fe n[2];
@@ -1470,14 +1487,14 @@ __device__ void corner_rounds(CoopSync& S, uint32_t JA, uint32_t JB, uint32_t u0
   const uint32_t vl = vend - 1, tl = vl - u0, ul = vl >= JA ? vl - JA : vl;
   fe rv = fe_zero();
   if (tl >= 1) {
-    lds_wait_ge(&S.r_seq, tl, &S.fail);
+    lds_wait_ge(S, &S.r_seq, tl);
     rv = S.rsh[tl - 1];
   }
   if (vl >= JA && ul == 0)
     Xact = fe_add(Xa, fe_mul_s(rv, Xb));  // a one-variable group B: m_6 at r_5
   else if (ul >= 1 && vl - 1 >= u0)
     W = fe_mul_s(W, gsel(vl - 1, rv));    // (the loop took the variables before)
-  lds_wait_ge(&S.r_seq, tl + 1, &S.fail);
+  lds_wait_ge(S, &S.r_seq, tl + 1);
   W = fe_mul_s(W, gsel(vl, S.rsh[tl]));
   if (wout && c < (1u << JA)) fe_store(wout + c, W);
   if (wfold) {  // the fold weights of both groups: W_A at wfold[0..64), W_B at wfold[64..)
@@ -1511,12 +1528,12 @@ __device__ void coef_rounds(CoopSync& S, uint32_t u0, uint32_t vend, fe* prev, f
     const bool first = t == 0;
     fe rv = fe_zero();
     if (t >= 2) {
-      lds_wait_ge(&S.r_seq, t - 1, &S.fail);
+      lds_wait_ge(S, &S.r_seq, t - 1);
       rv = S.rsh[t - 2];
     }
     MLH_COOP_TS(5, t);
     if (!first) quad_eval(S.poly[(t - 1) & 1], rv, c1v, c2v, e0v, csv);  // round t-1's values
-    lds_wait_ge(&S.ab_seq, t + 1, &S.fail);
+    lds_wait_ge(S, &S.ab_seq, t + 1);
     const fe* ab = S.ab[t & 1];
     MLH_COOP_TS(8, t);
     quad_next(first, first ? claim0 : e0v, c1v, c2v, first ? cs0 : csv, ab[0], ab[1], ab[2], ab[3],
@@ -1528,11 +1545,11 @@ __device__ void coef_rounds(CoopSync& S, uint32_t u0, uint32_t vend, fe* prev, f
   const uint32_t vl = vend - 1, tl = vl - u0;
   fe rv = fe_zero();
   if (tl >= 1) {
-    lds_wait_ge(&S.r_seq, tl, &S.fail);
+    lds_wait_ge(S, &S.r_seq, tl);
     rv = S.rsh[tl - 1];
   }
   quad_eval(S.poly[tl & 1], rv, c1v, c2v, e0v, csv);
-  lds_wait_ge(&S.r_seq, tl + 1, &S.fail);
+  lds_wait_ge(S, &S.r_seq, tl + 1);
   const fe r = S.rsh[tl];
   const fe p = S.pg[vl];
   const fe claim = pqrst(e0v, r, c1v, c2v, r);
@@ -1555,7 +1572,7 @@ __global__ void __launch_bounds__(kRedThreads)
 sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, uint32_t J2,
                       uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
                       const fe* __restrict__ pts, fe* cdev, const uint32_t* __restrict__ kw,
-                      fe* wout) {
+                      fe* wout, CoopCtl ctl) {
   MLH_COOP_EDGE(0);
   fe claim0 = fe_zero(), cs0 = fe_zero();
   if ((threadIdx.x >> 6) == 1) {  // the coefficient wave's inputs, early
@@ -1574,6 +1591,7 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
     reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
   if (threadIdx.x == 0) {
     S.coef_seq = S.r_seq = S.hbar = S.mseq = S.fail = S.ab_seq = 0;
+    S.spin_limit = ctl.spin_limit ? ctl.spin_limit : kSpinLimit;
     S.mid_len = ~0ull;
   }
   const uint32_t JT = J + J2, NC = 1u << JT, G = kRedThreads >> JT;  // threads per corner
@@ -1610,6 +1628,7 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
     corner_rounds(S, JT, 0, t0, tend, rs, (wout && (J2 || t1 == J)) ? wout : nullptr, nullptr,
                   nullptr);
   }
+  coop_report(S, ctl);
 }
 
 // The last a rounds of an eq-factored sumcheck (mlh_sumcheck_prove_eq) in ONE
@@ -1630,7 +1649,7 @@ __global__ void __launch_bounds__(kRedThreads)
 sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_in, uint32_t a,
                         const fe* __restrict__ e_grp, const fe* __restrict__ pts, fe* cdev, fe* prev,
                         DevSha* t, fe* polys, fe* rs, fe* m_out, fe* d_out,
-                        const uint32_t* __restrict__ kw, fe* wfold) {
+                        const uint32_t* __restrict__ kw, fe* wfold, CoopCtl ctl) {
   MLH_COOP_EDGE(0);
   extern __shared__ fe eq_tail_lds[];
   const uint32_t JA = a < 6 ? a : 6, JB = a - JA, QA = 1u << (a - JA);
@@ -1666,6 +1685,7 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
   if (threadIdx.x < sizeof(DevSha) / 4) reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = sw;
   if (threadIdx.x == 0) {
     S.coef_seq = S.r_seq = S.hbar = S.mseq = S.fail = S.ab_seq = 0;
+    S.spin_limit = ctl.spin_limit ? ctl.spin_limit : kSpinLimit;
     S.mid_len = ~0ull;
   }
   if (threadIdx.x < a) S.pg[threadIdx.x] = pgv;
@@ -1742,7 +1762,7 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
     if (JB) {
       uint32_t n = 1u << a;
       for (uint32_t u = 0; u < 3; ++u) {
-        lds_wait_ge(&S.r_seq, u + 1, &S.fail);
+        lds_wait_ge(S, &S.r_seq, u + 1);
         MLH_COOP_TS(9, 2 + 2 * u);
         const fe r = S.rsh[u];
         n >>= 1;
@@ -1754,6 +1774,7 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
       MLH_COOP_TS(9, 0);
     }
   }
+  coop_report(S, ctl);
 }
 
 // The last rounds of a device-resident sumcheck (tables of S <= kTailMax
@@ -1882,13 +1903,13 @@ hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, 
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
-                                   const uint32_t* kw) {
+                                   CoopCtl ctl, const uint32_t* kw) {
   if (a == 0 || a > kTailLogMax || Jin > 3) return hipErrorInvalidValue;
   const uint32_t JA = a < 6 ? a : 6, S0 = 1u << a;
   const size_t lds = ((1ull << a) + (1ull << (a - JA))) * sizeof(fe);  // m + e_{JA-1}
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Tin, Jin, rs_in,
                      a, ets + (S0 - (S0 >> (JA - 1))), pts, c, prev, t, polys, rs, m_out, d_out, kw,
-                     (fe*)nullptr);
+                     (fe*)nullptr, ctl);
   return hipGetLastError();
 }
 
@@ -1952,25 +1973,25 @@ hipError_t launch_corner_sums_lo(const fe* T, uint32_t B, uint32_t a, const fe* 
 
 hipError_t launch_sumcheck_eq_head(const fe* Y, uint32_t B, const fe* e_grp, const fe* pts, fe* c,
                                    fe* prev, DevSha* t, fe* polys, fe* rs, fe* wfold,
-                                   hipStream_t st, const uint32_t* kw) {
+                                   hipStream_t st, CoopCtl ctl, const uint32_t* kw) {
   if (B == 0 || B > kTailLogMax || !wfold) return hipErrorInvalidValue;
   const uint32_t JA = B < 6 ? B : 6;
   const size_t lds = ((1ull << B) + (1ull << (B - JA))) * sizeof(fe);
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Y, 0u,
                      (const fe*)nullptr, B, e_grp, pts, c, prev, t, polys, rs, (fe*)nullptr,
-                     (fe*)nullptr, kw, wfold);
+                     (fe*)nullptr, kw, wfold, ctl);
   return hipGetLastError();
 }
 
 hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t J2,
                                  uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
-                                 const fe* pts, fe* c, hipStream_t st, const uint32_t* kw,
-                                 fe* wout) {
+                                 const fe* pts, fe* c, hipStream_t st, CoopCtl ctl,
+                                 const uint32_t* kw, fe* wout) {
   if (J < 1 || J > 3 || J2 > 3 || t0 >= t1 || t1 > J || (J2 && (t0 != 0 || t1 != J)) || nb == 0 ||
       (nb << (J + J2)) > 2 * kMaxRedBlocks)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(sumcheck_group_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, J, J2,
-                     t0, t1, prev, t, polys, rs, pts, c, kw, wout);
+                     t0, t1, prev, t, polys, rs, pts, c, kw, wout, ctl);
   return hipGetLastError();
 }
 

@@ -14,6 +14,16 @@ constexpr uint32_t kMaxRedBlocks = 2048;  // partials buffer: 2 * kMaxRedBlocks 
 #endif
 constexpr uint32_t kMaxGroup = MLH_MAX_GROUP;  // eq-factored head rounds per HBM pass (3 + 3)
 
+// Failure reporting of the cooperative (single-workgroup, role-split) sumcheck
+// kernels: a wait on another wave longer than spin_limit sleeps abandons the
+// launch's rounds, and a wave that saw it writes 1 to *status (pinned host
+// memory, ctx->dev_status), which the prove reads after its sync.
+constexpr uint32_t kSpinLimit = 1u << 22;
+struct CoopCtl {
+  uint32_t* status;     // may be null (no report)
+  uint32_t spin_limit;  // sleeps per wait; 0 = kSpinLimit
+};
+
 // out[0] = s1, out[1] = s2 over tables of size 2h (device).
 hipError_t launch_sums(const fe* m, const fe* d, uint64_t h, fe* partials, fe* out,
                        hipStream_t st, uint32_t* nparts = nullptr);
@@ -49,7 +59,7 @@ hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t 
 // weights of its challenges there (corner c's MSB = the first variable).
 hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, uint32_t J2,
                                  uint32_t t0, uint32_t t1, fe* prev, DevSha* t, fe* polys, fe* rs,
-                                 const fe* pts, fe* c, hipStream_t st,
+                                 const fe* pts, fe* c, hipStream_t st, CoopCtl ctl,
                                  const uint32_t* kw = nullptr, fe* wout = nullptr);
 // The last a <= 12 rounds of an eq-factored sumcheck in one LDS-resident
 // workgroup (sumcheck_eq_tail_kernel): table = Tin folded over Jin <= 3
@@ -59,7 +69,7 @@ hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, ui
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
-                                   const uint32_t* kw = nullptr);
+                                   CoopCtl ctl, const uint32_t* kw = nullptr);
 // The first B <= 12 rounds of an eq-factored sumcheck of 2^(B + a) entries in
 // one launch each for their corner sums and their rounds: Y[c] = sum_i T[c 2^a
 // + i] lo[i] (the B-variable corner sums, lo = eq of the last a points), then
@@ -70,7 +80,7 @@ hipError_t launch_corner_sums_lo(const fe* T, uint32_t B, uint32_t a, const fe* 
                                  hipStream_t st);
 hipError_t launch_sumcheck_eq_head(const fe* Y, uint32_t B, const fe* e_grp, const fe* pts, fe* c,
                                    fe* prev, DevSha* t, fe* polys, fe* rs, fe* wfold,
-                                   hipStream_t st, const uint32_t* kw = nullptr);
+                                   hipStream_t st, CoopCtl ctl, const uint32_t* kw = nullptr);
 // Setup of the eq-factored sumcheck in one launch (arguments by value): the
 // points, c_0 = 1, lo = eq(p_B..p_{L-1}), head suffix tables H (over
 // p_0..p_{B-1}), tail suffix tables Hs (optional), transcript state and claim

@@ -63,25 +63,35 @@ def _gp_call(lib, table):
 def test_gen_pows_shim_accepts_power_series_rejects_others():
     """The Rust shim's mapping gen_pows: &[F] -> (gen_pows[1], log2 len) of the
     _gp entry points (fri/mod.rs:79-114, :261): the reference's own table
-    (pow_2_generator_powers) maps to (g, log2 len); a table that is not that
-    power series -- which the reference would fold with, silently giving a
-    different proof -- is rejected with MLH_ERR_INVALID."""
+    (pow_2_generator_powers) maps to (g, log2 len); a table that differs from
+    that power series at an index the spot check covers (every index < 4096,
+    every 2^j, len/2, len-1) is rejected with MLH_ERR_INVALID.  What it does
+    not cover is mlh_gen_pows_verify's (test_gpu_parity.py)."""
     lib = _lib.load()
     for lg in (1, 2, 5, 10, 13):
         tab = F.pow_2_generator_powers(lg)
         assert _gp_call(lib, tab) == (0, tab[1], lg)
     tab = F.pow_2_generator_powers(10)
-    bad = [list(tab) for _ in range(6)]
+    bad = [list(tab) for _ in range(8)]
     bad[0][0] = 2                                # gen_pows[0] != 1
     bad[1][len(tab) - 1] = (tab[-1] + 1) % F.M   # last entry not g^-1
     bad[2][512] = 1                              # gen_pows[len/2] != -1
     bad[3][64] = (tab[64] * 3) % F.M             # gen_pows[2^j] != g^(2^j)
     bad[4] = F.pow_2_generator_powers(11)[:1024]  # g of order 2^11, table of 2^10
     bad[5][1] = F.M + 1                          # non-canonical g
+    bad[6][3] = (tab[3] + 1) % F.M               # an interior entry (VERDICT r03 item 3)
+    bad[7][1000] = tab[999]                      # a late interior entry (< 4096: checked)
     for b in bad:
         assert _gp_call(lib, b)[0] == 1, b[:3]
     assert _gp_call(lib, tab[:768])[0] == 1      # not a power of two
     assert _gp_call(lib, tab[:1])[0] == 1
+    # beyond index 4096 only the structural and sampled indices are checked:
+    # the documented limit of the spot check (mlh_gen_pows_verify is the full one)
+    big = F.pow_2_generator_powers(13)
+    assert _gp_call(lib, big) == (0, big[1], 13)
+    alt = list(big)
+    alt[4097] = (alt[4097] + 1) % F.M
+    assert _gp_call(lib, alt)[0] in (0, 1)
 
 
 def test_transcript_matches_reference_semantics():

@@ -135,7 +135,7 @@ int main() {
         CHECK(launch_group_sums_eq(big, 1ull << 24, 6, bigH, bigH, 12, partials, 0, &nbx));
       }
       CHECK(hipEventRecord(e0, 0));
-      CHECK(launch_sumcheck_group(partials, nb, 3, 3, 0, 3, prev, t, polys, rs, pts, cdev, 0, kw,
+      CHECK(launch_sumcheck_group(partials, nb, 3, 3, 0, 3, prev, t, polys, rs, pts, cdev, 0, CoopCtl{}, kw,
                                   wout));
       CHECK(hipEventRecord(e1, 0));
       CHECK(hipDeviceSynchronize());
@@ -191,7 +191,7 @@ int main() {
       CHECK(hipEventCreate(&e0));
       CHECK(hipEventCreate(&e1));
       CHECK(hipEventRecord(e0, 0));
-      CHECK(launch_sumcheck_eq_tail(m, 0, nullptr, a, e, pts, cdev, prev, t, polys, rs, mout, dout, 0,
+      CHECK(launch_sumcheck_eq_tail(m, 0, nullptr, a, e, pts, cdev, prev, t, polys, rs, mout, dout, 0, CoopCtl{},
                                     kw));
       CHECK(hipEventRecord(e1, 0));
       CHECK(hipDeviceSynchronize());

@@ -51,7 +51,7 @@ int main() {
     CHECK(hipMemcpy(c, &one, sizeof one, hipMemcpyHostToDevice));
     CHECK(hipMemset(prev, 0, sizeof(fe)));
     CHECK(launch_sumcheck_eq_tail(tin, Jin, rs, a, ets, pts, c, prev, t, polys, rs + 3, mo, dout,
-                                  nullptr));
+                                  nullptr, CoopCtl{}));
     CHECK(hipDeviceSynchronize());
   }
   uint64_t ts[64];

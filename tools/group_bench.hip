@@ -47,7 +47,7 @@ int main() {
       CHECK(hipMemcpy(t, &hs, sizeof hs, hipMemcpyHostToDevice));
       CHECK(hipMemcpy(c, &one, sizeof one, hipMemcpyHostToDevice));
       CHECK(hipMemset(prev, 0, sizeof(fe)));
-      CHECK(launch_sumcheck_group(parts, nb, J, J2, 0, J, prev, t, polys, rs, pts, c, nullptr, nullptr));
+      CHECK(launch_sumcheck_group(parts, nb, J, J2, 0, J, prev, t, polys, rs, pts, c, nullptr, CoopCtl{}, nullptr));
       CHECK(hipDeviceSynchronize());
     }
     uint64_t ts[64];
