@@ -492,6 +492,10 @@ mlh_status mlh_comm_create(mlh_ctx* ctx, uint32_t world, uint32_t rank, const ui
                            mlh_comm** out);
 void mlh_comm_destroy(mlh_comm* comm);
 mlh_status mlh_comm_transport(mlh_comm* comm, mlh_transport* out);
+/* What RCCL itself reports for the communicator (ncclCommCount,
+ * ncclCommUserRank, ncclCommCuDevice): the ranks it connected, this rank, and
+ * its device -- the self-check a multi-GPU run prints. */
+mlh_status mlh_comm_info(mlh_comm* comm, uint32_t* count, uint32_t* rank, int* device);
 /* Polynomial::ntt / LagrangePolynomial::intt (ntt/mod.rs:69-173) of a 2^log_n
  * vector: forward takes the cyclic layout (2^log_n / P local elements) and
  * returns block 2^log_n / P^2; inverse != 0 the reverse.  One all-to-all. */

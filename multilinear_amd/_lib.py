@@ -203,6 +203,7 @@ SIGNATURES = {
     "mlh_comm_create": (_I, [_P, _U32, _U32, _P, ctypes.POINTER(_P)]),
     "mlh_comm_destroy": (None, [_P]),
     "mlh_comm_transport": (_I, [_P, ctypes.POINTER(TransportC)]),
+    "mlh_comm_info": (_I, [_P, ctypes.POINTER(_U32), ctypes.POINTER(_U32), ctypes.POINTER(ctypes.c_int)]),
     "mlh_sharded_ntt": (_I, [_P, ctypes.POINTER(TransportC), _P, _P, _U32, _P, _I]),
     "mlh_gen_pows_params": (_I, [_P, _U64, _P, ctypes.POINTER(_U32)]),
     "mlh_gen_pows_verify": (_I, [_P, _P, _U64, _P, ctypes.POINTER(_U32)]),

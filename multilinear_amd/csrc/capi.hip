@@ -861,9 +861,17 @@ struct FriDevLoop {
     return MLH_OK;
   }
 
+  // poly0 (optional): 32 bytes absorbed after root 0, before its challenge;
+  // n_extra: 16-byte slots at extra()
   mlh_status init(const void* dev_code, uint32_t log_code, const mlh_transcript* tr,
-                  bool challenge_after_root0) {
-    MLH_TRY(layout(log_code, tr));
+                  bool challenge_after_root0, const fe* poly0 = nullptr, size_t n_extra = 0) {
+    MLH_TRY(layout(log_code, tr, n_extra));
+    return init_after_layout(dev_code, log_code, challenge_after_root0, poly0);
+  }
+  // init's commit of layer 0, after layout() (whose extra() slots the caller
+  // may fill first)
+  mlh_status init_after_layout(const void* dev_code, uint32_t log_code, bool challenge_after_root0,
+                               const fe* poly0) {
     FriLayer l0;
     l0.values = reinterpret_cast<const fe*>(dev_code);
     l0.log_n = log_code;
@@ -874,13 +882,14 @@ struct FriDevLoop {
     p->layers.push_back(l0);
     HIP_TRY(ctx, launch_commit_pairs(
                      l0.values, L, l0.tree, ctx->stream,
-                     RootAbsorb{dt(), challenge_after_root0 ? r(0) : nullptr, root(0)}));
+                     RootAbsorb{dt(), challenge_after_root0 ? r(0) : nullptr, root(0), poly0}));
     return MLH_OK;
   }
 
   // fold_step k with the challenge at rp (device); absorbs the new root (or
-  // the last element); writes next_challenge() to r(k + 1) if challenge_next.
-  mlh_status step(uint32_t k, const fe* rp, bool challenge_next) {
+  // the last element) and (poly_next) 32 more bytes; writes next_challenge()
+  // to r(k + 1) if challenge_next.
+  mlh_status step(uint32_t k, const fe* rp, bool challenge_next, const fe* poly_next = nullptr) {
     if (done) return MLH_OK;
     const FriLayer cur = p->layers.back();
     const uint32_t log_n = cur.log_n;
@@ -911,7 +920,7 @@ struct FriDevLoop {
     HIP_TRY(ctx, launch_fri_fold_commit(
                      cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), nx.tree, fe{}, tlo,
                      thi, k, 1ull << p->log_gp, ctx->stream, ShardMap(), rp,
-                     RootAbsorb{dt(), challenge_next ? r(k + 1) : nullptr, root(t)}));
+                     RootAbsorb{dt(), challenge_next ? r(k + 1) : nullptr, root(t), poly_next}));
     return MLH_OK;
   }
 
@@ -1699,6 +1708,82 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
   return MLH_OK;
 }
 
+// PCSProverData::fold (multilinear_pcs.rs:43-76) for n_vars <= 24, with the
+// sumcheck off the transcript chain (sumcheck.hip "PCS rounds off the
+// transcript kernel"): round k's (c1, c2) come from a one-workgroup kernel on
+// the eq-factored table once r_{k-1} exists, and the launch that writes FRI
+// root k absorbs root k, then (c1, c2)_k, and draws r_k -- the transcript
+// order of the reference (root_k | c1_k | c2_k -> r_k), one kernel per round
+// less.  Head (the first B = n - 12 variables): the 2^B corner sums of the
+// 2^n table in one pass; after r_{B-1} two fold_group_eq passes fold the
+// table to the 2^12 entries the tail rounds use.
+static mlh_status pcs_rounds_fused(mlh_ctx* ctx, FriDevLoop& lp, const fe* evals, fe* work,
+                                   uint32_t n, const uint8_t* host_inputs, const uint8_t output[16],
+                                   const void* code, uint32_t log_domain, mlh_transcript* tr) {
+  EqSumcheck es(ctx);  // points, c, lo, head suffix tables H, tail suffix tables Hs
+  MLH_TRY(es.init(evals, work, n, host_inputs, /*want_tail=*/true));
+  const uint32_t B = es.B, a = es.a;
+  PoolBuf yb(ctx);
+  fe* Y = nullptr;  // head table: the 2^B corner sums, folded in place
+  fe* wf = nullptr;
+  if (B) {
+    MLH_TRY(yb.alloc(16 * ((1ull << B) + 128)));
+    Y = yb.as<fe>();
+    wf = Y + (1ull << B);
+  }
+  // e of round k: H_k (head) or Hs_{k-B} (tail); 2^(h-1) entries for a table of 2^h
+  auto e_of = [&](uint32_t k) -> const fe* {
+    return k < B ? es.Hk(k) : es.Hs + ((1ull << a) - (1ull << (a - (k - B))));
+  };
+  // round state (claim, c, e0, c1, c2) in the loop's scratch: claim = output, c = 1
+  struct {
+    uint8_t b[80];
+  } init_state{};
+  memcpy(init_state.b, output, 16);
+  init_state.b[16] = 1;
+  memcpy(ctx->pinned + kPinSlotA, init_state.b, 80);
+  MLH_TRY(lp.layout(log_domain, tr, 5));
+  PcsRoundState* st = reinterpret_cast<PcsRoundState*>(lp.extra());
+  HIP_TRY(ctx, hipMemcpyAsync(st, ctx->pinned + kPinSlotA, 80, hipMemcpyHostToDevice, ctx->stream));
+  // round 0's polynomial, then FRI init: root 0 | (c1, c2)_0 -> r_0
+  if (B) {
+    HIP_TRY(ctx, launch_corner_sums_lo(evals, B, a, es.lo, Y, ctx->stream));
+    HIP_TRY(ctx, launch_pcs_round(Y, Y, B, false, nullptr, nullptr, es.pts, e_of(0), st, lp.poly(0),
+                                  ctx->stream));
+  } else {
+    HIP_TRY(ctx, launch_pcs_round(evals, work, n, false, nullptr, nullptr, es.pts, e_of(0), st,
+                                  lp.poly(0), ctx->stream));
+  }
+  MLH_TRY(lp.init_after_layout(code, log_domain, true, lp.poly(0)));
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t kn = k + 1;  // the round whose polynomial follows r_k
+    if (kn < n) {
+      const fe* pp = es.pts + k;
+      if (kn < B) {  // head: fold Y with r_k
+        HIP_TRY(ctx, launch_pcs_round(Y, Y, B - kn, true, lp.r(k), pp, es.pts + kn, e_of(kn), st,
+                                      lp.poly(kn), ctx->stream));
+      } else if (kn == B) {  // fold the table over the B head variables, then round B on it
+        const uint32_t JA = B < 6 ? B : 6, JB = B - JA;
+        uint32_t nb = 0;
+        HIP_TRY(ctx, launch_eq_weights(lp.r(0), JA, JB, wf, ctx->stream));
+        HIP_TRY(ctx, launch_fold_group_eq(evals, 1ull << n, JA, 0, lp.r(0), wf, work, nullptr, es.lo, a,
+                                          ctx->partials, ctx->stream, &nb));
+        if (JB)
+          HIP_TRY(ctx, launch_fold_group_eq(work, 1ull << (n - JA), JB, 0, lp.r(JA), wf + 64, work,
+                                            nullptr, es.lo, a, ctx->partials, ctx->stream, &nb));
+        HIP_TRY(ctx, launch_pcs_round(work, work, a, false, lp.r(k), pp, es.pts + kn, e_of(kn), st,
+                                      lp.poly(kn), ctx->stream));
+      } else {  // tail: fold with r_k (the first tail fold of B = 0 reads the evaluations)
+        const fe* src = (B == 0 && kn == 1) ? evals : work;
+        HIP_TRY(ctx, launch_pcs_round(src, work, n - kn, true, lp.r(k), pp, es.pts + kn, e_of(kn), st,
+                                      lp.poly(kn), ctx->stream));
+      }
+    }
+    MLH_TRY(lp.step(k, lp.r(k), kn < n, kn < n ? lp.poly(kn) : nullptr));
+  }
+  return MLH_OK;
+}
+
 mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
                          const uint8_t* host_inputs, const uint8_t output[16], mlh_transcript* tr,
                          mlh_pcs_proof* proof) {
@@ -1727,18 +1812,23 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   fp->log_code = log_domain;
   FriDevLoop lp(ctx, fp.get());
   device_arm(ctx);
-  MLH_TRY(lp.init(code.p, log_domain, tr, false));
-  EqSumcheck es(ctx);  // delta = eq(inputs), factored (build_tables_for_pcs)
-  MLH_TRY(es.init(reinterpret_cast<const fe*>(dev_evals), matrix.as<fe>(), n_vars, host_inputs));
-  memcpy(ctx->pinned + kPinSlotA, output, 16);
-  HIP_TRY(ctx, hipMemcpyAsync(lp.prev(), ctx->pinned + kPinSlotA, 16, hipMemcpyHostToDevice,
-                              ctx->stream));
-  uint32_t np = 0;
-  MLH_TRY(es.first_sums(&np));
-  for (uint32_t k = 0; k < n_vars; ++k) {
-    MLH_TRY(es.round(k, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k)));
-    MLH_TRY(es.fold(k, lp.r(k), &np));
-    MLH_TRY(lp.step(k, lp.r(k), false));
+  if (n_vars <= 2 * EqSumcheck::kEqLo) {
+    MLH_TRY(pcs_rounds_fused(ctx, lp, reinterpret_cast<const fe*>(dev_evals), matrix.as<fe>(),
+                             n_vars, host_inputs, output, code.p, log_domain, tr));
+  } else {
+    MLH_TRY(lp.init(code.p, log_domain, tr, false));
+    EqSumcheck es(ctx);  // delta = eq(inputs), factored (build_tables_for_pcs)
+    MLH_TRY(es.init(reinterpret_cast<const fe*>(dev_evals), matrix.as<fe>(), n_vars, host_inputs));
+    memcpy(ctx->pinned + kPinSlotA, output, 16);
+    HIP_TRY(ctx, hipMemcpyAsync(lp.prev(), ctx->pinned + kPinSlotA, 16, hipMemcpyHostToDevice,
+                                ctx->stream));
+    uint32_t np = 0;
+    MLH_TRY(es.first_sums(&np));
+    for (uint32_t k = 0; k < n_vars; ++k) {
+      MLH_TRY(es.round(k, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k)));
+      MLH_TRY(es.fold(k, lp.r(k), &np));
+      MLH_TRY(lp.step(k, lp.r(k), false));
+    }
   }
   MLH_TRY(lp.finish(32ull * n_vars));
   // host transcript replay: root_0, then per round (c1, c2), root_{k+1} / last

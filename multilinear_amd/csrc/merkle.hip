@@ -172,9 +172,11 @@ top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ 
            RootAbsorb ra) {
   __shared__ Sha256State s[1024];
   __shared__ DevSha ts;
-  __shared__ uint32_t stage[8];
+  __shared__ uint32_t stage[8], pw[8];
   if (ra.t && threadIdx.x < sizeof(DevSha) / 4)
     reinterpret_cast<uint32_t*>(&ts)[threadIdx.x] = reinterpret_cast<const uint32_t*>(ra.t)[threadIdx.x];
+  if (ra.poly_in && threadIdx.x < 8)  // (loaded with the level, not on lane 0's chain)
+    pw[threadIdx.x] = reinterpret_cast<const uint32_t*>(ra.poly_in)[threadIdx.x];
   for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) s[i] = digest_load(level + i * 32);
   __syncthreads();
   uint64_t off = 0;
@@ -200,6 +202,12 @@ top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ 
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = bswap32(s[0].h[i]);
     dsha_absorb<8>(ts, w, stage);
+    if (ra.poly_in) {
+      uint32_t v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = pw[i];
+      dsha_absorb<8>(ts, v, stage);
+    }
     DevSha* t = ra.t;
     *t = ts;
     if (ra.copy_out) {
@@ -315,8 +323,11 @@ hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, 
     hipLaunchKernelGGL(top_kernel, dim3(1), dim3(threads), 0, st, layers + off * 32, n,
                        layers + (off + n) * 32, ra);
   } else if (ra.t) {  // the level is the root already (one leaf)
-    hipError_t e = launch_transcript_absorb(ra.t, layers + off * 32, 32, ra.r_out, st,
-                                            ra.copy_out);
+    hipError_t e = launch_transcript_absorb(ra.t, layers + off * 32, 32, ra.poly_in ? nullptr : ra.r_out,
+                                            st, ra.copy_out);
+    if (e == hipSuccess && ra.poly_in)
+      e = launch_transcript_absorb(ra.t, reinterpret_cast<const uint8_t*>(ra.poly_in), 32, ra.r_out, st,
+                                   nullptr);
     if (e != hipSuccess) return e;
   }
   return hipGetLastError();

@@ -18,10 +18,13 @@ struct DevSha;
 // copy_out, and write next_challenge() to r_out (each pointer optional; t
 // null = no transcript step).  Same effect as launch_transcript_absorb(t,
 // root, 32, r_out, st, copy_out) after the tree, without its launch.
+// poly_in (optional): 32 more bytes absorbed after the root and before the
+// challenge -- a PCS round's LE16(c1) || LE16(c2) (multilinear_pcs.rs:57-75).
 struct RootAbsorb {
   DevSha* t = nullptr;
   fe* r_out = nullptr;
   uint8_t* copy_out = nullptr;
+  const fe* poly_in = nullptr;
 };
 hipError_t launch_merkle_levels(uint8_t* layers, uint64_t L, hipStream_t st,
                                 RootAbsorb ra = RootAbsorb());

@@ -74,10 +74,20 @@ struct Tp {
     return MLH_OK;
   }
   // chunk i (bytes_per_rank) of send goes to rank i; chunk i of recv came from rank i
-  mlh_status all_to_all(const void* send, void* recv, uint64_t bytes_per_rank) {
+  // lab (optional): a kernel-timer label (mlh_profile_*) for the exchange
+  mlh_status all_to_all(const void* send, void* recv, uint64_t bytes_per_rank,
+                        const char* lab = nullptr) {
     MLH_TRY(prep());
-    if (t->all_to_all(t->user, send, recv, bytes_per_rank, ctx->stream) != 0)
-      return fail(ctx, MLH_ERR_COMM, "transport all_to_all failed");
+    auto go = [&]() { return t->all_to_all(t->user, send, recv, bytes_per_rank, ctx->stream); };
+    int rc;
+    if (lab) {
+      ProfScope ps(ctx, lab);
+      rc = go();
+      ps.end();
+    } else {
+      rc = go();
+    }
+    if (rc != 0) return fail(ctx, MLH_ERR_COMM, "transport all_to_all failed");
     return MLH_OK;
   }
   // recv = concatenation over ranks (rank order) of every rank's `bytes`
@@ -159,6 +169,18 @@ void mlh_comm_destroy(mlh_comm* c) {
   delete c;
 }
 
+mlh_status mlh_comm_info(mlh_comm* c, uint32_t* count, uint32_t* rank, int* device) {
+  if (!c || !c->comm) return MLH_ERR_INVALID;
+  int n = 0, r = 0, d = -1;
+  if (ncclCommCount(c->comm, &n) != ncclSuccess || ncclCommUserRank(c->comm, &r) != ncclSuccess ||
+      ncclCommCuDevice(c->comm, &d) != ncclSuccess)
+    return MLH_ERR_COMM;
+  if (count) *count = (uint32_t)n;
+  if (rank) *rank = (uint32_t)r;
+  if (device) *device = d;
+  return MLH_OK;
+}
+
 mlh_status mlh_comm_transport(mlh_comm* c, mlh_transport* out) {
   if (!c || !out) return MLH_ERR_INVALID;
   out->world = c->world;
@@ -196,7 +218,7 @@ mlh_status mlh_sharded_ntt(mlh_ctx* ctx, const mlh_transport* t, const void* dev
   MLH_TRY(b.get(M * 16, &recv));
   if (!inverse) {
     MLH_TRY(mlh_ntt(ctx, dev_in, z, log_n - tp.p, gp));
-    MLH_TRY(tp.all_to_all(z, recv, M / tp.P * 16));
+    MLH_TRY(tp.all_to_all(z, recv, M / tp.P * 16, "ntt_all_to_all"));
     MLH_TRY(mlh_shard_ntt_cross(ctx, recv, dev_out, log_n, tp.p, tp.rank, gen, 0));
   } else {
     MLH_TRY(mlh_shard_ntt_cross(ctx, dev_in, z, log_n, tp.p, tp.rank, gen, 1));
@@ -276,7 +298,7 @@ mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const voi
     HIP_TRY(ctx, hipStreamWaitEvent(side, a_done[k], 0));
     {
       StreamSwap sw(ctx, side);
-      MLH_TRY(tp.all_to_all(z[k], recv, M / tp.P * 16));
+      MLH_TRY(tp.all_to_all(z[k], recv, M / tp.P * 16, "ntt_all_to_all"));
       if (!inverse) MLH_TRY(mlh_shard_ntt_cross(ctx, recv, dev_out[i], log_n, tp.p, tp.rank, gen, 0));
       else MLH_TRY(mlh_intt(ctx, recv, dev_out[i], log_n - tp.p, gp));
     }

@@ -676,6 +676,64 @@ mobius_pass_kernel(const fe* src, fe* c, uint32_t log_n, uint32_t b0, uint32_t n
   (void)log_n;
 }
 
+// The same transform over 8 index bits [b0, b0 + 8) with the butterflies in
+// registers: a tile is 2^8 positions (the 8 bits) x 8 others (index bits 0..2
+// when b0 >= 3: 128-byte runs; bits 8..10 when b0 = 0: consecutive blocks),
+// 2048 elements; each thread holds 8 elements and applies 3 of the bits in
+// registers, 3 more after one LDS exchange and the last 2 after a second --
+// two exchanges instead of one LDS read-modify-write sweep per bit.  (Moebius
+// steps for different bits commute, so any order of the bits is the same map.)
+template <int SIGN>
+__device__ __forceinline__ void mobius_reg(fe (&v)[8], uint32_t jbits) {
+#pragma unroll
+  for (uint32_t b = 0; b < 3; ++b) {
+    if (!((jbits >> b) & 1u)) continue;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+      if (j & (1u << b)) v[j] = SIGN < 0 ? fe_sub(v[j], v[j ^ (1u << b)]) : fe_add(v[j], v[j ^ (1u << b)]);
+  }
+}
+template <int SIGN>
+__global__ void __launch_bounds__(256)
+mobius_pass8_kernel(const fe* src, fe* c, uint32_t b0) {
+  __shared__ fe lds[2048];
+  const uint32_t t = threadIdx.x;
+  const bool lowb = b0 == 0;
+  // thread -> (o, g): lanes along the contiguous index direction
+  const uint32_t o = lowb ? t >> 5 : t & 7, g = lowb ? t & 31 : t >> 3;
+  const uint64_t W = 1ull << b0;
+  uint64_t base;  // index of (p = 0, o = 0)
+  if (lowb) {
+    base = (uint64_t)blockIdx.x << 11;
+  } else {
+    const uint64_t lowcount = W >> 3, tile = blockIdx.x;
+    base = ((tile / lowcount) << (b0 + 8)) + ((tile % lowcount) << 3);
+  }
+  auto gidx = [&](uint32_t p) -> uint64_t { return lowb ? base + (o << 8) + p : base + p * W + o; };
+  auto lidx = [&](uint32_t p) -> uint32_t { return lowb ? (o << 8) + p : (p << 3) + o; };
+  fe v[8];
+  // round 1: positions g + 32 j (bits 5, 6, 7 in registers)
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) v[j] = fe_load(src + gidx(g + 32 * j));
+  mobius_reg<SIGN>(v, 7);
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) lds[lidx(g + 32 * j)] = v[j];
+  __syncthreads();
+  // round 2: positions (g & 3) + 4 j + 32 (g >> 2) (bits 2, 3, 4)
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) v[j] = lds[lidx((g & 3) + 4 * j + 32 * (g >> 2))];
+  mobius_reg<SIGN>(v, 7);
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) lds[lidx((g & 3) + 4 * j + 32 * (g >> 2))] = v[j];
+  __syncthreads();
+  // round 3: positions (j & 3) + 4 (j >> 2) + 8 g (bits 0, 1)
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) v[j] = lds[lidx((j & 3) + 4 * (j >> 2) + 8 * g)];
+  mobius_reg<SIGN>(v, 3);
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) fe_store(c + gidx((j & 3) + 4 * (j >> 2) + 8 * g), v[j]);
+}
+
 // out[i] = in[bitrev(i)] (bit_reverse_permutation, src/ntt/mod.rs:113-123).
 __global__ void __launch_bounds__(256)
 bitrev_kernel(const fe* __restrict__ in, fe* __restrict__ out, uint32_t log_n) {
@@ -683,6 +741,88 @@ bitrev_kernel(const fe* __restrict__ in, fe* __restrict__ out, uint32_t log_n) {
   if (i >= (1ull << log_n)) return;
   const uint64_t j = log_n ? (__builtin_bitreverse64(i) >> (64 - log_n)) : 0;
   fe_store(out + i, fe_load(in + j));
+}
+
+// ---- PCS rounds off the transcript kernel ----------------------------------
+// PCSProverData::fold (multilinear_pcs.rs:43-76): round k's polynomial
+// (sumcheck.rs:174-202) depends on r_{k-1} but not on the FRI root absorbed
+// between the two challenges, so it is computed here -- one small workgroup on
+// the eq-factored table -- and absorbed, with root k, by the launch that writes
+// root k (top_kernel, RootAbsorb::poly_in), which then draws r_k.  Nothing of
+// the sumcheck but those 32 bytes sits on the transcript chain.
+//
+// The table of round k (MSB = variable k) is, in the head (k < B), the B
+// corner sums Y[c] = sum_i T[c 2^a + i] lo[i] folded over the variables
+// already challenged, with e = H_k = eq(p_{k+1}..p_{B-1}); in the tail it is T
+// folded over the B head variables (fold_group_eq passes) and then over the
+// tail variables challenged so far, with e = eq(p_{k+1}..p_{L-1}) (Hs).  With
+// delta_k = c_k eq(p_k..) (never materialised):
+//   E_b = sum_{i<h/2} tab[b h/2 + i] e[i],  s1 = c_k p_k E1,
+//   s2 = c_k (3 p_k - 1)(2 E1 - E0),  e0 = claim - s1,
+//   c2 = (s2 - 2 s1 + e0) / 2,  c1 = s1 - e0 - c2        (x = 0, 1, 2)
+// and after r: claim' = e0 + c1 r + c2 r^2, c' = c ((1 - r)(1 - p) + r p).
+__global__ void __launch_bounds__(kRedThreads)
+pcs_round_kernel(const fe* src, fe* dst, uint32_t log_h, int fold, const fe* __restrict__ r_prev,
+                 const fe* __restrict__ p_prev, const fe* __restrict__ p_k,
+                 const fe* __restrict__ e, PcsRoundState* st, fe* __restrict__ poly_out) {
+  const uint64_t h = 1ull << log_h, q = h / 2;
+  fe r = fe_zero();
+  if (r_prev) r = fe_load(r_prev);
+  fe E0 = fe_zero(), E1 = fe_zero();
+  for (uint64_t i = threadIdx.x; i < q; i += blockDim.x) {
+    fe lo, hi;
+    if (fold) {  // tab = src folded over its MSB with r (sumcheck.rs:234-247)
+      lo = lerp_s(fe_load(src + i), fe_load(src + i + h), r);
+      hi = lerp_s(fe_load(src + i + q), fe_load(src + i + q + h), r);
+      fe_store(dst + i, lo);
+      fe_store(dst + i + q, hi);
+    } else {
+      lo = fe_load(src + i);
+      hi = fe_load(src + i + q);
+    }
+    const fe ei = fe_load(e + i);
+    E0 = fe_add(E0, fe_mul_s(lo, ei));
+    E1 = fe_add(E1, fe_mul_s(hi, ei));
+  }
+  block_reduce2(E0, E1);
+  if (threadIdx.x != 0) return;
+  const fe one = fe_one();
+  fe claim = fe_load(&st->claim), c = fe_load(&st->c);
+  if (r_prev) {  // the previous round's claim p(r) and eq scale
+    const fe pp = fe_load(p_prev);
+    claim = fe_add(fe_load(&st->e0), fe_mul_s(fe_add(fe_load(&st->c1), fe_mul_s(fe_load(&st->c2), r)), r));
+    c = fe_mul_s(c, fe_add(fe_mul_s(fe_sub(one, r), fe_sub(one, pp)), fe_mul_s(r, pp)));
+  }
+  const fe p = fe_load(p_k);
+  const fe s1 = fe_mul_s(c, fe_mul_s(p, E1));
+  const fe s2 = fe_mul_s(fe_mul_s(c, fe_sub(fe_add(fe_dbl(p), p), one)), fe_sub(fe_dbl(E1), E0));
+  const fe e0 = fe_sub(claim, s1);
+  const fe c2 = fe_half(fe_add(fe_sub(s2, fe_dbl(s1)), e0));
+  const fe c1 = fe_sub(fe_sub(s1, e0), c2);
+  fe_store(poly_out, c1);
+  fe_store(poly_out + 1, c2);
+  fe_store(&st->claim, claim);
+  fe_store(&st->c, c);
+  fe_store(&st->e0, e0);
+  fe_store(&st->c1, c1);
+  fe_store(&st->c2, c2);
+}
+
+// wf[c] = prod_{u<JA} (c_u ? r_u : 1 - r_u), wf[64 + c] the same over
+// r_{JA..JA+JB-1} (c_u = bit J-1-u of c): fold_group_eq's weights of two groups.
+__global__ void eq_weights_kernel(const fe* __restrict__ rs, uint32_t JA, uint32_t JB,
+                                  fe* __restrict__ wf) {
+  const uint32_t t = threadIdx.x;
+  const bool B = t >= 64;
+  const uint32_t c = t & 63, J = B ? JB : JA;
+  if (c >= (1u << J)) return;
+  const fe one = fe_one();
+  fe w = one;
+  for (uint32_t u = 0; u < J; ++u) {
+    const fe r = fe_load(rs + (B ? JA : 0) + u);
+    w = fe_mul_s(w, (c >> (J - 1 - u)) & 1u ? r : fe_sub(one, r));
+  }
+  fe_store(wf + t, w);
 }
 
 // ---- launchers -------------------------------------------------------------
@@ -917,6 +1057,21 @@ hipError_t launch_mobius(fe* c, uint32_t log_n, bool inverse_zeta, hipStream_t s
   uint32_t b0 = 0;
   while (b0 < log_n) {
     const uint32_t nb = (log_n - b0) < 8 ? (log_n - b0) : 8;
+#ifndef MLH_MOBIUS_REG
+#define MLH_MOBIUS_REG 1
+#endif
+    if (MLH_MOBIUS_REG && nb == 8 && log_n >= 11 && (b0 == 0 || b0 >= 3)) {
+      const unsigned tiles = (unsigned)((1ull << log_n) >> 11);
+      if (inverse_zeta)
+        hipLaunchKernelGGL(mobius_pass8_kernel<1>, dim3(tiles), dim3(256), 0, st, src, c, b0);
+      else
+        hipLaunchKernelGGL(mobius_pass8_kernel<-1>, dim3(tiles), dim3(256), 0, st, src, c, b0);
+      src = c;
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      b0 += 8;
+      continue;
+    }
     const uint64_t W = 1ull << b0;
     const uint64_t cols = W < 8 ? W : 8;
     // tile: 2^nb rows x cols elements must fit 2048 LDS slots
@@ -1992,6 +2147,22 @@ hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, ui
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(sumcheck_group_kernel, dim3(1), dim3(kRedThreads), 0, st, partials, nb, J, J2,
                      t0, t1, prev, t, polys, rs, pts, c, kw, wout, ctl);
+  return hipGetLastError();
+}
+
+hipError_t launch_pcs_round(const fe* src, fe* dst, uint32_t log_h, bool fold, const fe* r_prev,
+                            const fe* p_prev, const fe* p_k, const fe* e, PcsRoundState* st,
+                            fe* poly_out, hipStream_t stream) {
+  if (log_h < 1 || log_h > kTailLogMax || (fold && !r_prev) || (r_prev && !p_prev))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pcs_round_kernel, dim3(1), dim3(kRedThreads), 0, stream, src, dst, log_h,
+                     fold ? 1 : 0, r_prev, p_prev, p_k, e, st, poly_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_eq_weights(const fe* rs, uint32_t JA, uint32_t JB, fe* wf, hipStream_t st) {
+  if (JA > 6 || JB > 6) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(eq_weights_kernel, dim3(1), dim3(128), 0, st, rs, JA, JB, wf);
   return hipGetLastError();
 }
 

@@ -96,6 +96,20 @@ struct EqSetupArgs {
 // K + W table at kw + 64 k.
 hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* lo, fe* H, fe* Hs,
                            DevSha* dt_out, fe* prev_out, hipStream_t st, uint32_t* kw = nullptr);
+// PCS rounds (sumcheck.hip "PCS rounds off the transcript kernel"): the
+// running claim, eq scale and last polynomial (e0, c1, c2) in HBM.
+struct PcsRoundState {
+  fe claim, c, e0, c1, c2;
+};
+// Round k's (c1, c2) into poly_out from the table src (2^log_h entries after
+// the optional fold of src's 2^(log_h+1) entries with *r_prev into dst) and
+// e = eq suffix (2^(log_h-1) entries); r_prev non-null: first the previous
+// round's claim / eq scale update (p_prev = its point).  One workgroup.
+hipError_t launch_pcs_round(const fe* src, fe* dst, uint32_t log_h, bool fold, const fe* r_prev,
+                            const fe* p_prev, const fe* p_k, const fe* e, PcsRoundState* st,
+                            fe* poly_out, hipStream_t stream);
+// fold_group_eq weights of rs[0..JA) at wf[0..2^JA) and rs[JA..JA+JB) at wf[64..64+2^JB)
+hipError_t launch_eq_weights(const fe* rs, uint32_t JA, uint32_t JB, fe* wf, hipStream_t st);
 // out[i] = (*c) * src[i]
 hipError_t launch_scale_dev(const fe* src, const fe* c, uint64_t n, fe* out, hipStream_t st);
 // Trace::evaluate: out[j] = sum_i eq[i] * m[i * width + j], j < width;

@@ -159,6 +159,13 @@ class RcclComm:
     def transport(self):
         return self.c
 
+    def info(self):
+        """What RCCL reports for this communicator: {"ranks", "rank", "device"}
+        (ncclCommCount / ncclCommUserRank / ncclCommCuDevice)."""
+        n, r, d = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
+        check(lib().mlh_comm_info(self.h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d)))
+        return {"ranks": n.value, "rank": r.value, "device": d.value, "transport": "rccl"}
+
     def close(self):
         if self.h:
             lib().mlh_comm_destroy(self.h)
@@ -219,6 +226,37 @@ class HostTransport:
     @property
     def transport(self):
         return self.c
+
+    def info(self):
+        return {"ranks": self.tp.world, "rank": self.tp.rank, "device": self.device,
+                "transport": "host-staged torch.distributed (%s)" % self.tp.dist.get_backend(self.tp.group)}
+
+
+def ntt_block_owner(j, log_total, log_p):
+    """(rank, local index) holding X[j] of a sharded forward NTT (block
+    2^(log_total - 2 log_p) output layout)."""
+    log_s = log_total - 2 * log_p
+    r = (j >> log_s) & ((1 << log_p) - 1)
+    return r, ((j >> (log_s + log_p)) << log_s) | (j & ((1 << log_s) - 1))
+
+
+def ntt_spot_terms(x_local, log_total, gen, rank, world, js, device=0, ctx=None):
+    """This rank's share of X[j] = NTT(x)[j] = sum_i x_i gen^(i j) for each j
+    in ``js``, x cyclic over the ranks (rank g holds x[g + P m]): X[j] =
+    sum_g gen^(j g) poly_g(gen^(j P)), poly_g the rank's local coefficients as
+    a polynomial (Polynomial::evaluate, ntt/mod.rs:61-67, on the device:
+    mlh_poly_evaluate).  The sum over ranks mod M of these terms is X[j] -- an
+    independent check of a sharded transform's output at a few points.
+    ctx: an explicit mlh context (default: the device's)."""
+    ctx = ctx if ctx is not None else context(device)
+    n = x_local.shape[0]
+    out = (ctypes.c_uint8 * 16)()
+    terms = []
+    for j in js:
+        pt = pow(gen, j * world, M)
+        check(lib().mlh_poly_evaluate(ctx, ptr(x_local), n, fe_bytes(pt), out), ctx)
+        terms.append(fe_from_bytes(out) * pow(gen, j * rank, M) % M)
+    return terms
 
 
 def _tp(transport):

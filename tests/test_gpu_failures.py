@@ -80,17 +80,26 @@ def test_sumcheck_spin_timeout_is_an_error(n):
 
 
 def test_pcs_spin_timeout_is_an_error():
-    """The PCS prove's one-round cooperative launches (sumcheck_group_kernel)
-    and its eq tail report a timeout the same way."""
-    n = 14
-    ev, pts, total = _sumcheck_case(n, 77)
-    evd = D.to_device(D.ints_to_limbs(ev))
+    """The batched PCS prove's one-round cooperative launches
+    (sumcheck_group_kernel) report a timeout the same way.  The plain PCS
+    prove (n <= 24) runs no cooperative kernel: at the same limit it is
+    unaffected and its proof verifies."""
+    from multilinear_amd.batched import BatchedPCSProof
+
+    n, m = 13, 2
+    r = random.Random(78)
+    polys = [[r.randrange(F.M) for _ in range(1 << n)] for _ in range(m)]
+    pts = [r.randrange(F.M) for _ in range(n)]
+    outs = [OPL.mle_evaluate(p, pts) for p in polys]
+    evd = D.to_device(D.ints_to_limbs([v for p in polys for v in p]))
     with spin_limit(1):
         with pytest.raises(_lib.MlhError) as ei:
-            MP.PCSProof.prove(pts, total, evd, Transcript())
+            BatchedPCSProof.prove(pts, outs, evd, Transcript())
         assert ei.value.status == _lib.MLH_ERR_DEVICE
-    pf = MP.PCSProof.prove(pts, total, evd, Transcript())
-    assert pf.verify(Transcript())
+        pf = MP.PCSProof.prove(pts, outs[0], evd[: 1 << n], Transcript())
+        assert pf.verify(Transcript())
+    got = BatchedPCSProof.prove(pts, outs, evd, Transcript())
+    assert got.verify(Transcript())
 
 
 def _verify(table):

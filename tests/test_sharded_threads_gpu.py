@@ -184,6 +184,47 @@ def test_ntt_batch_pipelined_vs_c_oracle(P, log_n, count):
             assert np.array_equal(res[r][1][i], res[r][2][i]), "inverse of transform %d, rank %d" % (i, r)
 
 
+def test_ntt_spot_check_logic_vs_c_oracle_p8():
+    """The bench's in-run check of the sharded headline (bench.py
+    sharded_ntt_check) at P = 8 device-ordered ranks: the per-rank terms
+    gen^(jg) poly_g(gen^(jP)) (mlh_poly_evaluate on the cyclic shard) summed
+    over ranks equal the C oracle's X[j], and equal the sharded output at the
+    rank / local index ntt_block_owner names; an output altered at one
+    sampled index is caught."""
+    P, log_n = 8, 18
+    L = DV.lib()
+    x = DV.random_limbs(1 << log_n, seed=4242)
+    g = _gen(log_n)
+    rr = random.Random(0xC0FFEE)
+    js = [0, (1 << log_n) - 1] + [rr.randrange(1 << log_n) for _ in range(8)]
+
+    def body(r, ctx, st, t):
+        xin = DV.to_device(S.shard_cyclic(x, P, r))
+        out = DV.empty(xin.shape[0])
+        pi = (ctypes.c_void_p * 1)(xin.data_ptr())
+        po = (ctypes.c_void_p * 1)(out.data_ptr())
+        torch.cuda.current_stream().synchronize()
+        DV.check(L.mlh_sharded_ntt_batch(ctx, _tp(t), pi, po, 1, log_n, DV.fe_bytes(g), 0), ctx)
+        DV.check(L.mlh_synchronize(ctx), ctx)
+        terms = S.ntt_spot_terms(xin, log_n, g, r, P, js, ctx=ctx)
+        return DV.from_device(out), terms
+
+    res = _run_ranks(P, body)
+    want = C.ntt(x, log_n, g)
+    want_ints = DV.limbs_to_ints(want)
+    outs = [DV.limbs_to_ints(res[r][0]) for r in range(P)]
+    for i, j in enumerate(js):
+        X = sum(res[r][1][i] for r in range(P)) % F.M
+        assert X == want_ints[j], j
+        owner, loc = S.ntt_block_owner(j, log_n, 3)
+        assert outs[owner][loc] == X, j
+    # an altered output element is seen by the same comparison
+    j = js[5]
+    owner, loc = S.ntt_block_owner(j, log_n, 3)
+    outs[owner][loc] = (outs[owner][loc] + 1) % F.M
+    assert outs[owner][loc] != sum(res[r][1][5] for r in range(P)) % F.M
+
+
 def _sumcheck_oracle(ev, pts, claim):
     m, d = ev.copy(), C.eq_table_par(pts)
     n = len(pts)

@@ -1,0 +1,17 @@
+# Round-4 check on one box: the GPU suite (or a -k subset), the N = 2 gloo
+# rehearsal of the multi-GPU bench line (self-certification fields), and the
+# N = 1 bench.  usage: bash tools/r04_check.sh TAG [pytest -k expr]
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+TAG=$1; K=${2:-}
+if [ -n "$K" ]; then
+  timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$K" > gpurun_out/${TAG}_gputest.log 2>&1 || { tail -40 gpurun_out/${TAG}_gputest.log; exit 1; }
+else
+  timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gputest.log 2>&1 || { tail -40 gpurun_out/${TAG}_gputest.log; exit 1; }
+fi
+tail -2 gpurun_out/${TAG}_gputest.log
+MLH_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu --no-extras > gpurun_out/${TAG}_n2.json 2> gpurun_out/${TAG}_n2.err || { tail -30 gpurun_out/${TAG}_n2.err; exit 1; }
+python -c "import json; d=[json.loads(l) for l in open('gpurun_out/${TAG}_n2.json') if l.startswith('{')][-1]; print({k: d.get(k) for k in ['value','comm','rccl_ranks','sharded_phases','sharded_ntt_verified','sharded_ntt_check_error']})"
+timeout -k 10 300 python bench.py --no-cpu > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/${TAG}_bench.json')); print({k:d.get(k) for k in ['value','ms_per_step','fri_commit_ms','fri_prove_ms','sumcheck_ms','pcs_prove_ms','pcs_verified','config5_rs_fri_prove_ms']}); print(d['roofline']['launch_avg_ms'], d['roofline']['frac'])"
