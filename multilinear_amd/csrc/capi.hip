@@ -889,7 +889,9 @@ struct FriDevLoop {
   // fold_step k with the challenge at rp (device); absorbs the new root (or
   // the last element) and (poly_next) 32 more bytes; writes next_challenge()
   // to r(k + 1) if challenge_next.
-  mlh_status step(uint32_t k, const fe* rp, bool challenge_next, const fe* poly_next = nullptr) {
+  // job (optional): a PCS round run by an extra workgroup of the fold launch
+  mlh_status step(uint32_t k, const fe* rp, bool challenge_next, const fe* poly_next = nullptr,
+                  const PcsJob* job = nullptr) {
     if (done) return MLH_OK;
     const FriLayer cur = p->layers.back();
     const uint32_t log_n = cur.log_n;
@@ -898,6 +900,10 @@ struct FriDevLoop {
     void* vals;
     MLH_TRY(pool_alloc(ctx, half_n * sizeof(fe), &vals));
     if (half_n == (1ull << MLH_LOG_BLOWUP)) {  // fri/mod.rs:116-126
+      if (job || poly_next) {
+        pool_free(ctx, vals);
+        return fail(ctx, MLH_ERR_INVALID, "no PCS round after the last FRI fold");
+      }
       HIP_TRY(ctx, launch_fri_fold(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), fe{},
                                    tlo, thi, k, 1ull << p->log_gp, ctx->stream, ShardMap(), rp));
       HIP_TRY(ctx, launch_fri_last(reinterpret_cast<const fe*>(vals), dt(),
@@ -920,7 +926,7 @@ struct FriDevLoop {
     HIP_TRY(ctx, launch_fri_fold_commit(
                      cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), nx.tree, fe{}, tlo,
                      thi, k, 1ull << p->log_gp, ctx->stream, ShardMap(), rp,
-                     RootAbsorb{dt(), challenge_next ? r(k + 1) : nullptr, root(t), poly_next}));
+                     RootAbsorb{dt(), challenge_next ? r(k + 1) : nullptr, root(t), poly_next}, job));
     return MLH_OK;
   }
 
@@ -1757,12 +1763,15 @@ static mlh_status pcs_rounds_fused(mlh_ctx* ctx, FriDevLoop& lp, const fe* evals
   MLH_TRY(lp.init_after_layout(code, log_domain, true, lp.poly(0)));
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t kn = k + 1;  // the round whose polynomial follows r_k
-    if (kn < n) {
-      const fe* pp = es.pts + k;
+    PcsJob job{};
+    if (kn < n) {  // round kn: run by an extra workgroup of FRI step k's fold launch
+      job = PcsJob{nullptr, work, 0, 1, lp.r(k), es.pts + k, es.pts + kn, e_of(kn),
+                   st, lp.poly(kn)};
       if (kn < B) {  // head: fold Y with r_k
-        HIP_TRY(ctx, launch_pcs_round(Y, Y, B - kn, true, lp.r(k), pp, es.pts + kn, e_of(kn), st,
-                                      lp.poly(kn), ctx->stream));
-      } else if (kn == B) {  // fold the table over the B head variables, then round B on it
+        job.src = Y;
+        job.dst = Y;
+        job.log_h = B - kn;
+      } else if (kn == B) {  // fold the table over the B head variables first; round B on it
         const uint32_t JA = B < 6 ? B : 6, JB = B - JA;
         uint32_t nb = 0;
         HIP_TRY(ctx, launch_eq_weights(lp.r(0), JA, JB, wf, ctx->stream));
@@ -1771,15 +1780,15 @@ static mlh_status pcs_rounds_fused(mlh_ctx* ctx, FriDevLoop& lp, const fe* evals
         if (JB)
           HIP_TRY(ctx, launch_fold_group_eq(work, 1ull << (n - JA), JB, 0, lp.r(JA), wf + 64, work,
                                             nullptr, es.lo, a, ctx->partials, ctx->stream, &nb));
-        HIP_TRY(ctx, launch_pcs_round(work, work, a, false, lp.r(k), pp, es.pts + kn, e_of(kn), st,
-                                      lp.poly(kn), ctx->stream));
+        job.src = work;
+        job.log_h = a;
+        job.fold = 0;
       } else {  // tail: fold with r_k (the first tail fold of B = 0 reads the evaluations)
-        const fe* src = (B == 0 && kn == 1) ? evals : work;
-        HIP_TRY(ctx, launch_pcs_round(src, work, n - kn, true, lp.r(k), pp, es.pts + kn, e_of(kn), st,
-                                      lp.poly(kn), ctx->stream));
+        job.src = (B == 0 && kn == 1) ? evals : work;
+        job.log_h = n - kn;
       }
     }
-    MLH_TRY(lp.step(k, lp.r(k), kn < n, kn < n ? lp.poly(kn) : nullptr));
+    MLH_TRY(lp.step(k, lp.r(k), kn < n, kn < n ? lp.poly(kn) : nullptr, kn < n ? &job : nullptr));
   }
   return MLH_OK;
 }

@@ -19,6 +19,7 @@
 //   layer is written once and never re-read for hashing.
 #include "field.hpp"
 #include "merkle.hpp"
+#include "sc_dev.hpp"
 #include "sha256.hpp"
 #include "transcript_dev.hpp"
 
@@ -47,11 +48,18 @@ fri_fold_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next,
   fe_store(next + i, fold_one(a, b, r, tw));
 }
 
+// job.st non-null: the grid's last workgroup runs that PCS round instead
+// (sc_dev.hpp pcs_round_body; it reads the same challenge, so it overlaps the
+// fold and the tree instead of sitting between them).
 __global__ void __launch_bounds__(256)
 fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next,
                        uint8_t* __restrict__ leaves, fe r, const fe* __restrict__ tlo,
                        const fe* __restrict__ thi, uint32_t k, uint64_t n0, ShardMap map,
-                       const fe* __restrict__ rp) {
+                       const fe* __restrict__ rp, PcsJob job) {
+  if (job.st && blockIdx.x == gridDim.x - 1) {
+    pcs_round_body(job);
+    return;
+  }
   if (rp) r = fe_load(rp);
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t h = n / 2, q = n / 4;
@@ -77,9 +85,10 @@ fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict_
 // 129 VGPRs, 3 waves per SIMD, against the fold's 4 memory streams.)
 hipError_t launch_fri_fold_commit(const fe* layer, uint64_t n, fe* next, uint8_t* tree, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
-                                  hipStream_t st, ShardMap map, const fe* r_dev, RootAbsorb ra) {
+                                  hipStream_t st, ShardMap map, const fe* r_dev, RootAbsorb ra,
+                                  const PcsJob* job) {
   hipError_t e = launch_fri_fold_leaves(layer, n, next, tree, r, tlo_inv, thi_inv, k, n0, st, map,
-                                        r_dev);
+                                        r_dev, job);
   if (e != hipSuccess) return e;
   return launch_merkle_levels(tree, n / 4, st, ra);
 }
@@ -95,10 +104,17 @@ hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe
 
 hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t* leaves, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
-                                  hipStream_t st, ShardMap map, const fe* r_dev) {
+                                  hipStream_t st, ShardMap map, const fe* r_dev, const PcsJob* job) {
   const uint64_t q = n / 4;
-  hipLaunchKernelGGL(fri_fold_leaves_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, st,
-                     layer, n, next, leaves, r, tlo_inv, thi_inv, k, n0, map, r_dev);
+  PcsJob pj{};
+  if (job) {
+    if (job->log_h < 1 || job->log_h > 12 || (job->fold && !job->r_prev) || (job->r_prev && !job->p_prev))
+      return hipErrorInvalidValue;
+    pj = *job;
+  }
+  const unsigned blocks = (unsigned)((q + 255) / 256) + (job ? 1u : 0u);
+  hipLaunchKernelGGL(fri_fold_leaves_kernel, dim3(blocks), dim3(256), 0, st, layer, n, next, leaves,
+                     r, tlo_inv, thi_inv, k, n0, map, r_dev, pj);
   return hipGetLastError();
 }
 

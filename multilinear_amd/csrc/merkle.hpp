@@ -60,15 +60,19 @@ hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe
                            const fe* thi_inv, uint32_t k, uint64_t n0, hipStream_t st,
                            ShardMap map = ShardMap(), const fe* r_dev = nullptr);
 // Fold and hash the next layer's leaves (pairs (next[j], next[j + n/4])).
+struct PcsJob;
+// job (optional): one PCS round (sumcheck.hpp PcsJob) run by an extra
+// workgroup of the same launch
 hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t* leaves, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
                                   hipStream_t st, ShardMap map = ShardMap(),
-                                  const fe* r_dev = nullptr);
+                                  const fe* r_dev = nullptr, const PcsJob* job = nullptr);
 // Fold and commit the next layer: its whole tree (L = n/4 leaves, 2L-1
 // digests) into `tree` (leaves hashed by the fold lanes).
 hipError_t launch_fri_fold_commit(const fe* layer, uint64_t n, fe* next, uint8_t* tree, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
                                   hipStream_t st, ShardMap map = ShardMap(),
-                                  const fe* r_dev = nullptr, RootAbsorb ra = RootAbsorb());
+                                  const fe* r_dev = nullptr, RootAbsorb ra = RootAbsorb(),
+                                  const PcsJob* job = nullptr);
 
 }  // namespace mlh

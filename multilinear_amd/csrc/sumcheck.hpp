@@ -101,6 +101,20 @@ hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* 
 struct PcsRoundState {
   fe claim, c, e0, c1, c2;
 };
+// One PCS round's inputs (launch_pcs_round's arguments): src / dst / log_h /
+// fold: the table and its optional fold with *r_prev; p_prev, p_k: points of
+// the previous and this round; e: eq suffix; st: state; poly_out: (c1, c2).
+struct PcsJob {
+  const fe* src;
+  fe* dst;
+  uint32_t log_h, fold;
+  const fe* r_prev;
+  const fe* p_prev;
+  const fe* p_k;
+  const fe* e;
+  PcsRoundState* st;
+  fe* poly_out;
+};
 // Round k's (c1, c2) into poly_out from the table src (2^log_h entries after
 // the optional fold of src's 2^(log_h+1) entries with *r_prev into dst) and
 // e = eq suffix (2^(log_h-1) entries); r_prev non-null: first the previous
