@@ -142,24 +142,24 @@ __global__ void transcript_absorb_kernel(DevSha* t, const uint8_t* src, uint32_t
     if (copy_out) reinterpret_cast<uint32_t*>(copy_out)[tid] = v;
   }
   __syncthreads();
-  if (tid != 0) return;
+  // (one wave: the word paths on a lane pair, dsha2l_step)
   if (words && n == 32) {
     uint32_t w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = stage[i];
-    dsha_absorb<8>(s, w, stage2);
+    dsha2l_step<8>(s, w, stage2, r_out);
   } else if (words) {
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = stage[i];
-    dsha_absorb<4>(s, w, stage2);
-  } else {
+    dsha2l_step<4>(s, w, stage2, r_out);
+  } else if (tid == 0) {
     dsha_update(s, src, n);
     if (copy_out)
       for (uint32_t i = 0; i < n; ++i) copy_out[i] = src[i];
+    if (r_out) fe_store(r_out, dsha_challenge(s));
   }
-  *t = s;
-  if (r_out) fe_store(r_out, dsha_challenge(s));
+  if (tid == 0) *t = s;
 }
 
 hipError_t launch_transcript_absorb(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out,
@@ -175,13 +175,14 @@ __global__ void fri_last_kernel(const fe* vals, DevSha* t, uint32_t* flag, fe* l
   if (threadIdx.x < sizeof(DevSha) / 4)
     reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = reinterpret_cast<const uint32_t*>(t)[threadIdx.x];
   __syncthreads();
-  if (threadIdx.x != 0) return;
   const fe a = fe_load(vals), b = fe_load(vals + 1);
-  *flag = fe_eq(a, b) ? 0u : 1u;
-  fe_store(last_out, a);
+  if (threadIdx.x == 0) {
+    *flag = fe_eq(a, b) ? 0u : 1u;
+    fe_store(last_out, a);
+  }
   const uint32_t w[4] = {a.w[0], a.w[1], a.w[2], a.w[3]};
-  dsha_absorb<4>(s, w, stage);  // LE16(last)
-  *t = s;
+  dsha2l_step<4>(s, w, stage, nullptr);  // LE16(last) (one wave, lane pair)
+  if (threadIdx.x == 0) *t = s;
 }
 
 hipError_t launch_fri_last(const fe* vals, DevSha* t, uint32_t* flag, fe* last_out,

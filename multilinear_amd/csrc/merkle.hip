@@ -197,25 +197,30 @@ top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ 
     off += np;
     n = np;
   }
-  if (ra.t && threadIdx.x == 0) {  // s[0] is the root (memory bytes = bswap of the words)
+  if (ra.t && threadIdx.x < 64) {  // s[0] is the root (memory bytes = bswap of the words)
+    // wave 0 runs the transcript step on a lane pair (dsha2l_step)
     uint32_t w[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = bswap32(s[0].h[i]);
-    dsha_absorb<8>(ts, w, stage);
     if (ra.poly_in) {
-      uint32_t v[8];
+      uint32_t v[16];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = pw[i];
-      dsha_absorb<8>(ts, v, stage);
+      for (int i = 0; i < 8; ++i) {
+        v[i] = w[i];
+        v[8 + i] = pw[i];
+      }
+      dsha2l_step<16>(ts, v, stage, ra.r_out);
+    } else {
+      dsha2l_step<8>(ts, w, stage, ra.r_out);
     }
-    DevSha* t = ra.t;
-    *t = ts;
-    if (ra.copy_out) {
-      uint4* q = reinterpret_cast<uint4*>(ra.copy_out);
-      q[0] = make_uint4(w[0], w[1], w[2], w[3]);
-      q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    if (threadIdx.x == 0) {
+      *ra.t = ts;
+      if (ra.copy_out) {
+        uint4* q = reinterpret_cast<uint4*>(ra.copy_out);
+        q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+      }
     }
-    if (ra.r_out) fe_store(ra.r_out, dsha_challenge(ts));
   }
 }
 

@@ -482,6 +482,119 @@ __device__ inline fe dsha_challenge_kw(const DevSha& s, const uint32_t* kw) {
   return canon_with_carry(v, 0u);
 }
 
+// One compression of the 16 block words w0..w15 (big-endian, wave-uniform)
+// into the chaining value h0..h7 (wave-uniform) on a lane pair: sha2l rounds
+// with the two-lane message schedule; returns the new chaining value.  Out of
+// line with everything passed in registers: a transcript step calls it up to
+// three times, and one copy stays in the instruction cache.
+__device__ __noinline__ Sha256State sha2l_compress(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                                   uint32_t h4, uint32_t h5, uint32_t h6, uint32_t h7,
+                                                   uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                                   uint32_t w4, uint32_t w5, uint32_t w6, uint32_t w7,
+                                                   uint32_t w8, uint32_t w9, uint32_t w10, uint32_t w11,
+                                                   uint32_t w12, uint32_t w13, uint32_t w14,
+                                                   uint32_t w15) {
+  constexpr uint32_t K[64] = MLH_SHA_K;
+  const uint32_t h[8] = {h0, h1, h2, h3, h4, h5, h6, h7};
+  uint32_t blk[16] = {w0, w1, w2, w3, w4, w5, w6, w7, w8, w9, w10, w11, w12, w13, w14, w15};
+  const Sched2L sc = sched2l_init();
+  Sha2L q;
+  sha2l_init(q, h);
+  sha2l_rounds<0, 64>(q, [&](int t) -> uint32_t {
+    if (t >= 16) sha2l_sched(blk, t, sc);
+    return K[t] + blk[t & 15];
+  });
+  uint32_t v[8];
+  sha2l_state(q, v);
+  Sha256State o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o.h[i] = h[i] + v[i];
+  return o;
+}
+__device__ __forceinline__ void sha2l_compress_into(uint32_t (&h)[8], const uint32_t (&b)[16]) {
+  const Sha256State o = sha2l_compress(h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], b[0], b[1], b[2],
+                                       b[3], b[4], b[5], b[6], b[7], b[8], b[9], b[10], b[11], b[12],
+                                       b[13], b[14], b[15]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] = o.h[i];
+}
+
+// Transcript step on a lane pair, for a caller whose whole wave runs it
+// (uniform control flow; lanes 0 and 1 carry the two-lane SHA-256, the others
+// compute the same): absorb the NW words w (memory byte order, wave-uniform)
+// into s (shared memory; lane 0 writes it), then (r_out) write
+// next_challenge() to r_out.  Same state and challenge as dsha_absorb +
+// dsha_challenge, with the compressions at ~2.5 instead of ~4.3 us.  A
+// length not a multiple of 4 (bytes absorbed on the host) takes the one-lane
+// path.
+template <int NW>
+__device__ void dsha2l_step(DevSha& s, const uint32_t (&w)[NW], uint32_t* stage, fe* r_out) {
+  const uint32_t lane = __lane_id();
+  const uint64_t len0 = s.len;
+  if (len0 & 3) {
+    if (lane == 0) {
+      dsha_absorb<NW>(s, w, stage);
+      if (r_out) fe_store(r_out, dsha_challenge(s));
+    }
+    return;
+  }
+  uint32_t* bw = reinterpret_cast<uint32_t*>(s.buf);
+  uint32_t h[8], blk[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] = s.h[i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) blk[i] = bswap32(bw[i]);
+  const uint32_t pos0 = (uint32_t)(len0 & 63) / 4;
+  // the words that fit the buffer, then (if it fills) one compression and the
+  // rest into the next block -- selects over constant indices, no dynamic
+  // register indexing
+  uint32_t nxt[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) nxt[j] = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t x = bswap32(w[i]);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if ((uint32_t)j == pos0 + i) blk[j] = x;
+      if ((uint32_t)j + 16 == pos0 + i) nxt[j] = x;
+    }
+  }
+  uint32_t pos = pos0 + NW;
+  if (pos >= 16) {
+    sha2l_compress_into(h, blk);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) blk[j] = nxt[j];
+    pos -= 16;
+  }
+  const uint64_t len = len0 + 4 * NW;
+  if (lane == 0) {  // the state: chaining value, buffer (memory byte order), length
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.h[i] = h[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bw[i] = bswap32(blk[i]);
+    s.len = len;
+  }
+  if (!r_out) return;
+  // next_challenge(): finalize a copy -- 0x80, zeros, the bit length
+  const uint64_t bits = len * 8;
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    blk[j] = (uint32_t)j < pos ? blk[j] : ((uint32_t)j == pos ? 0x80000000u : 0u);
+  if (pos >= 14) {
+    sha2l_compress_into(h, blk);
+#pragma unroll
+    for (int j = 0; j < 14; ++j) blk[j] = 0;
+  }
+  blk[14] = (uint32_t)(bits >> 32);
+  blk[15] = (uint32_t)bits;
+  sha2l_compress_into(h, blk);
+  fe v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v.w[i] = bswap32(h[i]);
+  if (lane == 0) fe_store(r_out, canon_with_carry(v, 0u));
+}
+
 // absorb n bytes from device memory, then (if r_out) write next_challenge();
 // copy_out (optional) receives a copy of the absorbed bytes
 hipError_t launch_transcript_absorb(DevSha* t, const uint8_t* src, uint32_t n, fe* r_out,
