@@ -19,6 +19,7 @@
 //   layer is written once and never re-read for hashing.
 #include "field.hpp"
 #include "merkle.hpp"
+#include "merkle_dev.hpp"
 #include "sc_dev.hpp"
 #include "sha256.hpp"
 #include "transcript_dev.hpp"
@@ -79,6 +80,53 @@ fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict_
   digest_store(leaves + j * 32, sha256_msg32(m));
 }
 
+// fold_step + commit of a next layer whose tree has L = n/4 <= 1024 leaves,
+// in ONE workgroup of max(64, L) threads (the latency-bound tail rounds of a
+// prove): lane j folds pairs j and j + L, hashes leaf j into shared memory,
+// the levels run in shared memory (lds_tree_levels), wave 0 absorbs the root
+// (+ poly) and draws the next challenge (root_transcript); job.st: the PCS
+// round whose polynomial that absorb takes runs in between (sc_dev.hpp).
+// One launch per round instead of fold + top (+ the PCS round's): each launch
+// boundary drains the chain for several microseconds.
+__global__ void __launch_bounds__(1024)
+fri_fold_commit_small_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next,
+                             uint8_t* __restrict__ tree, fe r, const fe* __restrict__ tlo,
+                             const fe* __restrict__ thi, uint32_t k, uint64_t n0, ShardMap map,
+                             const fe* __restrict__ rp, RootAbsorb ra, PcsJob job) {
+  __shared__ Sha256State s[1024];
+  __shared__ DevSha ts;
+  __shared__ uint32_t stage[8], pw[8];
+  if (ra.t && threadIdx.x < sizeof(DevSha) / 4)
+    reinterpret_cast<uint32_t*>(&ts)[threadIdx.x] = reinterpret_cast<const uint32_t*>(ra.t)[threadIdx.x];
+  if (rp) r = fe_load(rp);
+  const uint64_t h = n / 2, q = n / 4;
+  const uint32_t j = threadIdx.x;
+  if (j < q) {
+    const fe a0 = fe_load(layer + j), b0 = fe_load(layer + j + h);
+    const fe a1 = fe_load(layer + j + q), b1 = fe_load(layer + j + q + h);
+    const fe x0 = fold_one(a0, b0, r, twiddle(tlo, thi, (map.global(j) << k) & (n0 - 1)));
+    const fe x1 = fold_one(a1, b1, r, twiddle(tlo, thi, (map.global(j + q) << k) & (n0 - 1)));
+    fe_store(next + j, x0);
+    fe_store(next + j + q, x1);
+    uint32_t m[8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      m[t] = bswap32(x0.w[t]);
+      m[4 + t] = bswap32(x1.w[t]);
+    }
+    const Sha256State leaf = sha256_msg32(m);
+    s[j] = leaf;
+    digest_store(tree + (uint64_t)j * 32, leaf);
+  }
+  if (job.st) pcs_round_body(job);  // (every thread: it reduces over the workgroup)
+  __syncthreads();
+  if (ra.poly_in && threadIdx.x < 8)  // written just above when job.st (same workgroup)
+    pw[threadIdx.x] = reinterpret_cast<const uint32_t*>(ra.poly_in)[threadIdx.x];
+  __syncthreads();
+  lds_tree_levels(s, q, tree + q * 32);
+  root_transcript(s[0], ts, stage, ra.poly_in ? pw : nullptr, ra);
+}
+
 // fold_step + commit of the next layer.  (A variant that also hashed the
 // tree's first two levels in the fold lanes, like leaf_pairs_level2_kernel,
 // measured 10 % slower over a FRI prove: 8 folds + 7 hashes per lane need
@@ -87,6 +135,21 @@ hipError_t launch_fri_fold_commit(const fe* layer, uint64_t n, fe* next, uint8_t
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
                                   hipStream_t st, ShardMap map, const fe* r_dev, RootAbsorb ra,
                                   const PcsJob* job) {
+#ifndef MLH_FRI_SMALL_LEAVES
+#define MLH_FRI_SMALL_LEAVES 1024  // trees of at most this many leaves: one fused launch (0: off)
+#endif
+  if (n / 4 <= MLH_FRI_SMALL_LEAVES && n >= 8) {
+    PcsJob pj{};
+    if (job) {
+      if (job->log_h < 1 || job->log_h > 12 || (job->fold && !job->r_prev) || (job->r_prev && !job->p_prev))
+        return hipErrorInvalidValue;
+      pj = *job;
+    }
+    const unsigned threads = n / 4 < 64 ? 64 : (unsigned)(n / 4);
+    hipLaunchKernelGGL(fri_fold_commit_small_kernel, dim3(1), dim3(threads), 0, st, layer, n, next, tree,
+                       r, tlo_inv, thi_inv, k, n0, map, r_dev, ra, pj);
+    return hipGetLastError();
+  }
   hipError_t e = launch_fri_fold_leaves(layer, n, next, tree, r, tlo_inv, thi_inv, k, n0, st, map,
                                         r_dev, job);
   if (e != hipSuccess) return e;

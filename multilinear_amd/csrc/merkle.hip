@@ -18,6 +18,7 @@
 //   * top          : one workgroup finishes the last <= 1024 nodes in LDS.
 #include "field.hpp"
 #include "merkle.hpp"
+#include "merkle_dev.hpp"
 #include "sha256.hpp"
 #include "transcript_dev.hpp"
 
@@ -164,9 +165,10 @@ level1_kernel(const uint8_t* __restrict__ child, uint8_t* __restrict__ parent, u
 }
 
 // Finish a level of n <= 1024 digests (n a power of two >= 2) to the root in
-// one workgroup; writes every level into `out` consecutively.  ra.t: lane 0
-// then absorbs the root into the device transcript (RootAbsorb); the state is
-// staged into LDS by parallel lanes while the levels run.
+// one workgroup; writes every level into `out` consecutively.  ra.t: wave 0
+// then absorbs the root (and ra.poly_in) into the device transcript
+// (RootAbsorb, merkle_dev.hpp); the state is staged into LDS by parallel lanes
+// while the levels run.
 __global__ void __launch_bounds__(512)
 top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ out,
            RootAbsorb ra) {
@@ -179,49 +181,8 @@ top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ 
     pw[threadIdx.x] = reinterpret_cast<const uint32_t*>(ra.poly_in)[threadIdx.x];
   for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) s[i] = digest_load(level + i * 32);
   __syncthreads();
-  uint64_t off = 0;
-  while (n > 1) {
-    const uint64_t np = n / 2;
-    Sha256State r;
-    // a level with at most half a lane per thread: two lanes per node
-    const bool two = 2 * np <= blockDim.x;
-    const uint32_t node = two ? threadIdx.x >> 1 : threadIdx.x;
-    const bool active = node < np;
-    if (active) r = two ? sha2l_node(s[2 * node], s[2 * node + 1]) : sha256_node(s[2 * node], s[2 * node + 1]);
-    __syncthreads();
-    if (active && (!two || (threadIdx.x & 1) == 0)) {
-      s[node] = r;
-      digest_store(out + (off + node) * 32, r);
-    }
-    __syncthreads();
-    off += np;
-    n = np;
-  }
-  if (ra.t && threadIdx.x < 64) {  // s[0] is the root (memory bytes = bswap of the words)
-    // wave 0 runs the transcript step on a lane pair (dsha2l_step)
-    uint32_t w[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = bswap32(s[0].h[i]);
-    if (ra.poly_in) {
-      uint32_t v[16];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        v[i] = w[i];
-        v[8 + i] = pw[i];
-      }
-      dsha2l_step<16>(ts, v, stage, ra.r_out);
-    } else {
-      dsha2l_step<8>(ts, w, stage, ra.r_out);
-    }
-    if (threadIdx.x == 0) {
-      *ra.t = ts;
-      if (ra.copy_out) {
-        uint4* q = reinterpret_cast<uint4*>(ra.copy_out);
-        q[0] = make_uint4(w[0], w[1], w[2], w[3]);
-        q[1] = make_uint4(w[4], w[5], w[6], w[7]);
-      }
-    }
-  }
+  lds_tree_levels(s, n, out);
+  root_transcript(s[0], ts, stage, ra.poly_in ? pw : nullptr, ra);
 }
 
 // The latency-bound tail of a tree (levels of <= kTailLevel digests, ~one

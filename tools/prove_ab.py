@@ -21,7 +21,7 @@ def load(path):
     return lib
 
 
-for rep in range(2):
+for rep in range(3):
     for path in sys.argv[1:]:
         lib = load(path)
         h = ctypes.c_void_p()
