@@ -38,3 +38,60 @@ def test_watchdog_silent_on_other_ranks():
     p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
                        timeout=60)
     assert p.returncode == 0 and p.stdout.strip() == ""
+
+
+def test_sharded_phases_split_and_bandwidth():
+    """The N > 1 line's phase split (bench.sharded_phases): local NTT = its
+    passes summed, all-to-all GB/s = (P-1)/P of the 16 x 2^log_n-byte shard
+    per all-to-all duration."""
+    import bench
+
+    k = {"ntt_pass<8,0,0>": {"avg_ms": 0.2, "launches": 3},
+         "ntt_pass<8,1,0>": {"avg_ms": 0.15, "launches": 3},
+         "ntt_pass<8,2,0>": {"avg_ms": 0.1, "launches": 3},
+         "ntt_all_to_all": {"avg_ms": 0.5, "launches": 3},
+         "shard_dft<3,0>": {"avg_ms": 0.05, "launches": 3}}
+    ph = bench.sharded_phases(k, 24, 3, 3)
+    assert abs(ph["local_ntt_ms"] - 0.45) < 1e-12
+    assert ph["shard_dft_ms"] == 0.05 and ph["all_to_all_ms"] == 0.5
+    sent = 16.0 * (1 << 24) * 7 / 8
+    assert ph["all_to_all_bytes_sent_per_rank"] == sent
+    assert abs(ph["all_to_all_gbs"] - sent / 0.5e-3 / 1e9) < 1e-6
+    assert bench.sharded_phases({}, 24, 1, 3)["all_to_all_gbs"] is None
+
+
+def test_sharded_ntt_spot_check_formula_vs_oracle():
+    """The identity bench.sharded_ntt_check relies on, in exact integers: for
+    x cyclic over P ranks (rank g holds x[g + P m]), X[j] = NTT(x)[j] =
+    sum_g gen^(j g) poly_g(gen^(j P)); and ntt_block_owner names the rank /
+    local index holding X[j] in the sharded NTT's block output layout (the
+    layout of tests/dist_spec.py, checked against the oracle there)."""
+    import random
+
+    from multilinear_amd.sharded import M, ntt_block_owner
+    from oracle import field as F
+    from oracle import ntt as ON
+
+    for log_n, log_p in ((6, 1), (8, 2), (9, 3)):
+        n, P = 1 << log_n, 1 << log_p
+        r = random.Random(log_n)
+        x = [r.randrange(M) for _ in range(n)]
+        g = F.pow_2_generator(log_n)
+        X = ON.ntt(x, g)
+        shards = [x[q::P] for q in range(P)]
+
+        def poly(c, t):
+            acc = 0
+            for v in reversed(c):
+                acc = (acc * t + v) % M
+            return acc
+
+        for j in [0, n - 1] + [r.randrange(n) for _ in range(6)]:
+            got = sum(pow(g, j * q, M) * poly(shards[q], pow(g, j * P, M)) for q in range(P)) % M
+            assert got == X[j]
+        # block layout: local l of rank q <-> global ((l >> s) << (s + p)) | (q << s) | (l mod 2^s)
+        s_ = log_n - 2 * log_p
+        for j in range(n):
+            q, l = ntt_block_owner(j, log_n, log_p)
+            assert ((l >> s_) << (s_ + log_p)) | (q << s_) | (l & ((1 << s_) - 1)) == j
+            assert 0 <= q < P and 0 <= l < n // P
