@@ -76,6 +76,10 @@ mlh_status mlh_set_ntt_plan(mlh_ctx* ctx, const uint32_t* logr, uint32_t count);
  * periods (0 restores the default 2^22).  A wait that exceeds it abandons the
  * kernel's rounds and the prove returns MLH_ERR_DEVICE. */
 mlh_status mlh_set_coop_spin_limit(mlh_ctx* ctx, uint32_t sleeps);
+/* Test hook: the PCS and batched PCS provers compute their sumcheck rounds
+ * off the transcript chain for n_vars <= max_vars (default and cap 24) and
+ * with one cooperative launch per round above it; both give the same proof. */
+mlh_status mlh_set_pcs_fused_max(mlh_ctx* ctx, uint32_t max_vars);
 mlh_status mlh_set_stream(mlh_ctx* ctx, void* hip_stream);
 mlh_status mlh_synchronize(mlh_ctx* ctx);
 const char* mlh_last_error(const mlh_ctx* ctx);

@@ -105,6 +105,7 @@ SIGNATURES = {
     "mlh_set_stream": (_I, [_P, _P]),
     "mlh_set_ntt_plan": (_I, [_P, ctypes.POINTER(ctypes.c_uint32), _U32]),
     "mlh_set_coop_spin_limit": (_I, [_P, _U32]),
+    "mlh_set_pcs_fused_max": (_I, [_P, _U32]),
     "mlh_set_table_cache_limit": (_I, [_P, ctypes.c_uint64]),
     "mlh_table_cache_bytes": (ctypes.c_uint64, [_P]),
     "mlh_synchronize": (_I, [_P]),

@@ -313,6 +313,12 @@ mlh_status mlh_set_coop_spin_limit(mlh_ctx* ctx, uint32_t sleeps) {
   return MLH_OK;
 }
 
+mlh_status mlh_set_pcs_fused_max(mlh_ctx* ctx, uint32_t max_vars) {
+  if (!ctx) return MLH_ERR_INVALID;
+  ctx->pcs_fused_max = max_vars < 24 ? max_vars : 24;
+  return MLH_OK;
+}
+
 mlh_status mlh_set_stream(mlh_ctx* ctx, void* hip_stream) {
   if (!ctx) return MLH_ERR_INVALID;
   ctx->stream = reinterpret_cast<hipStream_t>(hip_stream);
@@ -830,7 +836,7 @@ struct FriDevLoop {
 
   // batched_fold_step (batched_fri.rs:100-176): fold the fingerprinted pairs
   // with r at rp into the inner prover's first layer (or the last element).
-  mlh_status step_batched(const fe* rp, bool challenge_next) {
+  mlh_status step_batched(const fe* rp, bool challenge_next, const fe* poly_next = nullptr) {
     const uint32_t L = p->log_code;
     const uint64_t N = 1ull << L, half_n = N / 2;
     void* vals;
@@ -857,7 +863,7 @@ struct FriDevLoop {
     HIP_TRY(ctx, launch_batched_fold_leaves(codes, m, N, fr(), rp, tlo, thi,
                                             reinterpret_cast<fe*>(vals), nx.tree, ctx->stream));
     HIP_TRY(ctx, launch_merkle_levels(nx.tree, leaves, ctx->stream,
-                                      RootAbsorb{dt(), challenge_next ? r(1) : nullptr, root(0)}));
+                                      RootAbsorb{dt(), challenge_next ? r(1) : nullptr, root(0), poly_next}));
     return MLH_OK;
   }
 
@@ -1716,78 +1722,107 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
 
 // PCSProverData::fold (multilinear_pcs.rs:43-76) for n_vars <= 24, with the
 // sumcheck off the transcript chain (sumcheck.hip "PCS rounds off the
-// transcript kernel"): round k's (c1, c2) come from a one-workgroup kernel on
-// the eq-factored table once r_{k-1} exists, and the launch that writes FRI
-// root k absorbs root k, then (c1, c2)_k, and draws r_k -- the transcript
-// order of the reference (root_k | c1_k | c2_k -> r_k), one kernel per round
-// less.  Head (the first B = n - 12 variables): the 2^B corner sums of the
-// 2^n table in one pass; after r_{B-1} two fold_group_eq passes fold the
-// table to the 2^12 entries the tail rounds use.
+// transcript kernel"): round k's (c1, c2) come from a one-workgroup job on
+// the eq-factored table once r_{k-1} exists -- an extra workgroup of FRI step
+// k-1's fold launch -- and the launch that writes FRI root k absorbs root k,
+// then (c1, c2)_k, and draws r_k: the transcript order of the reference
+// (root_k | c1_k | c2_k -> r_k), with no sumcheck launch between challenges.
+// Head (the first B = n - 12 variables): the 2^B corner sums of the 2^n table
+// in one pass; after r_{B-1} two fold_group_eq passes fold the table to the
+// 2^12 entries the tail rounds use.  Shared by the PCS and the batched PCS.
+struct PcsRounds {
+  static constexpr uint32_t kMaxVars = 2 * EqSumcheck::kEqLo;
+  mlh_ctx* ctx;
+  FriDevLoop& lp;
+  EqSumcheck es;
+  PoolBuf yb;
+  const fe* evals = nullptr;
+  fe* work = nullptr;
+  fe* Y = nullptr;   // head table: the 2^B corner sums, folded in place
+  fe* wf = nullptr;  // the two fold_group_eq passes' weights
+  PcsRoundState* st = nullptr;
+  uint32_t n = 0, B = 0, a = 0;
+  PcsRounds(mlh_ctx* c, FriDevLoop& l) : ctx(c), lp(l), es(c), yb(c) {}
+
+  // after lp.layout(.., >= 5 extra slots): tables, round state (claim =
+  // claim_host, or claim_dev copied on the device), round 0's polynomial
+  mlh_status init(const fe* evals_, fe* work_, uint32_t n_, const uint8_t* host_inputs,
+                  const uint8_t* claim_host, const fe* claim_dev) {
+    evals = evals_;
+    work = work_;
+    n = n_;
+    MLH_TRY(es.init(evals, work, n, host_inputs, /*want_tail=*/true));
+    B = es.B;
+    a = es.a;
+    if (B) {
+      MLH_TRY(yb.alloc(16 * ((1ull << B) + 128)));
+      Y = yb.as<fe>();
+      wf = Y + (1ull << B);
+    }
+    uint8_t init_state[80] = {};  // (claim, c = 1, e0 = c1 = c2 = 0)
+    if (claim_host) memcpy(init_state, claim_host, 16);
+    init_state[16] = 1;
+    memcpy(ctx->pinned + kPinSlotA, init_state, 80);
+    st = reinterpret_cast<PcsRoundState*>(lp.extra());
+    HIP_TRY(ctx, hipMemcpyAsync(st, ctx->pinned + kPinSlotA, 80, hipMemcpyHostToDevice, ctx->stream));
+    if (claim_dev)
+      HIP_TRY(ctx, hipMemcpyAsync(&st->claim, claim_dev, 16, hipMemcpyDeviceToDevice, ctx->stream));
+    if (B) {
+      HIP_TRY(ctx, launch_corner_sums_lo(evals, B, a, es.lo, Y, ctx->stream));
+      HIP_TRY(ctx, launch_pcs_round(Y, Y, B, false, nullptr, nullptr, es.pts, e_of(0), st, lp.poly(0),
+                                    ctx->stream));
+    } else {
+      HIP_TRY(ctx, launch_pcs_round(evals, work, n, false, nullptr, nullptr, es.pts, e_of(0), st,
+                                    lp.poly(0), ctx->stream));
+    }
+    return MLH_OK;
+  }
+  // e of round k: H_k (head) or Hs_{k-B} (tail); 2^(h-1) entries for a table of 2^h
+  const fe* e_of(uint32_t k) const {
+    return k < B ? es.Hk(k) : es.Hs + ((1ull << a) - (1ull << (a - (k - B))));
+  }
+  // round kn (>= 1) as a job; at kn == B the table fold over the head
+  // variables is enqueued first (it needs r_0..r_{B-1})
+  mlh_status job(uint32_t kn, PcsJob* out) {
+    const uint32_t k = kn - 1;
+    PcsJob j{nullptr, work, 0, 1, lp.r(k), es.pts + k, es.pts + kn, e_of(kn), st, lp.poly(kn)};
+    if (kn < B) {  // head: fold Y with r_k
+      j.src = Y;
+      j.dst = Y;
+      j.log_h = B - kn;
+    } else if (kn == B) {  // fold the table over the B head variables; round B on it
+      const uint32_t JA = B < 6 ? B : 6, JB = B - JA;
+      uint32_t nb = 0;
+      HIP_TRY(ctx, launch_eq_weights(lp.r(0), JA, JB, wf, ctx->stream));
+      HIP_TRY(ctx, launch_fold_group_eq(evals, 1ull << n, JA, 0, lp.r(0), wf, work, nullptr, es.lo, a,
+                                        ctx->partials, ctx->stream, &nb));
+      if (JB)
+        HIP_TRY(ctx, launch_fold_group_eq(work, 1ull << (n - JA), JB, 0, lp.r(JA), wf + 64, work,
+                                          nullptr, es.lo, a, ctx->partials, ctx->stream, &nb));
+      j.src = work;
+      j.log_h = a;
+      j.fold = 0;
+    } else {  // tail: fold with r_k (the first tail fold of B = 0 reads the evaluations)
+      j.src = (B == 0 && kn == 1) ? evals : work;
+      j.log_h = n - kn;
+    }
+    *out = j;
+    return MLH_OK;
+  }
+};
+
 static mlh_status pcs_rounds_fused(mlh_ctx* ctx, FriDevLoop& lp, const fe* evals, fe* work,
                                    uint32_t n, const uint8_t* host_inputs, const uint8_t output[16],
                                    const void* code, uint32_t log_domain, mlh_transcript* tr) {
-  EqSumcheck es(ctx);  // points, c, lo, head suffix tables H, tail suffix tables Hs
-  MLH_TRY(es.init(evals, work, n, host_inputs, /*want_tail=*/true));
-  const uint32_t B = es.B, a = es.a;
-  PoolBuf yb(ctx);
-  fe* Y = nullptr;  // head table: the 2^B corner sums, folded in place
-  fe* wf = nullptr;
-  if (B) {
-    MLH_TRY(yb.alloc(16 * ((1ull << B) + 128)));
-    Y = yb.as<fe>();
-    wf = Y + (1ull << B);
-  }
-  // e of round k: H_k (head) or Hs_{k-B} (tail); 2^(h-1) entries for a table of 2^h
-  auto e_of = [&](uint32_t k) -> const fe* {
-    return k < B ? es.Hk(k) : es.Hs + ((1ull << a) - (1ull << (a - (k - B))));
-  };
-  // round state (claim, c, e0, c1, c2) in the loop's scratch: claim = output, c = 1
-  struct {
-    uint8_t b[80];
-  } init_state{};
-  memcpy(init_state.b, output, 16);
-  init_state.b[16] = 1;
-  memcpy(ctx->pinned + kPinSlotA, init_state.b, 80);
   MLH_TRY(lp.layout(log_domain, tr, 5));
-  PcsRoundState* st = reinterpret_cast<PcsRoundState*>(lp.extra());
-  HIP_TRY(ctx, hipMemcpyAsync(st, ctx->pinned + kPinSlotA, 80, hipMemcpyHostToDevice, ctx->stream));
-  // round 0's polynomial, then FRI init: root 0 | (c1, c2)_0 -> r_0
-  if (B) {
-    HIP_TRY(ctx, launch_corner_sums_lo(evals, B, a, es.lo, Y, ctx->stream));
-    HIP_TRY(ctx, launch_pcs_round(Y, Y, B, false, nullptr, nullptr, es.pts, e_of(0), st, lp.poly(0),
-                                  ctx->stream));
-  } else {
-    HIP_TRY(ctx, launch_pcs_round(evals, work, n, false, nullptr, nullptr, es.pts, e_of(0), st,
-                                  lp.poly(0), ctx->stream));
-  }
+  PcsRounds pr(ctx, lp);
+  MLH_TRY(pr.init(evals, work, n, host_inputs, output, nullptr));
+  // FRI init: root 0 | (c1, c2)_0 -> r_0
   MLH_TRY(lp.init_after_layout(code, log_domain, true, lp.poly(0)));
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t kn = k + 1;  // the round whose polynomial follows r_k
     PcsJob job{};
-    if (kn < n) {  // round kn: run by an extra workgroup of FRI step k's fold launch
-      job = PcsJob{nullptr, work, 0, 1, lp.r(k), es.pts + k, es.pts + kn, e_of(kn),
-                   st, lp.poly(kn)};
-      if (kn < B) {  // head: fold Y with r_k
-        job.src = Y;
-        job.dst = Y;
-        job.log_h = B - kn;
-      } else if (kn == B) {  // fold the table over the B head variables first; round B on it
-        const uint32_t JA = B < 6 ? B : 6, JB = B - JA;
-        uint32_t nb = 0;
-        HIP_TRY(ctx, launch_eq_weights(lp.r(0), JA, JB, wf, ctx->stream));
-        HIP_TRY(ctx, launch_fold_group_eq(evals, 1ull << n, JA, 0, lp.r(0), wf, work, nullptr, es.lo, a,
-                                          ctx->partials, ctx->stream, &nb));
-        if (JB)
-          HIP_TRY(ctx, launch_fold_group_eq(work, 1ull << (n - JA), JB, 0, lp.r(JA), wf + 64, work,
-                                            nullptr, es.lo, a, ctx->partials, ctx->stream, &nb));
-        job.src = work;
-        job.log_h = a;
-        job.fold = 0;
-      } else {  // tail: fold with r_k (the first tail fold of B = 0 reads the evaluations)
-        job.src = (B == 0 && kn == 1) ? evals : work;
-        job.log_h = n - kn;
-      }
-    }
+    if (kn < n) MLH_TRY(pr.job(kn, &job));
     MLH_TRY(lp.step(k, lp.r(k), kn < n, kn < n ? lp.poly(kn) : nullptr, kn < n ? &job : nullptr));
   }
   return MLH_OK;
@@ -1821,7 +1856,7 @@ mlh_status mlh_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n_vars,
   fp->log_code = log_domain;
   FriDevLoop lp(ctx, fp.get());
   device_arm(ctx);
-  if (n_vars <= 2 * EqSumcheck::kEqLo) {
+  if (n_vars <= ctx->pcs_fused_max) {
     MLH_TRY(pcs_rounds_fused(ctx, lp, reinterpret_cast<const fe*>(dev_evals), matrix.as<fe>(),
                              n_vars, host_inputs, output, code.p, log_domain, tr));
   } else {
@@ -2058,27 +2093,50 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   fp->log_code = log_domain;
   FriDevLoop lp(ctx, fp.get());
   device_arm(ctx);
-  MLH_TRY(lp.init_batched(codes.as<fe>(), num_polys, log_domain, tr, false));
+  const bool fused = n_vars <= ctx->pcs_fused_max;
+  MLH_TRY(lp.init_batched(codes.as<fe>(), num_polys, log_domain, tr, false, fused ? 5 : 0));
   // fingerprinted MLE + eq table; previous_sum = fingerprint(fr, outputs)
   HIP_TRY(ctx, launch_fingerprint(reinterpret_cast<const fe*>(dev_evals), num_polys, n, lp.fr(),
                                   matrix.as<fe>(), ctx->stream));
-  EqSumcheck es(ctx);  // delta = eq(inputs), factored
-  MLH_TRY(es.init(matrix.as<fe>(), nullptr, n_vars, inputs));
   {
     std::vector<uint8_t> ob(outputs, outputs + 16ull * num_polys);
     HIP_TRY(ctx, hipMemcpyAsync(outs.p, ob.data(), ob.size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // ob is pageable and goes out of scope
   }
   HIP_TRY(ctx, launch_fingerprint_scalar(outs.as<fe>(), num_polys, lp.fr(), lp.prev(), ctx->stream));
-  uint32_t np = 0;
-  MLH_TRY(es.first_sums(&np));
-  for (uint32_t k = 0; k < n_vars; ++k) {  // fold (batched_pcs.rs:80-125)
-    MLH_TRY(es.round(k, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k)));
-    MLH_TRY(es.fold(k, lp.r(k), &np));
-    if (k == 0)
-      MLH_TRY(lp.step_batched(lp.r(0), false));
-    else
-      MLH_TRY(lp.step(k, lp.r(k), false));
+  if (fused) {  // (batched_pcs.rs:80-125) the PCS rounds off the transcript chain (PcsRounds)
+    PcsRounds pr(ctx, lp);
+    fe* mt = matrix.as<fe>();  // the fingerprinted table is ours: its folds run in place
+    MLH_TRY(pr.init(mt, mt, n_vars, inputs, nullptr, lp.prev()));
+    HIP_TRY(ctx, launch_transcript_absorb(lp.dt(), reinterpret_cast<const uint8_t*>(lp.poly(0)), 32,
+                                          lp.r(0), ctx->stream));  // (c1, c2)_0 -> r_0
+    for (uint32_t k = 0; k < n_vars; ++k) {
+      const uint32_t kn = k + 1;
+      PcsJob job{};
+      if (kn < n_vars) MLH_TRY(pr.job(kn, &job));
+      if (k == 0) {  // the batched step: round 1 as its own launch before its tree's root absorb
+        if (kn < n_vars)
+          HIP_TRY(ctx, launch_pcs_round(job.src, job.dst, job.log_h, job.fold != 0, job.r_prev, job.p_prev,
+                                        job.p_k, job.e, job.st, job.poly_out, ctx->stream));
+        MLH_TRY(lp.step_batched(lp.r(0), kn < n_vars, kn < n_vars ? lp.poly(1) : nullptr));
+      } else {
+        MLH_TRY(lp.step(k, lp.r(k), kn < n_vars, kn < n_vars ? lp.poly(kn) : nullptr,
+                        kn < n_vars ? &job : nullptr));
+      }
+    }
+  } else {
+    EqSumcheck es(ctx);  // delta = eq(inputs), factored
+    MLH_TRY(es.init(matrix.as<fe>(), nullptr, n_vars, inputs));
+    uint32_t np = 0;
+    MLH_TRY(es.first_sums(&np));
+    for (uint32_t k = 0; k < n_vars; ++k) {  // fold (batched_pcs.rs:80-125)
+      MLH_TRY(es.round(k, np, lp.prev(), lp.dt(), lp.poly(k), lp.r(k)));
+      MLH_TRY(es.fold(k, lp.r(k), &np));
+      if (k == 0)
+        MLH_TRY(lp.step_batched(lp.r(0), false));
+      else
+        MLH_TRY(lp.step(k, lp.r(k), false));
+    }
   }
   MLH_TRY(lp.finish(32ull * n_vars));
   // host transcript replay

@@ -66,6 +66,7 @@ struct mlh_ctx {
   // out).  Cleared before, read after each prove's final sync (device_check).
   volatile uint32_t* dev_status = nullptr;
   uint32_t coop_spin = 0;  // cooperative kernels' wait limit in sleeps (0: default)
+  uint32_t pcs_fused_max = 24;  // PCS provers: rounds off the transcript chain up to this many vars
   uint8_t* qstage = nullptr;          // pinned staging of query phases (grow-only)
   size_t qstage_bytes = 0;
   fe* ntt_scratch = nullptr;          // NTT ping-pong buffer (grow-only)

@@ -3,7 +3,8 @@
 * A cooperative sumcheck kernel whose LDS wait times out (forced here with a
   spin limit of one sleep, mlh_set_coop_spin_limit) makes the prove return
   MLH_ERR_DEVICE instead of MLH_OK with wrong round polynomials; the next
-  prove on the same context, at the default limit, is bit-exact again.
+  prove on the same context, at the default limit, is bit-exact again.  (The
+  PCS provers no longer run a cooperative kernel at n <= 24.)
   (reference: sumcheck.rs:188-199, transcript.rs:23-38.)
 * mlh_gen_pows_verify compares every entry of a host gen_pows table with
   gen_pows[1]^i on the device: the reference's pow_2_generator_powers passes,
@@ -79,11 +80,11 @@ def test_sumcheck_spin_timeout_is_an_error(n):
     assert polys == want_polys and rs == want_rs and tr.random() == otr.random()
 
 
-def test_pcs_spin_timeout_is_an_error():
-    """The batched PCS prove's one-round cooperative launches
-    (sumcheck_group_kernel) report a timeout the same way.  The plain PCS
-    prove (n <= 24) runs no cooperative kernel: at the same limit it is
-    unaffected and its proof verifies."""
+def test_pcs_provers_run_no_cooperative_kernel():
+    """The PCS and batched PCS provers (n <= 24) compute their rounds off the
+    transcript chain with no cooperative kernel, so a spin limit of one sleep
+    does not touch them: both proofs verify (the cooperative sumcheck above
+    reports it)."""
     from multilinear_amd.batched import BatchedPCSProof
 
     n, m = 13, 2
@@ -93,13 +94,10 @@ def test_pcs_spin_timeout_is_an_error():
     outs = [OPL.mle_evaluate(p, pts) for p in polys]
     evd = D.to_device(D.ints_to_limbs([v for p in polys for v in p]))
     with spin_limit(1):
-        with pytest.raises(_lib.MlhError) as ei:
-            BatchedPCSProof.prove(pts, outs, evd, Transcript())
-        assert ei.value.status == _lib.MLH_ERR_DEVICE
+        got = BatchedPCSProof.prove(pts, outs, evd, Transcript())
+        assert got.verify(Transcript())
         pf = MP.PCSProof.prove(pts, outs[0], evd[: 1 << n], Transcript())
         assert pf.verify(Transcript())
-    got = BatchedPCSProof.prove(pts, outs, evd, Transcript())
-    assert got.verify(Transcript())
 
 
 def _verify(table):
