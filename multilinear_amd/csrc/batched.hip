@@ -108,10 +108,10 @@ fingerprint_kernel(const fe* __restrict__ polys, uint32_t m, uint64_t n,
 // 207-224, Merkle::batch_open): record q at out + q * qbytes.
 __global__ void batch_query_kernel(const fe* __restrict__ codes, uint32_t m, uint64_t N,
                                    const uint8_t* __restrict__ tree,
-                                   const uint64_t* __restrict__ idx, uint64_t qbytes,
+                                   const QueryIdx idx, uint64_t qbytes,
                                    uint8_t* __restrict__ out) {
   const uint32_t qi = blockIdx.x;
-  const uint64_t h = N / 2, i = idx[qi];
+  const uint64_t h = N / 2, i = idx.v[qi];
   uint8_t* rec = out + qi * qbytes;
   for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
     fe_store(reinterpret_cast<fe*>(rec + 32ull * j), fe_load(codes + (uint64_t)j * N + i));
@@ -166,9 +166,10 @@ hipError_t launch_fingerprint_scalar(const fe* vals, uint32_t m, const fe* fr, f
 }
 
 hipError_t launch_batch_queries(const fe* codes, uint32_t m, uint64_t N, const uint8_t* tree,
-                                const uint64_t* idx, uint32_t nq, uint64_t qbytes, uint8_t* out,
+                                const QueryIdx& idx, uint32_t nq, uint64_t qbytes, uint8_t* out,
                                 hipStream_t st) {
   if (nq == 0) return hipSuccess;
+  if (nq > 128) return hipErrorInvalidValue;
   hipLaunchKernelGGL(batch_query_kernel, dim3(nq), dim3(64), 0, st, codes, m, N, tree, idx, qbytes,
                      out);
   return hipGetLastError();

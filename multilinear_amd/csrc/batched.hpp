@@ -7,6 +7,12 @@
 
 namespace mlh {
 
+// A query phase's indices, passed by value in the kernel arguments (no
+// host-to-device copy on the proof's critical path).
+struct QueryIdx {
+  uint64_t v[128];  // MLH_NUM_QUERIES
+};
+
 hipError_t launch_batch_pairs_leaves(const fe* codes, uint32_t m, uint64_t N, uint8_t* leaves,
                                      hipStream_t st);
 // fr, r: device pointers; leaves may be null (final fold to two values)
@@ -18,7 +24,7 @@ hipError_t launch_fingerprint(const fe* polys, uint32_t m, uint64_t n, const fe*
 hipError_t launch_fingerprint_scalar(const fe* vals, uint32_t m, const fe* fr, fe* out,
                                      hipStream_t st);
 hipError_t launch_batch_queries(const fe* codes, uint32_t m, uint64_t N, const uint8_t* tree,
-                                const uint64_t* idx, uint32_t nq, uint64_t qbytes, uint8_t* out,
+                                const QueryIdx& idx, uint32_t nq, uint64_t qbytes, uint8_t* out,
                                 hipStream_t st);
 
 }  // namespace mlh

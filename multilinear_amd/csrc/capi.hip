@@ -1038,29 +1038,40 @@ struct QueryTree {
   const uint8_t* tree;
   uint32_t log_n;  // layer values
 };
+// The layer table travels in the kernel arguments (up to 40 layers, ~1 KB)
+// with, for a proof's 128 queries, the indices (1 KB): the query phase is then
+// one launch and one D2H copy, no host-to-device copies.
+constexpr uint32_t kMaxQueryTrees = 40;
+struct QueryTrees {
+  QueryTree t[kMaxQueryTrees];
+  uint32_t n;
+};
+static_assert(MLH_NUM_QUERIES == 128, "QueryIdx holds 128 indices");
+static_assert(sizeof(QueryTrees) + sizeof(mlh::QueryIdx) + 64 <= 4096, "kernel argument budget");
 
-__global__ void gather_queries_kernel(const QueryTree* __restrict__ trees, uint32_t ntrees,
-                                      const uint64_t* __restrict__ indices, uint32_t nq,
+// d_idx: device indices (openings of more than 128 queries), else idx.v
+__global__ void gather_queries_kernel(const QueryTrees trees, const mlh::QueryIdx idx,
+                                      const uint64_t* __restrict__ d_idx, uint32_t nq,
                                       uint64_t qbytes, uint64_t base, uint8_t* __restrict__ out) {
   const uint32_t q = blockIdx.x;
   if (q >= nq) return;
+  const uint64_t iq = d_idx ? d_idx[q] : idx.v[q];
   // record offsets per tree
   uint64_t off = base;
-  for (uint32_t t = 0; t < ntrees; ++t) {
-    const QueryTree T = trees[t];
+  for (uint32_t t = 0; t < trees.n; ++t) {
+    const QueryTree T = trees.t[t];
     const uint64_t half = 1ull << (T.log_n - 1);  // leaves
-    const uint64_t idx = indices[q] % half;        // fri/mod.rs:169-170
+    const uint64_t i = iq % half;                   // fri/mod.rs:169-170
     const uint32_t depth = T.log_n - 1;
     uint8_t* rec = out + q * qbytes + off;
     if (threadIdx.x == 0) {
-      fe_store(reinterpret_cast<fe*>(rec), fe_load(T.values + idx));
-      fe_store(reinterpret_cast<fe*>(rec + 16), fe_load(T.values + idx + half));
+      fe_store(reinterpret_cast<fe*>(rec), fe_load(T.values + i));
+      fe_store(reinterpret_cast<fe*>(rec + 16), fe_load(T.values + i + half));
     }
-    // siblings: level l node (idx >> l) ^ 1, level l starts at sum_{i<l} half>>i
+    // siblings: level l node (i >> l) ^ 1, level l starts at sum_{j<l} half>>j
     for (uint32_t l = threadIdx.x; l < depth; l += blockDim.x) {
-      uint64_t lvl_off = 0;
-      for (uint32_t i = 0; i < l; ++i) lvl_off += half >> i;
-      const uint64_t sib = ((idx >> l) ^ 1ull);
+      const uint64_t lvl_off = 2 * half - (2 * half >> l);
+      const uint64_t sib = ((i >> l) ^ 1ull);
       const uint4* src = reinterpret_cast<const uint4*>(T.tree + (lvl_off + sib) * 32);
       uint4* dst = reinterpret_cast<uint4*>(rec + 32 + (uint64_t)l * 32);
       dst[0] = src[0];
@@ -1070,11 +1081,10 @@ __global__ void gather_queries_kernel(const QueryTree* __restrict__ trees, uint3
   }
 }
 
-// Launch the per-tree gathers of p's layers into device records (qbytes
-// each, this part starting at byte `base` of a record).
-// Pinned host staging for a query phase (indices up, tree table up, records
-// down): pageable copies of these cost ~0.1 ms each on the critical path.
-// Grow-only; a caller's stream sync ends every use before the next one.
+// Pinned host staging for a query phase: the gather kernels write the
+// records straight into it (zero-copy over PCIe, ~1.3 MB for a 2^25 code: no
+// device buffer, no copy launch), and it holds indices beyond 128.  Grow-only;
+// a caller's stream sync ends every use before the next one.
 static mlh_status query_stage(mlh_ctx* ctx, size_t bytes, uint8_t** out) {
   if (bytes > ctx->qstage_bytes) {
     if (ctx->qstage) HIP_TRY(ctx, hipHostFree(ctx->qstage));
@@ -1089,20 +1099,23 @@ static mlh_status query_stage(mlh_ctx* ctx, size_t bytes, uint8_t** out) {
   return MLH_OK;
 }
 
-// qt_stage: pinned host space for the tree table (layers.size() entries)
-static mlh_status gather_queries_dev(mlh_ctx* ctx, const mlh_fri_prover* p, const uint64_t* d_idx,
-                                     uint32_t nq, uint64_t qbytes, uint64_t base, uint8_t* d_out,
-                                     PoolBuf& dtrees, uint8_t* qt_stage) {
+// Launch the per-tree gathers of p's layers into records at d_out (qbytes
+// each, this part starting at byte `base` of a record; device or pinned host
+// memory); indices in idx.v, or
+// at d_idx (device) when nq > 128.
+static mlh_status gather_queries_dev(mlh_ctx* ctx, const mlh_fri_prover* p, const mlh::QueryIdx& idx,
+                                     const uint64_t* d_idx, uint32_t nq, uint64_t qbytes,
+                                     uint64_t base, uint8_t* d_out) {
   const uint32_t nt = (uint32_t)p->layers.size();
   if (nt == 0 || nq == 0) return MLH_OK;
-  QueryTree* qt = reinterpret_cast<QueryTree*>(qt_stage);
+  if (nt > kMaxQueryTrees) return fail(ctx, MLH_ERR_INVALID, "more than 40 FRI layers");
+  if (nq > MLH_NUM_QUERIES && !d_idx) return fail(ctx, MLH_ERR_INVALID, "query indices not on the device");
+  QueryTrees qt;
+  qt.n = nt;
   for (uint32_t t = 0; t < nt; ++t)
-    qt[t] = QueryTree{p->layers[t].values, p->layers[t].tree, p->layers[t].log_n};
-  MLH_TRY(dtrees.alloc(nt * sizeof(QueryTree)));
-  HIP_TRY(ctx, hipMemcpyAsync(dtrees.p, qt, nt * sizeof(QueryTree), hipMemcpyHostToDevice,
-                              ctx->stream));
-  hipLaunchKernelGGL(gather_queries_kernel, dim3(nq), dim3(64), 0, ctx->stream,
-                     dtrees.as<QueryTree>(), nt, d_idx, nq, qbytes, base, d_out);
+    qt.t[t] = QueryTree{p->layers[t].values, p->layers[t].tree, p->layers[t].log_n};
+  hipLaunchKernelGGL(gather_queries_kernel, dim3(nq), dim3(64), 0, ctx->stream, qt, idx,
+                     nq > MLH_NUM_QUERIES ? d_idx : nullptr, nq, qbytes, base, d_out);
   HIP_TRY(ctx, hipGetLastError());
   return MLH_OK;
 }
@@ -1110,18 +1123,21 @@ static mlh_status gather_queries_dev(mlh_ctx* ctx, const mlh_fri_prover* p, cons
 static mlh_status gather_queries(mlh_ctx* ctx, const mlh_fri_prover* p, const uint64_t* idx,
                                  uint32_t nq, uint8_t* host_out) {
   const uint64_t qbytes = mlh_fri_query_bytes(p->log_code);
-  const size_t off_qt = 8ull * nq, off_out = off_qt + sizeof(QueryTree) * (p->layers.size() + 1);
+  const size_t off_out = nq > MLH_NUM_QUERIES ? 8ull * nq : 0;
   uint8_t* h;
   MLH_TRY(query_stage(ctx, off_out + nq * qbytes, &h));
-  memcpy(h, idx, 8ull * nq);
-  PoolBuf dtrees(ctx), didx(ctx), dout(ctx);
-  MLH_TRY(didx.alloc(nq * sizeof(uint64_t)));
-  MLH_TRY(dout.alloc(nq * qbytes));
-  HIP_TRY(ctx, hipMemcpyAsync(didx.p, h, nq * sizeof(uint64_t), hipMemcpyHostToDevice,
-                              ctx->stream));
-  MLH_TRY(gather_queries_dev(ctx, p, didx.as<uint64_t>(), nq, qbytes, 0, dout.as<uint8_t>(), dtrees,
-                             h + off_qt));
-  HIP_TRY(ctx, hipMemcpyAsync(h + off_out, dout.p, nq * qbytes, hipMemcpyDeviceToHost, ctx->stream));
+  mlh::QueryIdx qi;
+  memset(&qi, 0, sizeof(qi));
+  PoolBuf didx(ctx);
+  if (nq > MLH_NUM_QUERIES) {
+    memcpy(h, idx, 8ull * nq);
+    MLH_TRY(didx.alloc(nq * sizeof(uint64_t)));
+    HIP_TRY(ctx, hipMemcpyAsync(didx.p, h, nq * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                ctx->stream));
+  } else {
+    memcpy(qi.v, idx, 8ull * nq);
+  }
+  MLH_TRY(gather_queries_dev(ctx, p, qi, didx.as<uint64_t>(), nq, qbytes, 0, h + off_out));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   memcpy(host_out, h + off_out, nq * qbytes);
   return MLH_OK;
@@ -2005,23 +2021,16 @@ static mlh_status batched_queries(mlh_ctx* ctx, FriDevLoop& lp, mlh_transcript* 
   if (pf->commitments) mlh_fri_prover_roots(lp.p, pf->commitments);
   if (!pf->queries) return MLH_OK;
   const uint64_t qbytes = mlh_batched_fri_query_bytes(L, m);
-  const size_t off_qt = 8ull * MLH_NUM_QUERIES,
-               off_out = off_qt + sizeof(QueryTree) * (lp.p->layers.size() + 1);
   uint8_t* h;
-  MLH_TRY(query_stage(ctx, off_out + MLH_NUM_QUERIES * qbytes, &h));
-  memcpy(h, idx.data(), 8ull * MLH_NUM_QUERIES);
-  PoolBuf didx(ctx), dout(ctx), dtrees(ctx);
-  MLH_TRY(didx.alloc(MLH_NUM_QUERIES * sizeof(uint64_t)));
-  MLH_TRY(dout.alloc(MLH_NUM_QUERIES * qbytes));
-  HIP_TRY(ctx, hipMemcpyAsync(didx.p, h, MLH_NUM_QUERIES * 8, hipMemcpyHostToDevice, ctx->stream));
-  HIP_TRY(ctx, launch_batch_queries(lp.codes, m, N, lp.btree.as<uint8_t>(), didx.as<uint64_t>(),
-                                    MLH_NUM_QUERIES, qbytes, dout.as<uint8_t>(), ctx->stream));
-  MLH_TRY(gather_queries_dev(ctx, lp.p, didx.as<uint64_t>(), MLH_NUM_QUERIES, qbytes,
-                             32ull * m + 32ull * (L - 1), dout.as<uint8_t>(), dtrees, h + off_qt));
-  HIP_TRY(ctx, hipMemcpyAsync(h + off_out, dout.p, MLH_NUM_QUERIES * qbytes,
-                              hipMemcpyDeviceToHost, ctx->stream));
+  MLH_TRY(query_stage(ctx, MLH_NUM_QUERIES * qbytes, &h));
+  mlh::QueryIdx qi;
+  memcpy(qi.v, idx.data(), 8ull * MLH_NUM_QUERIES);
+  HIP_TRY(ctx, launch_batch_queries(lp.codes, m, N, lp.btree.as<uint8_t>(), qi, MLH_NUM_QUERIES,
+                                    qbytes, h, ctx->stream));
+  MLH_TRY(gather_queries_dev(ctx, lp.p, qi, nullptr, MLH_NUM_QUERIES, qbytes,
+                             32ull * m + 32ull * (L - 1), h));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  memcpy(pf->queries, h + off_out, MLH_NUM_QUERIES * qbytes);
+  memcpy(pf->queries, h, MLH_NUM_QUERIES * qbytes);
   return MLH_OK;
 }
 
