@@ -109,6 +109,18 @@ class FriProverData:
         check(lib().mlh_fri_prover_open_query(ctx, self.h, index, buf), ctx)
         return parse_query(bytes(buf), log_code)
 
+    def open_queries(self, indices, log_code, device=0):
+        """open_query_at for many indices in one gather (any count; up to 128
+        travel in the kernel arguments, more through device memory)."""
+        ctx = context(device)
+        nb = lib().mlh_fri_query_bytes(log_code)
+        n = len(indices)
+        idx = (ctypes.c_uint64 * max(n, 1))(*indices)
+        buf = (ctypes.c_uint8 * max(nb * n, 1))()
+        check(lib().mlh_fri_prover_open_queries(ctx, self.h, idx, n, buf), ctx)
+        raw = bytes(buf)
+        return [parse_query(raw[q * nb:(q + 1) * nb], log_code) for q in range(n)]
+
 
 def parse_query(raw, log_code):
     """-> [(pair_bytes32, [sibling digests])] per tree (QueryProof.paths)."""

@@ -335,6 +335,32 @@ def test_fri_prover_step_api():
     assert [v for v, _ in q] == [v for v, _ in wq]
 
 
+@pytest.mark.parametrize("nq", [1, 5, 128, 129, 300])
+def test_fri_prover_open_queries_many(nq):
+    """mlh_fri_prover_open_queries: indices in the kernel arguments (<= 128)
+    or in device memory (> 128); duplicates and both ends of the range."""
+    log_n = 9
+    vals = rand_vals(1 << log_n, 5)
+    gp = F.pow_2_generator_powers(log_n + 1)
+    code = OF.reed_solomon(vals, gp[1])
+    opd = OF.FriProverData.fold(gp, code, OT.Transcript())
+    pd = MF.FriProverData.fold(dev(code), Transcript())
+    rng = random.Random(nq)
+    half = 1 << log_n
+    idx = [rng.randrange(half) for _ in range(nq)]
+    idx[0] = half - 1
+    if nq > 2:
+        idx[1] = 0
+        idx[2] = idx[0]
+    got = pd.open_queries(idx, log_n + 1)
+    for i, q in zip(idx, got):
+        want = opd.open_query_at(i)
+        assert [v for v, _ in q] == [v for v, _ in want]
+        assert [s for _, s in q] == [[s for s, _ in path] for _, path in want]
+    with pytest.raises(_lib.MlhError):
+        pd.open_queries(idx[:-1] + [half], log_n + 1)
+
+
 def test_fri_not_rs_code():
     """fold of a non-codeword hits the reference's "not an RS code" assert."""
     log_code = 6
