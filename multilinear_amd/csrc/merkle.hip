@@ -24,6 +24,18 @@
 
 namespace mlh {
 
+#ifdef MLH_TREE_TS
+__device__ uint64_t g_tree_ts[4][64];
+// host access for the bench (out: 4 x 64 stamps; clear before a stamped call)
+hipError_t tree_ts_read(uint64_t* out, bool clear) {
+  if (clear) {
+    static const uint64_t zero[4][64] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tree_ts), zero, sizeof(zero));
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tree_ts), sizeof(g_tree_ts));
+}
+#endif
+
 __global__ void __launch_bounds__(256)
 leaf_pairs_kernel(const fe* __restrict__ code, uint64_t half, uint8_t* __restrict__ leaves) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -175,14 +187,17 @@ top_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restrict__ 
   __shared__ Sha256State s[1024];
   __shared__ DevSha ts;
   __shared__ uint32_t stage[8], pw[8];
+  MLH_TREE_STAMP(1, 0);
   if (ra.t && threadIdx.x < sizeof(DevSha) / 4)
     reinterpret_cast<uint32_t*>(&ts)[threadIdx.x] = reinterpret_cast<const uint32_t*>(ra.t)[threadIdx.x];
   if (ra.poly_in && threadIdx.x < 8)  // (loaded with the level, not on lane 0's chain)
     pw[threadIdx.x] = reinterpret_cast<const uint32_t*>(ra.poly_in)[threadIdx.x];
   for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) s[i] = digest_load(level + i * 32);
   __syncthreads();
+  MLH_TREE_STAMP(1, 1);
   lds_tree_levels(s, n, out);
   root_transcript(s[0], ts, stage, ra.poly_in ? pw : nullptr, ra);
+  MLH_TREE_STAMP(1, 63);
 }
 
 // The latency-bound tail of a tree (levels of <= kTailLevel digests, ~one
@@ -200,10 +215,14 @@ subtree_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restric
   const uint64_t b = blockIdx.x;
   uint32_t m = blockDim.x;  // nodes of this chunk at the current level
   const uint8_t* c = level + (b * 2 * m + 2 * t) * 32;
-  Sha256State r = sha256_node(digest_load(c), digest_load(c + 32));
+  MLH_TREE_STAMP(0, 0);
+  const Sha256State c0 = digest_load(c), c1 = digest_load(c + 32);
+  MLH_TREE_STAMP(0, 1);
+  Sha256State r = sha256_node(c0, c1);
   uint64_t off = 0, lvl = n / 2;  // offset and size of the current level in out
   digest_store(out + (off + b * m + t) * 32, r);
   s[t] = r;
+  MLH_TREE_STAMP(0, 2);
   while (m > 1) {
     off += lvl;
     lvl /= 2;
@@ -219,6 +238,7 @@ subtree_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restric
       s[node] = r;
       digest_store(out + (off + b * mp + node) * 32, r);
     }
+    MLH_TREE_STAMP(0, 2 + __builtin_ctz(blockDim.x / mp));
     m = mp;
   }
 }

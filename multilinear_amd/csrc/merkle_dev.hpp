@@ -10,12 +10,31 @@
 
 namespace mlh {
 
+// Per-level s_memtime stamps of a tree tail's workgroup 0 (tools/
+// tree_tail_bench.hip builds merkle.hip with MLH_TREE_TS; off otherwise).
+#ifdef MLH_TREE_TS
+extern __device__ uint64_t g_tree_ts[4][64];
+#define MLH_TREE_STAMP(k, i)                                                  \
+  do {                                                                         \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (i) < 64) {                  \
+      g_tree_ts[k][i] = __builtin_amdgcn_s_memtime();                          \
+      g_tree_ts[(k) + 2][i] = __builtin_amdgcn_s_memrealtime();                \
+    }                                                                          \
+  } while (0)
+#else
+#define MLH_TREE_STAMP(k, i) \
+  do {                       \
+  } while (0)
+#endif
+
 // The levels above the n digests in s (shared memory, n a power of two) up to
 // the root s[0], each level written to out consecutively (level order); a
 // level with at most half a node per thread hashes each node on a lane pair
 // (sha2l_node).  Every thread of the workgroup calls it.
-__device__ __forceinline__ void lds_tree_levels(Sha256State* s, uint64_t n, uint8_t* __restrict__ out) {
+__device__ __forceinline__ void lds_tree_levels(Sha256State* s, uint64_t n, uint8_t* __restrict__ out,
+                                                int ts_k = 1) {
   uint64_t off = 0;
+  [[maybe_unused]] int lvl = 0;
   while (n > 1) {
     const uint64_t np = n / 2;
     Sha256State r;
@@ -29,6 +48,8 @@ __device__ __forceinline__ void lds_tree_levels(Sha256State* s, uint64_t n, uint
       digest_store(out + (off + node) * 32, r);
     }
     __syncthreads();
+    MLH_TREE_STAMP(ts_k, 2 + lvl);
+    ++lvl;
     off += np;
     n = np;
   }
