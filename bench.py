@@ -610,6 +610,10 @@ def main():
         result["pcs_prove_n_vars"] = log_n
         result["pcs_verified"] = bool(pcs.verify(Transcript()))
         del pcs
+        try:
+            result["reference_test_points"] = reference_test_points(lib, ctx, local, reps)
+        except Exception as e:  # keep the headline line; report the failure
+            result["reference_test_points_error"] = "%s: %s" % (type(e).__name__, e)
 
     if not args.no_extras and args.fri_log:
         try:
@@ -921,6 +925,87 @@ def config4_sharded(args, local, world, rank, barrier):
     return {"config4_sharded_eq_sumcheck_ms": _allreduce_max(dt) * 1e3,
             "config3_sharded_fri_commit_ms": commit_ms,
             "config4_layout": "sharded x%d (cyclic by low index bits)" % world}
+
+
+def reference_test_points(lib, ctx, local, reps):
+    """The reference's own benchmark!() points, same sizes and inputs, on the
+    device (its numbers are printed, never published: BASELINE.md section 1):
+    ntt/mod.rs:191-201 (2^18 NTT -> INTT, coeffs i), fri/mod.rs:365-398 (2^20
+    values i: gen_pows(21), RS, FriProof::prove, verify, bincode size),
+    multilinear_pcs.rs:210-228 (20 vars, evals 7i + 3, inputs 0..19: prove,
+    verify), batched_pcs.rs:261-306 (20 vars x 10 polys, evals (3j + 5i) % 100:
+    prove, verify).  Median of `reps` timed calls after one warm-up; device
+    calls end synchronised (the provers sync inside; the transforms here)."""
+    import numpy as np
+    import torch
+
+    from multilinear_amd import device as D
+    from multilinear_amd import fri as MF
+    from multilinear_amd import ntt as MN
+    from multilinear_amd import polynomials as MPL
+    from multilinear_amd.batched import BatchedPCSProof
+    from multilinear_amd.multilinear_pcs import PCSProof
+    from multilinear_amd.transcript import Transcript
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        out = None
+        for _ in range(max(1, reps)):
+            t0 = time.perf_counter()
+            out = fn()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        ts.sort()
+        return ts[len(ts) // 2], out
+
+    def dev_ints(vals):
+        a = np.zeros((len(vals), 4), dtype=np.uint32)
+        a[:, 0] = vals
+        return torch.from_numpy(a.view(np.int32)).to("cuda:%d" % local)
+
+    res = {}
+    # ntt/mod.rs:191-201
+    n18 = 1 << 18
+    c18 = dev_ints(np.arange(n18, dtype=np.uint32))
+    ev18, back = D.empty(n18, local), D.empty(n18, local)
+    g18 = _gen(lib, 18)
+    t_ntt, _ = timed(lambda: D.check(lib.mlh_ntt(ctx, D.ptr(c18), D.ptr(ev18), 18, g18), ctx))
+    t_intt, _ = timed(lambda: D.check(lib.mlh_intt(ctx, D.ptr(ev18), D.ptr(back), 18, g18), ctx))
+    res["ntt_intt_2_18"] = {"ntt_ms": t_ntt, "intt_ms": t_intt,
+                            "round_trip_equal": bool(torch.equal(back, c18)), "ref": "ntt/mod.rs:191-201"}
+    # fri/mod.rs:365-398
+    n20 = 1 << 20
+    vals = dev_ints(np.arange(n20, dtype=np.uint32))
+    t_gp, gp = timed(lambda: MN.pow_2_generator_powers(21, local))
+    g1 = D.fe_from_bytes(gp[1].cpu().numpy().tobytes())
+    t_rs, code = timed(lambda: MF.reed_solomon(vals, g1, local))
+    t_pf, proof = timed(lambda: MF.FriProof.prove(code, Transcript(), local))
+    t_vf, ok = timed(lambda: proof.verify())
+    res["fri_2_20"] = {"gen_pows_ms": t_gp, "reed_solomon_ms": t_rs, "prove_ms": t_pf,
+                       "verify_ms_host": t_vf, "verified": bool(ok),
+                       "proof_bytes": len(proof.to_bytes()), "ref": "fri/mod.rs:365-398"}
+    del gp, code, proof
+    # multilinear_pcs.rs:210-228
+    ev = dev_ints((7 * np.arange(n20, dtype=np.uint64) + 3).astype(np.uint32))
+    inputs = list(range(20))
+    output = MPL.evaluate(ev, inputs, local)
+    t_pp, pcs = timed(lambda: PCSProof.prove(inputs, output, ev, Transcript(), local))
+    t_pv, ok = timed(lambda: pcs.verify(Transcript()))
+    res["pcs_20_vars"] = {"prove_ms": t_pp, "verify_ms_host": t_pv, "verified": bool(ok),
+                          "ref": "multilinear_pcs.rs:210-228"}
+    del pcs, ev
+    # batched_pcs.rs:261-306
+    m = 10
+    j = np.arange(n20, dtype=np.uint64)
+    evs = dev_ints(np.concatenate([((3 * j + 5 * i) % 100).astype(np.uint32) for i in range(m)]))
+    outs = [MPL.evaluate(evs[i * n20:(i + 1) * n20], inputs, local) for i in range(m)]
+    t_bp, bpf = timed(lambda: BatchedPCSProof.prove(inputs, outs, evs, Transcript(), local))
+    t_bv, ok = timed(lambda: bpf.verify(Transcript()))
+    res["batched_pcs_20_vars_x10"] = {"prove_ms": t_bp, "verify_ms_host": t_bv, "verified": bool(ok),
+                                      "ref": "batched_pcs.rs:261-306"}
+    return res
 
 
 def config5(args, lib, ctx, local, world, rank, barrier):
