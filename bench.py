@@ -109,6 +109,35 @@ def cpu_baseline(log_n):
     }
 
 
+def cpu_baseline_fri_commit(log_n, sample_log=21):
+    """Config 3 (the metric's "FRI commit ms") on one host core: the oracle's C
+    restatement of reed_solomon (fri/mod.rs:19-28, NTT of the zero-padded
+    coefficients) and commit_rs_code + Merkle::commit (fri/mod.rs:30-55,
+    merkle_tree/mod.rs:65-85: SHA-256 per leaf and node, every layer kept) on a
+    bounded sample of 2^sample_log coefficients (~8 s of one core), scaled to
+    2^log_n: the RS part by N log N, the Merkle part by N (bench leg only)."""
+    from multilinear_amd import device as D
+    from oracle import coracle
+    from oracle import field as F
+
+    sl = min(sample_log, log_n)
+    x = D.random_limbs(1 << sl, 3)
+    g2 = F.pow_2_generator(sl + 1)
+    t0 = time.perf_counter()
+    code = coracle.reed_solomon(x, sl, g2)
+    t1 = time.perf_counter()
+    layers = coracle.merkle_commit_pairs(code, sl + 1)
+    t2 = time.perf_counter()
+    del code, layers
+    k = float(1 << (log_n - sl))
+    rs_ms = (t1 - t0) * 1e3 * k * (log_n + 1) / (sl + 1)
+    mk_ms = (t2 - t1) * 1e3 * k
+    return {"ms": rs_ms + mk_ms, "rs_ms": rs_ms, "merkle_ms": mk_ms, "cores": 1, "kind": "port",
+            "sample": "one commit of 2^%d coefficients (2^%d code, 2^%d leaves) in %.2f s, C "
+                      "restatement of the reference loops; scaled to 2^%d (RS x N log N, Merkle x N)"
+                      % (sl, sl + 1, sl, t2 - t0, log_n)}
+
+
 def cpu_baseline_all_cores(log_n):
     """OpenMP variant of the same C restatement on the host cores the box
     grants (OMP_NUM_THREADS, else os.cpu_count()); SURVEY.md 8(d)."""
@@ -649,6 +678,13 @@ def main():
         except Exception as e:  # the 1-core baseline stays the reported one
             result["cpu_baseline_all_cores"] = {"error": str(e)}
         result["vs_cpu_1core"] = value / result["cpu_baseline"]["value"]
+        if not args.no_extras and result.get("fri_commit_ms"):
+            try:
+                cf = cpu_baseline_fri_commit(log_n)
+                result["cpu_baseline_fri_commit"] = cf
+                result["fri_commit_vs_cpu_1core"] = cf["ms"] / result["fri_commit_ms"]
+            except Exception as e:
+                result["cpu_baseline_fri_commit"] = {"error": str(e)}
 
     if dist is not None:
         dist.barrier()
