@@ -274,6 +274,12 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--extras-budget-s", type=float, default=240.0,
                     help="watchdog on the secondary timings (0: off)")
+    ap.add_argument("--headline-budget-s", type=float, default=180.0,
+                    help="N > 1: watchdog from before the first collective to the headline "
+                         "line (0: off); on expiry rank 0 prints a diagnostic line and every "
+                         "rank exits non-zero")
+    ap.add_argument("--preflight-bytes", type=int, default=1 << 20,
+                    help="N > 1: total bytes of the pre-flight all-to-all (checked pattern)")
     ap.add_argument("--fri-log", type=int, default=28, help="config 5 codeword size (log2)")
     ap.add_argument("--mode", choices=["replicas", "sharded"], default="sharded",
                     help="N > 1 headline step: one N*2^24 transform sharded with an all-to-all "
@@ -291,9 +297,15 @@ def main():
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
+    hw = None
     if world > 1:
         import torch.distributed as dist
 
+        # armed before the first collective (init_process_group with device_id
+        # connects eagerly): a stalled exchange ends the run with a line that
+        # names the phase instead of a silent kill at the driver's limit
+        hw = _HeadlineWatchdog(rank, world, args.headline_budget_s)
+        hw.phase("init_process_group")
         if BACKEND == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:  # rehearsal of the N > 1 path with several ranks on one GPU
@@ -320,8 +332,18 @@ def main():
         D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(out), log_n, gen), ctx)
 
     batch = None
+    preflight = None
     if world > 1:  # the C ABI's pipelined sharded NTT over libmlhip's RCCL communicator
-        batch = _ShardedBatch(lib, ctx, _transport(local), x, out, log_n + log_p, local)
+        hw.phase("comm_create")
+        tp = _transport(local)
+        hw.info = tp.info()
+        hw.phase("preflight")
+        preflight = run_preflight(tp, world, args.preflight_bytes, local)
+        hw.preflight = preflight
+        if not preflight["ok"]:
+            hw.fail("pre-flight all-to-all/all-gather pattern mismatch: %d words on the worst rank"
+                    % preflight["mismatches_max"])
+        batch = _ShardedBatch(lib, ctx, tp, x, out, log_n + log_p, local)
 
     def run_steps(k):
         """k headline steps, enqueued (x: this rank's shard / polynomial)."""
@@ -339,6 +361,8 @@ def main():
 
     # setup (not a step): tables, allocator, clock ramp.  The iteration count
     # is agreed over ranks so the sharded step's collectives stay matched.
+    if hw:
+        hw.phase("first_step")
     run_steps(1)
     barrier()
     t_one = time.perf_counter()
@@ -347,10 +371,16 @@ def main():
     iters = int(args.spinup_s / max(time.perf_counter() - t_one, 1e-5)) + 1
     if dist is not None:
         iters = int(_allreduce_max(iters))
+    if hw:
+        hw.phase("spinup")
     run_steps(min(iters, 5000))
     barrier()
+    if hw:
+        hw.phase("warmup")
     run_steps(args.warmup)
     barrier()
+    if hw:
+        hw.phase("timed_steps")
     lib.mlh_profile_reset(ctx)
     lib.mlh_profile_enable(ctx, max(1, args.prof_every))
     t0 = time.perf_counter()
@@ -363,6 +393,8 @@ def main():
         elapsed = _allreduce_max(elapsed)
     barrier()
 
+    if hw:
+        hw.phase("headline_checks")
     # dominant kernel timing (HIP events on the launch stream, timed region)
     kernels = {}
     labels = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(4)
@@ -410,7 +442,10 @@ def main():
             "parallelism": "single GPU" if world == 1 else
                            ("replicas x%d (independent 2^%d polynomial per GPU)" % (world, log_n)
                             if not sharded else
-                            "sharded x%d (four-step NTT, all-to-all over xGMI)" % world),
+                            ("sharded x%d (four-step NTT, RCCL all-to-all over xGMI)" % world
+                             if BACKEND == "nccl" else
+                             "sharded x%d (four-step NTT, host-staged %s all-to-all; rehearsal, "
+                             "not xGMI)" % (world, BACKEND))),
         },
         "ntt_hbm_frac": (32.0 * N / (ms_per_step * 1e-3) / 1e9) / HBM_PEAK_GBS,
         "roofline": {
@@ -458,6 +493,10 @@ def main():
                 result["sharded_ntt_verified"] = False
                 result["sharded_ntt_check_error"] = "%s: %s" % (type(e).__name__, e)
 
+    if preflight is not None:
+        result["preflight"] = preflight
+    if hw:
+        hw.disarm()
     # The extras run collectives at N > 1; if one of them stalls (a rank raising
     # inside a sharded prove leaves the others waiting in RCCL), every rank's
     # watchdog prints the headline line measured above and ends the process, so
@@ -694,6 +733,86 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def run_preflight(tp, world, total_bytes, local):
+    """mlh_comm_preflight through the headline's transport: an all-to-all of
+    total_bytes (total_bytes / world per rank pair) and an all-gather, each
+    word tagged with (source, destination, position) and checked on the
+    device; the worst rank's mismatch count is agreed over ranks."""
+    from multilinear_amd import sharded as SH
+
+    per = max(4, (total_bytes // world) // 4 * 4)
+    bad, ms = SH.preflight(tp, per, local)
+    worst = int(_allreduce_max(bad))
+    return {"bytes_per_rank_pair": per, "all_to_all_bytes": per * world, "mismatches_max": worst,
+            "ok": worst == 0, "ms_rank0": ms,
+            "transport": "rccl" if BACKEND == "nccl" else "host-staged " + BACKEND}
+
+
+class _HeadlineWatchdog:
+    """N > 1 guard from before the first collective until the headline line is
+    built.  phase() records how far this rank got; if budget_s passes first (a
+    stalled init, pre-flight or exchange -- RCCL waits forever for a missing
+    peer), rank 0 prints one JSON line with the metric, "value": null,
+    "headline_error", the phase reached, the per-phase times and what RCCL
+    reported (rccl_ranks), and every rank ends with os._exit(3).  fail() does
+    the same at once for a detected error (pre-flight mismatch)."""
+
+    def __init__(self, rank, world, budget_s):
+        import threading
+
+        self.rank, self.world = rank, world
+        self.info, self.preflight = None, None
+        self._t0 = time.perf_counter()
+        self._phases = []
+        self._lock = threading.Lock()
+        self._done = False
+        self._timer = threading.Timer(budget_s, self._fire)
+        self._timer.daemon = True
+        self.budget_s = budget_s
+        if budget_s > 0:
+            self._timer.start()
+
+    def phase(self, name):
+        self._phases.append((name, round(time.perf_counter() - self._t0, 3)))
+
+    def disarm(self):
+        self._timer.cancel()
+        with self._lock:
+            self._done = True
+
+    def _line(self, error):
+        info = self.info or {}
+        return {
+            "metric": "NTT 2^24 field-elems/sec + FRI commit ms; % HBM roofline at 1/2/4/8 GPUs",
+            "value": None, "unit": "field-elems/s", "n_gpus": self.world, "higher_is_better": True,
+            "headline_error": error,
+            "phase": self._phases[-1][0] if self._phases else None,
+            "phases_started_s": dict(self._phases),
+            "comm": self.info,
+            "rccl_ranks": info.get("ranks") if info.get("transport") == "rccl" else None,
+            "preflight": self.preflight,
+        }
+
+    def _end(self, error, code):
+        with self._lock:
+            if self._done:
+                return
+            self._done = True
+        if self.rank == 0:
+            print(json.dumps(self._line(error)), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(code)
+
+    def _fire(self):
+        self._end("watchdog: phase %r did not finish within %.0f s"
+                  % (self._phases[-1][0] if self._phases else None, self.budget_s), 3)
+
+    def fail(self, error):
+        self._timer.cancel()
+        self._end(error, 4)
 
 
 class _ExtrasWatchdog:
@@ -1102,7 +1221,20 @@ def _transport(local):
         if BACKEND == "nccl":
             _TRANSPORT.append(SH.RcclComm.from_torch(device=local))
         else:
-            _TRANSPORT.append(SH.HostTransport(SH.Transport(host_staged=True), local))
+            ht = SH.HostTransport(SH.Transport(host_staged=True), local)
+            stall = os.environ.get("MLH_BENCH_TEST_STALL_A2A")
+            if stall is not None and ht.tp.rank == int(stall):
+                # test hook of the gloo rehearsal only (tests/test_bench_rehearsal_gpu.py):
+                # this rank's all-to-all never returns, as a dead RCCL peer would
+                from multilinear_amd import _lib
+
+                def hang(user, send, recv, per, stream):
+                    time.sleep(1e9)
+                    return 1
+
+                ht._hang = _lib.ALL_TO_ALL_FN(hang)
+                ht.c.all_to_all = ht._hang
+            _TRANSPORT.append(ht)
     return _TRANSPORT[0]
 
 

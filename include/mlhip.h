@@ -193,8 +193,21 @@ mlh_status mlh_fri_prover_init(mlh_ctx* ctx, const void* dev_code, uint32_t log_
 mlh_status mlh_fri_prover_init_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
                                   const uint8_t gen_pows_1[16], uint32_t log_gen_pows,
                                   mlh_transcript* tr, mlh_fri_prover** out);
+/* fold_step(&mut self, gen_pows, k, r, transcript) (fri/mod.rs:79-134).  The
+ * plain form folds with the table the prover was created with (init: the
+ * code's canonical table); _gp takes the caller's table for this step, as the
+ * reference does at every call (multilinear_pcs.rs:72, batched_pcs.rs:121,
+ * batched_fri.rs:200, fri/mod.rs:141): twiddle gen_pows[len - i 2^k] =
+ * gen_pows_1^(-(i 2^k) mod len) for a table of 2^log_gen_pows powers of a
+ * generator of that exact order (MLH_ERR_BAD_GENERATOR otherwise).  Any k is
+ * accepted while (n/2 - 1) 2^k <= len (beyond it the reference's index
+ * underflows: MLH_ERR_INVALID).  Like the reference, a step after the last
+ * element folds the last tree again and re-absorbs the element. */
 mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
                                     const uint8_t r[16], mlh_transcript* tr); /* :79-134 */
+mlh_status mlh_fri_prover_fold_step_gp(mlh_ctx* ctx, mlh_fri_prover* p, const uint8_t gen_pows_1[16],
+                                       uint32_t log_gen_pows, uint32_t k, const uint8_t r[16],
+                                       mlh_transcript* tr);
 mlh_status mlh_fri_prover_fold(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
                                mlh_transcript* tr, mlh_fri_prover** out); /* :136-145 */
 mlh_status mlh_fri_prover_fold_gp(mlh_ctx* ctx, const void* dev_code, uint32_t log_code,
@@ -500,6 +513,14 @@ mlh_status mlh_comm_transport(mlh_comm* comm, mlh_transport* out);
  * ncclCommUserRank, ncclCommCuDevice): the ranks it connected, this rank, and
  * its device -- the self-check a multi-GPU run prints. */
 mlh_status mlh_comm_info(mlh_comm* comm, uint32_t* count, uint32_t* rank, int* device);
+/* Transport pre-flight (no reference counterpart): one all-to-all of
+ * P x bytes_per_rank and one all-gather of bytes_per_rank through `tp`, each
+ * word a function of (source rank, destination rank, position), checked on the
+ * device.  *mismatches = the words this rank received wrong (0 on a sound
+ * transport); *ms (optional) = the two collectives' duration on the context
+ * stream.  Run it before the first data-path collective of a multi-GPU job. */
+mlh_status mlh_comm_preflight(mlh_ctx* ctx, const mlh_transport* tp, uint64_t bytes_per_rank,
+                              uint64_t* mismatches, float* ms);
 /* Polynomial::ntt / LagrangePolynomial::intt (ntt/mod.rs:69-173) of a 2^log_n
  * vector: forward takes the cyclic layout (2^log_n / P local elements) and
  * returns block 2^log_n / P^2; inverse != 0 the reverse.  One all-to-all. */

@@ -135,6 +135,7 @@ SIGNATURES = {
     "mlh_fri_fold": (_I, [_P, _P, _U32, _U32, _U32, _P, _P]),
     "mlh_fri_prover_init": (_I, [_P, _P, _U32, _P, ctypes.POINTER(_P)]),
     "mlh_fri_prover_fold_step": (_I, [_P, _P, _U32, _P, _P]),
+    "mlh_fri_prover_fold_step_gp": (_I, [_P, _P, _P, _U32, _U32, _P, _P]),
     "mlh_fri_prover_fold": (_I, [_P, _P, _U32, _P, ctypes.POINTER(_P)]),
     "mlh_fri_prover_init_gp": (_I, [_P, _P, _U32, _P, _U32, _P, ctypes.POINTER(_P)]),
     "mlh_fri_prover_fold_gp": (_I, [_P, _P, _U32, _P, _U32, _P, ctypes.POINTER(_P)]),
@@ -205,6 +206,8 @@ SIGNATURES = {
     "mlh_comm_destroy": (None, [_P]),
     "mlh_comm_transport": (_I, [_P, ctypes.POINTER(TransportC)]),
     "mlh_comm_info": (_I, [_P, ctypes.POINTER(_U32), ctypes.POINTER(_U32), ctypes.POINTER(ctypes.c_int)]),
+    "mlh_comm_preflight": (_I, [_P, ctypes.POINTER(TransportC), ctypes.c_uint64,
+                                ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_float)]),
     "mlh_sharded_ntt": (_I, [_P, ctypes.POINTER(TransportC), _P, _P, _U32, _P, _I]),
     "mlh_gen_pows_params": (_I, [_P, _U64, _P, ctypes.POINTER(_U32)]),
     "mlh_gen_pows_verify": (_I, [_P, _P, _U64, _P, ctypes.POINTER(_U32)]),

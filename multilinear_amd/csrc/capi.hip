@@ -715,18 +715,25 @@ mlh_status mlh_fri_prover_init_gp(mlh_ctx* ctx, const void* dev_code, uint32_t l
   return MLH_OK;
 }
 
-mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
-                                    const uint8_t r[16], mlh_transcript* tr) {
-  if (!ctx || !p || !r || !tr) return fail(ctx, MLH_ERR_INVALID, "null argument");
+}  // extern "C"
+
+// fold_step (fri/mod.rs:79-134) with the table (gen, log_gp): twiddle
+// gen_pows[len - i 2^k] = gen^(-(i 2^k) mod len).  The reference accepts any k
+// whose indices stay in the table -- (n/2 - 1) 2^k <= len, else its usize index
+// underflows (a panic, MLH_ERR_INVALID here); its callers pass k in sequence.
+static mlh_status fold_step_impl(mlh_ctx* ctx, mlh_fri_prover* p, u128 gen, uint32_t log_gp,
+                                 uint32_t k, const uint8_t r[16], mlh_transcript* tr) {
   const FriLayer& cur = p->layers.back();
   const uint32_t log_n = cur.log_n;  // n = 2 * pairs
   const uint64_t blowup = 1ull << MLH_LOG_BLOWUP;
   if ((1ull << log_n) <= blowup) return MLH_OK;  // fri/mod.rs:83-85
-  if (p->has_last) return MLH_OK;
+  // (after the last element, the reference folds its last tree again and
+  // re-absorbs the element: layers.back() is still that tree here, too)
   const uint64_t half_n = 1ull << (log_n - 1);
-  if (k + log_n != p->log_code) return fail(ctx, MLH_ERR_INVALID, "fold index k out of sequence");
+  if (k > 40 || ((half_n - 1) << k) > (1ull << log_gp))
+    return fail(ctx, MLH_ERR_INVALID, "gen_pows index len - i*2^k underflows (fri/mod.rs:106-110)");
   const fe *tlo, *thi;
-  MLH_TRY(fold_tables_g(ctx, p->gp_gen, p->log_gp, &tlo, &thi));
+  MLH_TRY(fold_tables_g(ctx, gen, log_gp, &tlo, &thi));
   const fe rr = to_fe(h_load(r));
   FriLayer nx;
   nx.log_n = log_n - 1;
@@ -736,7 +743,7 @@ mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
   nx.values = reinterpret_cast<const fe*>(vals);
   if (half_n == blowup) {  // fri/mod.rs:116-126
     HIP_TRY(ctx, launch_fri_fold(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), rr, tlo,
-                                 thi, k, 1ull << p->log_gp, ctx->stream));
+                                 thi, k, 1ull << log_gp, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, vals, 32, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     pool_free(ctx, vals);
@@ -752,12 +759,31 @@ mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
   MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
   nx.tree = reinterpret_cast<uint8_t*>(tree);
   HIP_TRY(ctx, launch_fri_fold_commit(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
-                                      nx.tree, rr, tlo, thi, k, 1ull << p->log_gp,
+                                      nx.tree, rr, tlo, thi, k, 1ull << log_gp,
                                       ctx->stream));
   MLH_TRY(read_root(ctx, nx.tree, L, nx.root));
   p->layers.push_back(nx);
   mlh_transcript_absorb(tr, p->layers.back().root, 32);
   return MLH_OK;
+}
+
+extern "C" {
+
+mlh_status mlh_fri_prover_fold_step(mlh_ctx* ctx, mlh_fri_prover* p, uint32_t k,
+                                    const uint8_t r[16], mlh_transcript* tr) {
+  if (!ctx || !p || !r || !tr) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  return fold_step_impl(ctx, p, p->gp_gen, p->log_gp, k, r, tr);
+}
+
+mlh_status mlh_fri_prover_fold_step_gp(mlh_ctx* ctx, mlh_fri_prover* p, const uint8_t gen_pows_1[16],
+                                       uint32_t log_gen_pows, uint32_t k, const uint8_t r[16],
+                                       mlh_transcript* tr) {
+  if (!ctx || !p || !gen_pows_1 || !r || !tr) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_gen_pows < 1 || log_gen_pows > 40) return fail(ctx, MLH_ERR_INVALID, "gen_pows length");
+  const u128 g = h_load(gen_pows_1);
+  if (!check_generator(g, log_gen_pows))
+    return fail(ctx, MLH_ERR_BAD_GENERATOR, "gen_pows[1] must have order exactly gen_pows.len()");
+  return fold_step_impl(ctx, p, g, log_gen_pows, k, r, tr);
 }
 
 }  // extern "C"
@@ -1084,14 +1110,19 @@ __global__ void gather_queries_kernel(const QueryTrees trees, const mlh::QueryId
 // Pinned host staging for a query phase: the gather kernels write the
 // records straight into it (zero-copy over PCIe, ~1.3 MB for a 2^25 code: no
 // device buffer, no copy launch), and it holds indices beyond 128.  Grow-only;
-// a caller's stream sync ends every use before the next one.
+// a caller's stream sync ends every use before the next one.  Allocated
+// non-coherent (explicitly; what flags 0 gives under the default
+// HIP_HOST_COHERENT=0): the kernels' writes become visible to the host only
+// at the end of the kernel, so EVERY host read of records a kernel wrote here
+// must follow a sync of the stream that ran it (each caller syncs ctx->stream
+// before copying records out).
 static mlh_status query_stage(mlh_ctx* ctx, size_t bytes, uint8_t** out) {
   if (bytes > ctx->qstage_bytes) {
     if (ctx->qstage) HIP_TRY(ctx, hipHostFree(ctx->qstage));
     ctx->qstage = nullptr;
     ctx->qstage_bytes = 0;
     void* h = nullptr;
-    HIP_TRY(ctx, hipHostMalloc(&h, bytes, 0));
+    HIP_TRY(ctx, hipHostMalloc(&h, bytes, hipHostMallocNonCoherent));
     ctx->qstage = reinterpret_cast<uint8_t*>(h);
     ctx->qstage_bytes = bytes;
   }
@@ -2094,9 +2125,12 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
     MLH_TRY(mlh_reed_solomon_brev(ctx, coeffs.p, n_vars, genb,
                                   codes.as<uint8_t>() + (uint64_t)j * N * 16));
   }
-  // init (batched_pcs.rs:36-78): absorb the claim, batched FRI init
-  for (uint32_t i = 0; i < n_vars; ++i) mlh_transcript_absorb(tr, inputs + 16 * i, 16);
-  for (uint32_t j = 0; j < num_polys; ++j) mlh_transcript_absorb(tr, outputs + 16 * j, 16);
+  // init (batched_pcs.rs:36-78): absorb the claim, batched FRI init.  The
+  // replay check is armed first: any failure from here on restores the
+  // caller's transcript to its state at entry.
+  ReplayCheck rc(ctx, tr);
+  for (uint32_t i = 0; i < n_vars; ++i) rc.absorb(inputs + 16 * i, 16);
+  for (uint32_t j = 0; j < num_polys; ++j) rc.absorb(outputs + 16 * j, 16);
   std::unique_ptr<mlh_fri_prover> fp(new mlh_fri_prover());
   fp->ctx = ctx;
   fp->log_code = log_domain;
@@ -2151,7 +2185,6 @@ mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t n
   // host transcript replay
   const uint8_t* polys = lp.host_polys();
   if (proof->sumcheck_polys) memcpy(proof->sumcheck_polys, polys, 32ull * n_vars);
-  ReplayCheck rc(ctx, tr);
   rc.absorb(lp.host_broot(), 32);
   rc.expect(lp.host_fr());
   rc.absorb(lp.host_fr(), 16);

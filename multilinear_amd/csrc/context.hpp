@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/mlhip.h"
+#include "host_transcript.hpp"
 #include "field.hpp"
 #include "host_field.hpp"
 #include "ntt.hpp"
@@ -163,7 +164,12 @@ inline mlh_status fail(mlh_ctx* ctx, mlh_status st, const std::string& msg) {
 
 // Device-side failures (MLH_ERR_DEVICE).  device_arm before a prove enqueues
 // its cooperative kernels, device_check after its final sync.
-inline void device_arm(mlh_ctx* ctx) { *ctx->dev_status = 0; }
+// The clear is enqueued on ctx->stream (not a host store), so a kernel of an
+// earlier call still running on the stream cannot set the word after it is
+// cleared, nor have a real report wiped.
+inline void device_arm(mlh_ctx* ctx) {
+  (void)hipMemsetAsync(const_cast<uint32_t*>(ctx->dev_status), 0, sizeof(uint32_t), ctx->stream);
+}
 inline mlh_status device_check(mlh_ctx* ctx) {
   const uint32_t s = *ctx->dev_status;
   if (!s) return MLH_OK;
@@ -176,12 +182,22 @@ inline mlh_status device_check(mlh_ctx* ctx) {
 // the device absorbed and, at each point where the device drew a challenge,
 // compares next_challenge() with the device's value.  Any difference -- a
 // device SHA-256 or synchronisation fault -- fails the prove (MLH_ERR_DEVICE)
-// instead of returning a proof whose challenges do not follow from it.
+// instead of returning a proof whose challenges do not follow from it.  The
+// caller's transcript is restored to its state at construction unless
+// status() succeeded, so a rejected prove leaves it as a device_check failure
+// does: untouched (mlhip.h).
 struct ReplayCheck {
   mlh_ctx* ctx;
   mlh_transcript* tr;
+  mlh::HostSha256 saved;
+  bool committed = false;
   uint32_t bad = 0, first_bad = ~0u, n = 0;
-  ReplayCheck(mlh_ctx* c, mlh_transcript* t) : ctx(c), tr(t) {}
+  ReplayCheck(mlh_ctx* c, mlh_transcript* t) : ctx(c), tr(t), saved(t->sha) {}
+  ReplayCheck(const ReplayCheck&) = delete;
+  ReplayCheck& operator=(const ReplayCheck&) = delete;
+  ~ReplayCheck() {
+    if (!committed) tr->sha = saved;
+  }
   void absorb(const uint8_t* p, uint64_t len) { mlh_transcript_absorb(tr, p, len); }
   void expect(const uint8_t* dev_r) {
     uint8_t h[16];
@@ -192,8 +208,11 @@ struct ReplayCheck {
     }
     ++n;
   }
-  mlh_status status() const {
-    if (!bad) return MLH_OK;
+  mlh_status status() {
+    if (!bad) {
+      committed = true;
+      return MLH_OK;
+    }
     return fail(ctx, MLH_ERR_DEVICE,
                 "device transcript diverged from the host replay at challenge " +
                     std::to_string(first_bad) + " (" + std::to_string(bad) + " of " +

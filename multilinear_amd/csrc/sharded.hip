@@ -193,6 +193,102 @@ mlh_status mlh_comm_transport(mlh_comm* c, mlh_transport* out) {
 }
 
 // ---------------------------------------------------------------------------
+// Transport pre-flight: one all-to-all and one all-gather of a rank-tagged
+// pattern, checked on the device.  A multi-GPU caller runs it before its first
+// data-path collective, so a miswired or stalled transport shows up as a
+// named failure (and a watchdog can say which phase hung) instead of a wrong
+// proof.  Word i of the chunk rank s sends to rank d is pf_word(s, d, i); the
+// all-gather sends pf_word(s, kPfGather, i).
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr uint32_t kPfGather = 0xA5u;
+
+__device__ __forceinline__ uint32_t pf_word(uint32_t src, uint32_t dst, uint32_t i) {
+  uint32_t x = src * 0x9E3779B1u ^ (dst + 0x7F4A7C15u) * 0x85EBCA77u ^ i * 0xC2B2AE3Du;
+  x ^= x >> 15;
+  x *= 0x2C1B3C6Du;
+  x ^= x >> 12;
+  return x;
+}
+
+__global__ void __launch_bounds__(256)
+pf_fill_kernel(uint32_t* a2a_send, uint32_t* ag_send, uint32_t words, uint32_t P, uint32_t rank) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= words) return;
+  for (uint32_t d = 0; d < P; ++d) a2a_send[(uint64_t)d * words + i] = pf_word(rank, d, i);
+  ag_send[i] = pf_word(rank, kPfGather, i);
+}
+
+__global__ void __launch_bounds__(256)
+pf_check_kernel(const uint32_t* a2a_recv, const uint32_t* ag_recv, uint32_t words, uint32_t P,
+                uint32_t rank, unsigned long long* bad) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= words) return;
+  unsigned long long n = 0;
+  for (uint32_t s = 0; s < P; ++s) {
+    n += a2a_recv[(uint64_t)s * words + i] != pf_word(s, rank, i);
+    n += ag_recv[(uint64_t)s * words + i] != pf_word(s, kPfGather, i);
+  }
+  if (n) atomicAdd(bad, n);
+}
+
+}  // namespace
+
+extern "C" mlh_status mlh_comm_preflight(mlh_ctx* ctx, const mlh_transport* tp, uint64_t bytes_per_rank,
+                                         uint64_t* mismatches, float* ms) {
+  if (!ctx || !mismatches) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  MLH_TRY(check_transport(ctx, tp));
+  if (bytes_per_rank == 0 || bytes_per_rank % 4 || bytes_per_rank > (1ull << 30))
+    return fail(ctx, MLH_ERR_INVALID, "preflight chunk must be a non-zero multiple of 4 B, <= 1 GiB");
+  Tp T(ctx, tp);
+  const uint32_t P = T.P, words = (uint32_t)(bytes_per_rank / 4);
+  Bufs B(ctx);
+  uint32_t *send, *recv, *ags, *agr;
+  unsigned long long* bad;
+  MLH_TRY(B.get(bytes_per_rank * P, &send));
+  MLH_TRY(B.get(bytes_per_rank * P, &recv));
+  MLH_TRY(B.get(bytes_per_rank, &ags));
+  MLH_TRY(B.get(bytes_per_rank * P, &agr));
+  MLH_TRY(B.get(16, &bad));
+  HIP_TRY(ctx, hipMemsetAsync(bad, 0, 8, ctx->stream));
+  HIP_TRY(ctx, hipMemsetAsync(recv, 0, bytes_per_rank * P, ctx->stream));
+  HIP_TRY(ctx, hipMemsetAsync(agr, 0, bytes_per_rank * P, ctx->stream));
+  const unsigned grid = (words + 255) / 256;
+  hipLaunchKernelGGL(pf_fill_kernel, dim3(grid), dim3(256), 0, ctx->stream, send, ags, words, P, T.rank);
+  HIP_TRY(ctx, hipGetLastError());
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ms) {
+    HIP_TRY(ctx, hipEventCreate(&e0));
+    HIP_TRY(ctx, hipEventCreate(&e1));
+    HIP_TRY(ctx, hipEventRecord(e0, ctx->stream));
+  }
+  mlh_status st = T.all_to_all(send, recv, bytes_per_rank);
+  if (st == MLH_OK) st = T.all_gather(ags, agr, bytes_per_rank);
+  if (st == MLH_OK && ms) {
+    if (T.t->host_side) (void)hipStreamSynchronize(ctx->stream);
+    (void)hipEventRecord(e1, ctx->stream);
+  }
+  if (st == MLH_OK) {
+    hipLaunchKernelGGL(pf_check_kernel, dim3(grid), dim3(256), 0, ctx->stream, recv, agr, words, P, T.rank,
+                       bad);
+    if (hipGetLastError() != hipSuccess) st = fail(ctx, MLH_ERR_HIP, "preflight check launch");
+  }
+  unsigned long long h = 0;
+  if (st == MLH_OK && hipMemcpyAsync(ctx->pinned, bad, 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    st = fail(ctx, MLH_ERR_HIP, "preflight copy");
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess && st == MLH_OK) st = fail(ctx, MLH_ERR_HIP, "preflight sync");
+  if (st == MLH_OK) {
+    memcpy(&h, ctx->pinned, 8);
+    *mismatches = h;
+    if (ms) (void)hipEventElapsedTime(ms, e0, e1);
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  return st;
+}
+
+// ---------------------------------------------------------------------------
 // NTT / INTT / Reed-Solomon (ntt/mod.rs:69-173, fri/mod.rs:19-28)
 // ---------------------------------------------------------------------------
 // X[j + M t] = sum_g wP^(g t) w^(g j) Z_g[j], Z_g = NTT_M(x[g + P .]) with

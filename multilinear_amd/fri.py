@@ -71,9 +71,15 @@ class FriProverData:
                                                ctypes.byref(h)), ctx)
         return FriProverData(h.value, code)
 
-    def fold_step(self, k, r, transcript, device=0):
+    def fold_step(self, k, r, transcript, device=0, gen_pows=None):
+        """fold_step(gen_pows, k, r, transcript) (fri/mod.rs:79-134); gen_pows:
+        None (the table given at init) or (gen_pows[1], log2(gen_pows.len()))."""
         ctx = context(device)
-        check(lib().mlh_fri_prover_fold_step(ctx, self.h, k, fe_bytes(r), transcript.h), ctx)
+        if gen_pows is None:
+            check(lib().mlh_fri_prover_fold_step(ctx, self.h, k, fe_bytes(r), transcript.h), ctx)
+        else:
+            check(lib().mlh_fri_prover_fold_step_gp(ctx, self.h, fe_bytes(gen_pows[0]), gen_pows[1], k,
+                                                    fe_bytes(r), transcript.h), ctx)
 
     @staticmethod
     def fold(code, transcript, device=0, gen_pows=None):

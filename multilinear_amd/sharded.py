@@ -232,6 +232,17 @@ class HostTransport:
                 "transport": "host-staged torch.distributed (%s)" % self.tp.dist.get_backend(self.tp.group)}
 
 
+def preflight(transport, bytes_per_rank, device=0):
+    """mlh_comm_preflight: one all-to-all and one all-gather of a rank-tagged
+    pattern through the transport, checked on the device -> (mismatched words
+    on this rank, ms of the two collectives)."""
+    ctx = context(device)
+    bad, ms = ctypes.c_uint64(), ctypes.c_float()
+    check(lib().mlh_comm_preflight(ctx, _tp(transport), bytes_per_rank, ctypes.byref(bad),
+                                   ctypes.byref(ms)), ctx)
+    return bad.value, ms.value
+
+
 def ntt_block_owner(j, log_total, log_p):
     """(rank, local index) holding X[j] of a sharded forward NTT (block
     2^(log_total - 2 log_p) output layout)."""

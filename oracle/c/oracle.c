@@ -683,3 +683,351 @@ void orc_dot_par(const uint8_t* m, const uint8_t* d, uint32_t log_n, uint8_t out
   }
   st(out, tot);
 }
+
+/* ============================================ whole PCS / batched PCS prove */
+/* PCSProof::prove (src/fri/multilinear_pcs.rs:90-136, PCSProverData::fold
+ * :43-76) and BatchedPCSProof::prove (src/fri/batched_pcs.rs:127-180,
+ * BatchedPCSProverData::{init,fold} :36-125), restated end to end in C so the
+ * production-shape GPU prove (n = 19..24 variables; batched (10, 20)) can be
+ * compared byte for byte: every round polynomial, the batch root, every fold
+ * root, the last element, the final transcript digest and all 128 query
+ * records.  The reference order is kept: to_coefficient -> bit reversal ->
+ * reed_solomon; FriProverData::init; per round compute_sumcheck_polynomial
+ * (sumcheck.rs:174-202: partial_sum at 1 and 2, Lagrange interpolation on
+ * 0,1,2, absorb the two nonzero coefficients, next_challenge, fold) then
+ * fold_step (fri/mod.rs:79-134) with the same r; queries as fri/mod.rs:268-277
+ * and open_query_at :154-175.  OpenMP only splits independent loops (leaves,
+ * pairs, table entries); every field value is exact, so the result does not
+ * depend on the thread count. */
+
+typedef struct {
+  uint64_t len;  /* values in the layer; pairs (i, i + len/2) */
+  u128* vals;
+  uint8_t* tree; /* (len - 1) * 32: len/2 leaf digests, then each level */
+} orc_layer;
+
+static u128 tr_challenge(const sha_t* tr) { /* transcript.rs next_challenge */
+  uint8_t rnd[32];
+  sha_final(tr, rnd);
+  u128 r = ld(rnd);
+  return r >= MOD ? r - MOD : r;
+}
+
+static void commit_layer(orc_layer* ly, int threads) { /* commit_rs_code, fri/mod.rs:45-55 */
+  ly->tree = (uint8_t*)malloc((ly->len - 1) * 32);
+  merkle_pairs_par((const uint8_t*)ly->vals, (uint32_t)__builtin_ctzll(ly->len), ly->tree, threads);
+}
+static const uint8_t* layer_root(const orc_layer* ly) { return ly->tree + 32 * (ly->len - 2); }
+
+/* Merkle::open (merkle_tree/mod.rs:31-58) of the pair at idx: value bytes,
+ * then the sibling of every level below the root.  Returns bytes written. */
+static uint64_t open_layer(const orc_layer* ly, uint64_t idx, uint8_t* out) {
+  const uint64_t L = ly->len / 2;
+  st(out, ly->vals[idx]);
+  st(out + 16, ly->vals[idx + L]);
+  uint64_t w = 32, off = 0, cnt = L, cur = idx;
+  while (cnt > 1) {
+    memcpy(out + w, ly->tree + 32 * (off + (cur ^ 1)), 32);
+    w += 32;
+    off += cnt;
+    cnt /= 2;
+    cur /= 2;
+  }
+  return w;
+}
+
+/* the fold loop of fold_step (fri/mod.rs:89-114): next[i] =
+ * ((a + b) + r (a - b) gen_pows[len - i 2^k]) / 2, i = 0 with twiddle 1 */
+static void fold_layer_par(const u128* src, uint64_t n, const u128* gp, uint64_t glen, uint32_t k, u128 r,
+                           u128* dst, int threads) {
+  const uint64_t half = n / 2;
+  const u128 inv2 = finv(2);
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (long long ii = 0; ii < (long long)half; ii++) {
+    const uint64_t i = (uint64_t)ii;
+    const u128 a = src[i], b = src[i + half];
+    const u128 tw = i == 0 ? 1 : gp[glen - i * (1ull << k)];
+    dst[i] = fmul(fadd(fadd(a, b), fmul(r, fmul(fsub(a, b), tw))), inv2);
+  }
+}
+
+/* Horner fingerprint (batched_fri.rs:30-38): ((c_0 r + c_1) r + ...) + c_{m-1} */
+static u128 fingerprint_col(u128 r, const u128* base, uint64_t stride, uint32_t m, uint64_t i) {
+  u128 acc = 0;
+  for (uint32_t j = 0; j < m; j++) acc = fadd(fmul(acc, r), base[(uint64_t)j * stride + i]);
+  return acc;
+}
+
+/* PolynomialEvals::interpolate (polynomials.rs:51-87) on x = 0, 1, 2 */
+static void interpolate3(const u128 e[3], u128 c[3]) {
+  c[0] = c[1] = c[2] = 0;
+  for (int j = 0; j < 3; j++) {
+    u128 lj[3] = {1, 0, 0}, denom = 1;
+    int deg = 0;
+    for (int m = 0; m < 3; m++) {
+      if (m == j) continue;
+      u128 nl[3] = {0, 0, 0};
+      for (int i = 0; i <= deg; i++) {
+        nl[i] = fsub(nl[i], fmul(lj[i], (u128)m));
+        nl[i + 1] = fadd(nl[i + 1], lj[i]);
+      }
+      deg++;
+      memcpy(lj, nl, sizeof nl);
+      denom = fmul(denom, j >= m ? (u128)(j - m) : fsub(0, (u128)(m - j)));
+    }
+    const u128 sc = fmul(e[j], finv(denom));
+    for (int i = 0; i < 3; i++) c[i] = fadd(c[i], fmul(sc, lj[i]));
+  }
+}
+
+/* one compute_sumcheck_polynomial (sumcheck.rs:174-202) on (mt, dt) of 2^lh
+ * entries with composition x[0]; writes c1 || c2, absorbs them, returns r and
+ * folds the tables in place (sumcheck.rs:234-247). */
+static u128 sumcheck_round(u128* mt, u128* dt, uint32_t lh, u128* prev, sha_t* tr, uint8_t out[32],
+                           int threads) {
+  const uint64_t off = (1ull << lh) / 2;
+  u128 s1 = 0, s2 = 0;
+  const u128 two = 2, mone = fsub(1, two);
+#pragma omp parallel num_threads(threads)
+  {
+    u128 a1 = 0, a2 = 0;
+#pragma omp for schedule(static)
+    for (long long ii = 0; ii < (long long)off; ii++) {
+      const uint64_t i = (uint64_t)ii;
+      a1 = fadd(a1, fmul(mt[i + off], dt[i + off]));
+      const u128 dd = fadd(fmul(mone, dt[i]), fmul(two, dt[i + off]));
+      const u128 mm = fadd(fmul(mone, mt[i]), fmul(two, mt[i + off]));
+      a2 = fadd(a2, fmul(mm, dd));
+    }
+#pragma omp critical
+    {
+      s1 = fadd(s1, a1);
+      s2 = fadd(s2, a2);
+    }
+  }
+  const u128 e[3] = {fsub(*prev, s1), s1, s2};
+  u128 c[3];
+  interpolate3(e, c);
+  st(out, c[1]);
+  st(out + 16, c[2]);
+  sha_update(tr, out, 32);
+  const u128 r = tr_challenge(tr);
+  *prev = fadd(c[0], fmul(r, fadd(c[1], fmul(r, c[2]))));
+  const u128 s = fsub(1, r);
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (long long ii = 0; ii < (long long)off; ii++) {
+    const uint64_t i = (uint64_t)ii;
+    dt[i] = fadd(fmul(s, dt[i]), fmul(r, dt[i + off]));
+    mt[i] = fadd(fmul(s, mt[i]), fmul(r, mt[i + off]));
+  }
+  return r;
+}
+
+/* Bytes of one query record in the flat layout written below (the layout
+ * libmlhip's query staging uses): unbatched, per tree t < n: pair (32 B) +
+ * (n - t) siblings; batched, the column (m x 32 B) + n batch-path siblings,
+ * then per inner tree t < n - 1: pair + (n - 1 - t) siblings. */
+uint64_t orc_pcs_query_bytes(uint32_t m, uint32_t n, int batched) {
+  uint64_t b = 0;
+  if (!batched) {
+    for (uint32_t t = 0; t < n; t++) b += 32ull * (1 + n - t);
+    return b;
+  }
+  b = 32ull * m + 32ull * n;
+  for (uint32_t t = 0; t + 1 < n; t++) b += 32ull * (n - t);
+  return b;
+}
+
+/* evals: m x 2^n (poly-major); points: n; outputs: m claims (unbatched: m = 1,
+ * the claimed evaluation).  prefix bytes are absorbed into the fresh
+ * transcript first.  Outputs: polys n x 32 (c1 || c2), batch_root 32
+ * (batched only), roots (n - batched) x 32, last 16, last_random 32, qidx 128,
+ * qrec 128 x orc_pcs_query_bytes.  Returns 0, 2 (bad shape), 5 (alloc) or 6
+ * (the last layer is not constant: "not an RS code"). */
+int orc_pcs_prove_par(const uint8_t* evals, uint32_t m, uint32_t n, const uint8_t* points,
+                      const uint8_t* outputs, int batched, const uint8_t* prefix, uint64_t prefix_len,
+                      uint8_t* polys, uint8_t* batch_root, uint8_t* roots, uint8_t last[16],
+                      uint8_t last_random[32], uint64_t* qidx, uint8_t* qrec, int threads) {
+  if (n < 1 || m < 1 || (!batched && m != 1) || n > 30) return 2;
+  const uint64_t H = 1ull << n, N0 = 2 * H; /* evaluations, code length */
+  const uint32_t log_dom = n + 1;            /* + LOG_BLOWUP */
+  sha_t tr;
+  sha_init(&tr);
+  if (prefix_len) sha_update(&tr, prefix, prefix_len);
+  /* gen_pows = pow_2_generator_powers(log_domain) (multilinear_pcs.rs:97-99) */
+  u128* gp = (u128*)malloc(N0 * sizeof(u128));
+  u128* codes = (u128*)malloc((uint64_t)m * N0 * sizeof(u128));
+  orc_layer* lay = (orc_layer*)calloc(n + 1, sizeof(orc_layer));
+  u128* mt = (u128*)malloc(H * sizeof(u128));
+  u128* dt = (u128*)malloc(H * sizeof(u128));
+  if (!gp || !codes || !lay || !mt || !dt) return 5;
+  const u128 g = fpow(3, (MOD - 1) >> log_dom);
+  pow_series_par(gp, N0, g, threads);
+  uint8_t gb[16];
+  st(gb, gp[1]);
+  /* per polynomial: to_coefficient, bit_reverse_permutation, reed_solomon */
+  for (uint32_t j = 0; j < m; j++) {
+    u128* c = codes + (uint64_t)j * N0;
+    memcpy(c, evals + 16 * (uint64_t)j * H, H * 16);
+    for (uint32_t i = 0; i < n; i++) { /* polynomials.rs:150-163 */
+      const uint64_t msk = 1ull << i;
+#pragma omp parallel for num_threads(threads) schedule(static)
+      for (long long jj = 0; jj < (long long)H; jj++)
+        if ((uint64_t)jj & msk) c[jj] = fsub(c[jj], c[(uint64_t)jj ^ msk]);
+    }
+    bit_reverse_permutation(c, H);
+    memset(c + H, 0, H * 16);
+    orc_ntt_par((const uint8_t*)c, (uint8_t*)c, log_dom, gb, 0, threads);
+  }
+  /* claim absorb + first commitment */
+  u128 fr = 0, prev;
+  uint8_t* batch_tree = NULL;
+  if (batched) {
+    for (uint32_t i = 0; i < n; i++) sha_update(&tr, points + 16 * i, 16);
+    for (uint32_t j = 0; j < m; j++) sha_update(&tr, outputs + 16 * j, 16);
+    /* BatchedFriProverData::init (batched_fri.rs:41-98): Merkle::batch_commit
+     * of the per-code RS pairs, leaf i = SHA256(pair_0[i] || pair_1[i] || ..) */
+    batch_tree = (uint8_t*)malloc((2 * H - 1) * 32);
+    if (!batch_tree) return 5;
+#pragma omp parallel num_threads(threads)
+    {
+      uint8_t* buf = (uint8_t*)malloc(32ull * m);
+#pragma omp for schedule(static)
+      for (long long ii = 0; ii < (long long)H; ii++) {
+        for (uint32_t j = 0; j < m; j++) {
+          st(buf + 32ull * j, codes[(uint64_t)j * N0 + (uint64_t)ii]);
+          st(buf + 32ull * j + 16, codes[(uint64_t)j * N0 + (uint64_t)ii + H]);
+        }
+        orc_sha256(buf, 32ull * m, batch_tree + 32 * (uint64_t)ii);
+      }
+      free(buf);
+    }
+    uint64_t off = 0, cnt = H;
+    while (cnt > 1) {
+#pragma omp parallel for num_threads(threads) schedule(static) if (cnt > 4096)
+      for (long long jn = 0; jn < (long long)(cnt / 2); jn++)
+        orc_sha256(batch_tree + 32 * (off + 2 * (uint64_t)jn), 64, batch_tree + 32 * (off + cnt + (uint64_t)jn));
+      off += cnt;
+      cnt /= 2;
+    }
+    memcpy(batch_root, batch_tree + 32 * (2 * H - 2), 32);
+    sha_update(&tr, batch_root, 32);
+    fr = tr_challenge(&tr);
+    uint8_t fb[16];
+    st(fb, fr);
+    sha_update(&tr, fb, 16);
+    /* fingerprinted evaluations -> the sumcheck matrix (batched_pcs.rs:54-64) */
+    u128* ev = (u128*)malloc((uint64_t)m * H * sizeof(u128));
+    if (!ev) return 5;
+    memcpy(ev, evals, (uint64_t)m * H * 16);
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (long long ii = 0; ii < (long long)H; ii++) mt[ii] = fingerprint_col(fr, ev, H, m, (uint64_t)ii);
+    free(ev);
+    u128* outs = (u128*)malloc(m * sizeof(u128));
+    for (uint32_t j = 0; j < m; j++) outs[j] = ld(outputs + 16 * j);
+    prev = fingerprint_col(fr, outs, 1, m, 0);
+    free(outs);
+  } else {
+    /* FriProverData::init (fri/mod.rs:58-76) */
+    lay[0].len = N0;
+    lay[0].vals = codes;
+    commit_layer(&lay[0], threads);
+    sha_update(&tr, layer_root(&lay[0]), 32);
+    memcpy(mt, evals, H * 16);
+    prev = ld(outputs);
+  }
+  /* build_tables_for_pcs (sumcheck.rs:128-145): delta = eq(points), big endian */
+  dt[0] = 1;
+  for (uint32_t i = n; i-- > 0;) {
+    const uint64_t cur = 1ull << (n - 1 - i);
+    const u128 p = ld(points + 16 * i), q = fsub(1, p);
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (long long jj = 0; jj < (long long)cur; jj++) {
+      dt[(uint64_t)jj + cur] = fmul(dt[jj], p);
+      dt[jj] = fmul(dt[jj], q);
+    }
+  }
+  /* rounds: compute_sumcheck_polynomial, then fold_step with the same r */
+  uint32_t nl = batched ? 0 : 1; /* committed FRI layers */
+  int rc = 0;
+  u128 last_el = 0;
+  for (uint32_t k = 0; k < n; k++) {
+    const u128 r = sumcheck_round(mt, dt, n - k, &prev, &tr, polys + 32 * k, threads);
+    const u128* src;
+    uint64_t len;
+    u128* fpv = NULL;
+    if (batched && k == 0) { /* batched_fold_step (batched_fri.rs:100-176) */
+      fpv = (u128*)malloc(N0 * sizeof(u128));
+      if (!fpv) return 5;
+#pragma omp parallel for num_threads(threads) schedule(static)
+      for (long long ii = 0; ii < (long long)N0; ii++) fpv[ii] = fingerprint_col(fr, codes, N0, m, (uint64_t)ii);
+      src = fpv;
+      len = N0;
+    } else {
+      src = lay[nl - 1].vals;
+      len = lay[nl - 1].len;
+    }
+    if (len <= 2) break;
+    u128* nxt = (u128*)malloc((len / 2) * sizeof(u128));
+    if (!nxt) return 5;
+    fold_layer_par(src, len, gp, N0, k, r, nxt, threads);
+    free(fpv);
+    if (len / 2 == 2) {
+      if (nxt[0] != nxt[1]) rc = 6;
+      last_el = nxt[0];
+      st(last, last_el);
+      sha_update(&tr, last, 16);
+      free(nxt);
+      break;
+    }
+    lay[nl].len = len / 2;
+    lay[nl].vals = nxt;
+    commit_layer(&lay[nl], threads);
+    sha_update(&tr, layer_root(&lay[nl]), 32);
+    nl++;
+  }
+  for (uint32_t t = 0; t < nl; t++) memcpy(roots + 32 * t, layer_root(&lay[t]), 32);
+  /* queries (multilinear_pcs.rs:113-121 / batched_pcs.rs:160-168) */
+  const uint64_t qb = orc_pcs_query_bytes(m, n, batched);
+  for (int q = 0; q < 128; q++) {
+    uint8_t rnd[32];
+    sha_final(&tr, rnd);
+    uint64_t r64;
+    memcpy(&r64, rnd, 8);
+    const uint64_t idx = r64 % (N0 / 2);
+    qidx[q] = idx;
+    uint8_t* o = qrec + qb * (uint64_t)q;
+    uint64_t cur = idx;
+    if (batched) { /* batched open_query_at (batched_fri.rs:207-224) */
+      for (uint32_t j = 0; j < m; j++) {
+        st(o, codes[(uint64_t)j * N0 + idx]);
+        st(o + 16, codes[(uint64_t)j * N0 + idx + H]);
+        o += 32;
+      }
+      uint64_t off = 0, cnt = H, c2 = idx;
+      while (cnt > 1) {
+        memcpy(o, batch_tree + 32 * (off + (c2 ^ 1)), 32);
+        o += 32;
+        off += cnt;
+        cnt /= 2;
+        c2 /= 2;
+      }
+      cur = idx % (H / 2);
+    }
+    for (uint32_t t = 0; t < nl; t++) { /* open_query_at (fri/mod.rs:154-175) */
+      o += open_layer(&lay[t], cur, o);
+      cur %= lay[t].len / 4 ? lay[t].len / 4 : 1;
+    }
+    sha_update(&tr, (const uint8_t*)&idx, 8);
+  }
+  sha_final(&tr, last_random);
+  for (uint32_t t = batched ? 0 : 1; t < nl; t++) free(lay[t].vals);
+  for (uint32_t t = 0; t < nl; t++) free(lay[t].tree);
+  free(lay);
+  free(batch_tree);
+  free(codes);
+  free(gp);
+  free(mt);
+  free(dt);
+  return rc;
+}

@@ -38,6 +38,9 @@ def lib():
         L.orc_partial_sums_par.argtypes = [P, P, U, P, I]
         L.orc_fold_par.argtypes = [P, P, U, P, I]
         L.orc_dot_par.argtypes = [P, P, U, P, I]
+        L.orc_pcs_query_bytes.argtypes = [U, U, I]
+        L.orc_pcs_query_bytes.restype = ctypes.c_uint64
+        L.orc_pcs_prove_par.argtypes = [P, U, U, P, P, I, P, ctypes.c_uint64, P, P, P, P, P, P, P, I]
         _lib = L
     return _lib
 
@@ -188,3 +191,53 @@ def dot_par(m, d, log_n):
     out = np.zeros(16, dtype=np.uint8)
     lib().orc_dot_par(_p(np.ascontiguousarray(m)), _p(np.ascontiguousarray(d)), log_n, _p(out), threads())
     return int.from_bytes(bytes(out), "little")
+
+
+def _fe_array(vals):
+    return np.frombuffer(b"".join(int(v).to_bytes(16, "little") for v in vals) or b"\0" * 16,
+                         dtype=np.uint8).copy()
+
+
+def pcs_prove_par(evals, n, points, outputs, batched=False, prefix=b""):
+    """PCSProof::prove (multilinear_pcs.rs:90-136) or, batched,
+    BatchedPCSProof::prove (batched_pcs.rs:127-180) in C, end to end.
+    evals: (m * 2^n, 4) uint32 limbs, polynomial-major.  Returns a dict with
+    polys [(c1, c2)], batch_root, roots, last_elem, last_random, indices and
+    the flat query records (bytes, the layout of libmlhip's query staging)."""
+    ev = np.ascontiguousarray(evals, dtype=np.uint32)
+    m = ev.shape[0] >> n
+    assert ev.shape[0] == m << n and len(outputs) == m
+    L = lib()
+    qb = L.orc_pcs_query_bytes(m, n, 1 if batched else 0)
+    polys = np.zeros(32 * n, dtype=np.uint8)
+    broot = np.zeros(32, dtype=np.uint8)
+    nroots = n - (1 if batched else 0)
+    roots = np.zeros(32 * max(nroots, 1), dtype=np.uint8)
+    last = np.zeros(16, dtype=np.uint8)
+    lr = np.zeros(32, dtype=np.uint8)
+    qidx = np.zeros(128, dtype=np.uint64)
+    qrec = np.zeros(128 * qb, dtype=np.uint8)
+    pre = np.frombuffer(prefix, dtype=np.uint8).copy() if prefix else np.zeros(1, dtype=np.uint8)
+    rc = L.orc_pcs_prove_par(_p(ev), m, n, _p(_fe_array(points)), _p(_fe_array(outputs)),
+                             1 if batched else 0, _p(pre), len(prefix), _p(polys), _p(broot), _p(roots),
+                             _p(last), _p(lr), _p(qidx), _p(qrec), threads())
+    raw = bytes(polys)
+    rr = bytes(roots)
+    return {
+        "rc": rc,
+        "polys": [(int.from_bytes(raw[32 * k:32 * k + 16], "little"),
+                   int.from_bytes(raw[32 * k + 16:32 * k + 32], "little")) for k in range(n)],
+        "batch_root": bytes(broot) if batched else None,
+        "roots": [rr[32 * i:32 * i + 32] for i in range(nroots)],
+        "last_elem": int.from_bytes(bytes(last), "little"),
+        "last_random": bytes(lr),
+        "indices": [int(x) for x in qidx],
+        "queries": bytes(qrec),
+        "query_bytes": qb,
+    }
+
+
+def mle_evaluate_par(evals, n, points):
+    """MultilinearPolynomialEvals::evaluate (polynomials.rs:165-187) as
+    sum_i evals[i] * eq(points)[i]."""
+    return dot_par(np.ascontiguousarray(evals, dtype=np.uint32), eq_table_par(points), n)

@@ -95,3 +95,78 @@ def test_sharded_ntt_spot_check_formula_vs_oracle():
             q, l = ntt_block_owner(j, log_n, log_p)
             assert ((l >> s_) << (s_ + log_p)) | (q << s_) | (l & ((1 << s_) - 1)) == j
             assert 0 <= q < P and 0 <= l < n // P
+
+
+def test_headline_watchdog_fires_with_phase_and_exits_nonzero():
+    code = ("import bench, time\n"
+            "w = bench._HeadlineWatchdog(0, 8, 0.3)\n"
+            "w.info = {'ranks': 8, 'rank': 0, 'device': 0, 'transport': 'rccl'}\n"
+            "w.phase('comm_create'); w.phase('preflight')\n"
+            "time.sleep(20)\n"
+            "print('not reached')\n")
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=60)
+    assert p.returncode == 3
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and "not reached" not in p.stdout
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["phase"] == "preflight" and d["rccl_ranks"] == 8
+    assert "preflight" in d["headline_error"] and d["n_gpus"] == 8
+    assert list(d["phases_started_s"]) == ["comm_create", "preflight"]
+
+
+def test_headline_watchdog_disarm_and_fail():
+    code = ("import bench, time\n"
+            "w = bench._HeadlineWatchdog(0, 2, 0.3)\n"
+            "w.disarm(); time.sleep(1.0)\n"
+            "w2 = bench._HeadlineWatchdog(0, 2, 30)\n"
+            "w2.phase('preflight'); w2.fail('pre-flight mismatch')\n")
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=60)
+    assert p.returncode == 4
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["headline_error"] == "pre-flight mismatch"
+
+
+_STALL_SCRIPT = r'''
+import os, sys, time
+sys.path.insert(0, os.environ["MLH_ROOT"])
+import torch.distributed as dist
+import torch
+import bench
+dist.init_process_group("gloo")
+rank = dist.get_rank()
+w = bench._HeadlineWatchdog(rank, 2, 5.0)
+w.info = {"ranks": 2, "rank": rank, "device": 0, "transport": "host-staged gloo"}
+w.phase("preflight")
+if rank == 1:
+    time.sleep(120)          # a dead peer: never joins the collective
+t = torch.zeros(8)
+dist.all_reduce(t)           # rank 0 waits here
+print("not reached", flush=True)
+'''
+
+
+def test_headline_watchdog_ends_a_stalled_gloo_collective_world2(tmp_path):
+    """world 2 over gloo on the CPU: rank 1 never joins, rank 0 blocks inside a
+    real collective; within the budget rank 0 prints the diagnostic line (the
+    phase reached) and both ranks exit non-zero."""
+    import socket
+
+    script = tmp_path / "stall.py"
+    script.write_text(_STALL_SCRIPT)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MLH_ROOT=ROOT)
+    t0 = __import__("time").time()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+                        "2", "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)],
+                       cwd=ROOT, capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode != 0
+    assert __import__("time").time() - t0 < 90
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout + p.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["phase"] == "preflight" and "did not finish" in d["headline_error"]
+    assert "not reached" not in p.stdout

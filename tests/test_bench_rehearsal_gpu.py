@@ -1,0 +1,58 @@
+"""bench.py's N > 1 script rehearsed with two ranks sharing the box's one GPU
+(gloo, host-staged transport; never a result): the line certifies itself
+(pre-flight pattern check, in-run output check, a transport label that does
+not claim xGMI), and a rank whose all-to-all never returns -- a dead RCCL peer
+on the 8-GPU node -- ends the run within the headline budget with a
+diagnostic line naming the phase, instead of a silent kill."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(extra_env, args, timeout):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MLH_BENCH_BACKEND="gloo", **extra_env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2"] + args
+    t0 = time.time()
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    return p, lines, time.time() - t0
+
+
+def test_rehearsal_n2_line_certifies_itself():
+    p, lines, _ = _run({}, ["--log-n", "20", "--steps", "3", "--warmup", "1", "--no-extras",
+                            "--spinup-s", "0"], 110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines) == 1, p.stdout + p.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["preflight"]["ok"] and d["preflight"]["mismatches_max"] == 0
+    assert d["sharded_ntt_verified"] is True
+    assert "xGMI" not in d["config"]["parallelism"] and "rehearsal" in d["config"]["parallelism"]
+    assert d["rccl_ranks"] is None
+
+
+def test_rehearsal_n2_stalled_all_to_all_reports_phase():
+    p, lines, dt = _run({"MLH_BENCH_TEST_STALL_A2A": "1"},
+                        ["--log-n", "20", "--steps", "3", "--warmup", "1", "--no-extras",
+                         "--headline-budget-s", "20"], 110)
+    assert p.returncode != 0
+    assert len(lines) == 1, p.stdout + p.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["phase"] == "preflight"
+    assert "did not finish within 20 s" in d["headline_error"]
+    assert d["comm"]["ranks"] == 2 and d["rccl_ranks"] is None
+    assert dt < 100

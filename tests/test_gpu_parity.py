@@ -335,6 +335,74 @@ def test_fri_prover_step_api():
     assert [v for v, _ in q] == [v for v, _ in wq]
 
 
+def _step_both(opd, otr, pd, tr, gp_list, gp_arg, steps):
+    """Run fold_step(gen_pows, k, r, tr) on the oracle and through
+    mlh_fri_prover_fold_step_gp with the same table; compare after each step.
+    Returns the step at which the oracle panicked ("not an RS code"), else None."""
+    for k in range(steps):
+        r = tr.next_challenge()
+        assert r == otr.next_challenge()
+        try:
+            opd.fold_step(gp_list, k, r, otr)
+        except AssertionError:
+            with pytest.raises(RuntimeError, match="not an RS code"):
+                pd.fold_step(k, r, tr, gen_pows=gp_arg)
+            return k
+        pd.fold_step(k, r, tr, gen_pows=gp_arg)
+        assert pd.fold_roots() == opd.fold_roots(), k
+        assert tr.random() == otr.random(), k
+    return None
+
+
+@pytest.mark.parametrize("log_n", [3, 8, 11])
+def test_fri_prover_fold_step_gp_reference_signature(log_n):
+    """The reference's step API shape: FriProverData::init(code, tr) with no
+    table, then fold_step(gen_pows, k, r, tr) with one (multilinear_pcs.rs:72,
+    batched_fri.rs:200, fri/mod.rs:141).  (1) the canonical table
+    pow_2_generator_powers(L); (2) the table of another generator h = g^3 of
+    the same order with a code built with h; (3) a 2x-length table, which the
+    reference folds with g_2N^(-i 2^k) and rejects at the last layer ("not an
+    RS code") -- the same step returns MLH_ERR_NOT_RS_CODE here; (4) a table
+    shorter than half the code (the reference's index underflows) and a
+    generator of the wrong order are rejected; (5) a step after the last
+    element re-absorbs it, as the reference does."""
+    L = log_n + 1
+    vals = rand_vals(1 << log_n, 40 + log_n)
+    g = F.pow_2_generator(L)
+    for h in (g, pow(g, 3, F.M)):
+        code = OF.reed_solomon(vals, h)
+        gp = [pow(h, j, F.M) for j in range(1 << L)]
+        otr, tr = OT.Transcript(), Transcript()
+        opd = OF.FriProverData.init(code, otr)
+        pd = MF.FriProverData.init(dev(code), tr)
+        assert _step_both(opd, otr, pd, tr, gp, (h, L), log_n) is None
+        assert pd.last_element == opd.last_element
+        assert [v for v, _ in pd.open_query_at(5, L)] == [v for v, _ in opd.open_query_at(5)]
+        # (5) one more step: the reference folds its last tree again
+        r = tr.next_challenge()
+        opd.fold_step(gp, log_n - 1, r, otr)
+        pd.fold_step(log_n - 1, r, tr, gen_pows=(h, L))
+        assert tr.random() == otr.random() and pd.last_element == opd.last_element
+    # (3) gen_pows twice the code's length
+    code = OF.reed_solomon(vals, g)
+    gp2 = F.pow_2_generator_powers(L + 1)
+    otr, tr = OT.Transcript(), Transcript()
+    opd = OF.FriProverData.init(code, otr)
+    pd = MF.FriProverData.init(dev(code), tr)
+    assert _step_both(opd, otr, pd, tr, gp2, (gp2[1], L + 1), log_n) == log_n - 1
+    # (4) shorter than half the code; wrong order
+    lib, ctx = D.lib(), D.context()
+    tr = Transcript()
+    pd = MF.FriProverData.init(dev(code), tr)
+    r = D.fe_bytes(tr.next_challenge())
+    st = lib.mlh_fri_prover_fold_step_gp(ctx, pd.h, D.fe_bytes(F.pow_2_generator(L - 2)), L - 2, 0, r,
+                                         tr.h)
+    assert st == _lib.MLH_ERR_INVALID and b"underflow" in lib.mlh_last_error(ctx)
+    st = lib.mlh_fri_prover_fold_step_gp(ctx, pd.h, D.fe_bytes(g * g % F.M), L, 0, r, tr.h)
+    assert st == _lib.MLH_ERR_BAD_GENERATOR
+    assert pd.fold_roots() == [OF.commit_rs_code(code).root()]  # rejected steps left no layer
+
+
 @pytest.mark.parametrize("nq", [1, 5, 128, 129, 300])
 def test_fri_prover_open_queries_many(nq):
     """mlh_fri_prover_open_queries: indices in the kernel arguments (<= 128)

@@ -255,3 +255,66 @@ def test_trace_evaluate_oracle():
     assert OS.trace_evaluate([a, b, c, d], 2, [p]) == [((1 - p) * a + p * c) % F.M,
                                                        ((1 - p) * b + p * d) % F.M]
     assert OS.trace_evaluate([9, 8], 2, []) == [9, 8]
+
+
+def _flat_fri_queries(queries):
+    return b"".join(v + b"".join(s for s, _ in path) for q in queries for v, path in q)
+
+
+def _flat_batched_queries(queries):
+    raw = b""
+    for (col, bpath), inner in queries:
+        raw += b"".join(col) + b"".join(s for s, _ in bpath)
+        for value, path in inner:
+            raw += value + b"".join(s for s, _ in path)
+    return raw
+
+
+@pytest.mark.parametrize("n,prefix", [(1, b""), (2, b""), (5, b"abc"), (8, b""), (10, b"")])
+def test_c_pcs_prove_matches_python(C, n, prefix):
+    """The C end-to-end PCSProof::prove (multilinear_pcs.rs:90-136) -- the
+    full-size checker of the GPU prove -- against the Python restatement:
+    every round polynomial, root, query record, last element and the final
+    transcript digest.  n = 10 is also the golden fixture."""
+    from multilinear_amd.device import ints_to_limbs
+
+    ev = [F.from_i64(7 * i + 3) for i in range(1 << n)]
+    pts = [F.from_i64(i) for i in range(n)]
+    out = OPL.mle_evaluate(ev, pts)
+    assert C.mle_evaluate_par(ints_to_limbs(ev), n, pts) == out
+    tr = OT.Transcript()
+    tr.absorb(prefix)
+    want = OP.PCSProof.prove(pts, out, ev, tr)
+    got = C.pcs_prove_par(ints_to_limbs(ev), n, pts, [out], prefix=prefix)
+    assert got["rc"] == 0
+    assert got["polys"] == [tuple(p) for p in want.sumcheck_polynomials]
+    assert got["roots"] == want.fri_proof.commitments
+    assert got["last_elem"] == want.fri_proof.last_elem
+    assert got["last_random"] == want.fri_proof.last_random
+    assert got["queries"] == _flat_fri_queries(want.fri_proof.queries)
+    if n == 10 and not prefix:
+        pr = GOLDEN["pcs_7i3_n10"]
+        assert [[h(c) for c in q] for q in got["polys"]] == pr["sumcheck_polys"]
+        assert got["last_random"].hex() == pr["last_random"]
+
+
+@pytest.mark.parametrize("m,n", [(1, 1), (2, 1), (3, 5), (10, 6), (2, 8)])
+def test_c_batched_pcs_prove_matches_python(C, m, n):
+    """The C end-to-end BatchedPCSProof::prove (batched_pcs.rs:127-180) against
+    the Python restatement, with batched_pcs_verify_test's inputs
+    (batched_pcs.rs:261-306) at a small size."""
+    from multilinear_amd.device import ints_to_limbs
+    from oracle import batched as OB
+
+    pts = [F.from_i64(i) for i in range(n)]
+    polys = [[F.from_i64((j * 3 + i * 5) % 100) for j in range(1 << n)] for i in range(m)]
+    outs = [OPL.mle_evaluate(p, pts) for p in polys]
+    want = OB.BatchedPCSProof.prove(pts, outs, polys, OT.Transcript())
+    got = C.pcs_prove_par(ints_to_limbs([v for p in polys for v in p]), n, pts, outs, batched=True)
+    assert got["rc"] == 0
+    assert got["polys"] == [tuple(p) for p in want.sumcheck_polynomials]
+    assert got["batch_root"] == want.fri_proof.batch_commitment
+    assert got["roots"] == want.fri_proof.commitments
+    assert got["last_elem"] == want.fri_proof.last_elem
+    assert got["last_random"] == want.fri_proof.last_random
+    assert got["queries"] == _flat_batched_queries(want.fri_proof.queries)

@@ -52,7 +52,7 @@ def _hip():
 class ThreadDeviceTransport:
     """P in-process ranks; collectives enqueued on the caller's stream."""
 
-    def __init__(self, P):
+    def __init__(self, P, a2a_shift=0):
         self.P = P
         self.hip = _hip()
         self.bar = threading.Barrier(P, timeout=120)
@@ -64,7 +64,7 @@ class ThreadDeviceTransport:
         def a2a(user, send, recv, per, stream):  # (void* arguments arrive as int or None)
             me = user or 0
             return self._run(me, send, stream, lambda s, src: self._copy(
-                (recv or 0) + s * per, (src or 0) + me * per, per, stream))
+                (recv or 0) + s * per, (src or 0) + ((me + a2a_shift) % P) * per, per, stream))
 
         def ag(user, send, recv, nbytes, stream):
             return self._run(user or 0, send, stream, lambda s, src: self._copy(
@@ -109,9 +109,9 @@ class _Tp:
         self.transport = c
 
 
-def _run_ranks(P, body):
+def _run_ranks(P, body, tr=None):
     """body(rank, ctx, stream_ptr, transport) in P threads; returns the results."""
-    tr = ThreadDeviceTransport(P)
+    tr = tr or ThreadDeviceTransport(P)
     out, errs = [None] * P, []
     streams = [torch.cuda.Stream() for _ in range(P)]
     ctxs = []
@@ -223,6 +223,31 @@ def test_ntt_spot_check_logic_vs_c_oracle_p8():
     owner, loc = S.ntt_block_owner(j, log_n, 3)
     outs[owner][loc] = (outs[owner][loc] + 1) % F.M
     assert outs[owner][loc] != sum(res[r][1][5] for r in range(P)) % F.M
+
+
+@pytest.mark.parametrize("P", [2, 8])
+def test_comm_preflight_pattern_p8(P):
+    """mlh_comm_preflight (bench.py runs it before the first data-path
+    collective): a 1 MiB all-to-all + all-gather of rank-tagged words through
+    a device-ordered transport -- 0 mismatches on every rank; a transport that
+    delivers each all-to-all chunk from the wrong offset (a miswired exchange)
+    is caught on every rank, with exactly the all-to-all's words counted."""
+    per = (1 << 20) // P
+
+    def body(r, ctx, st, t):
+        return S.preflight(t, per)
+
+    for shift, want in ((0, 0), (1, per // 4 * P)):
+        res = _run_ranks(P, body, ThreadDeviceTransport(P, a2a_shift=shift))
+        for r in range(P):
+            bad, ms = res[r]
+            assert bad == want, (shift, r, bad)
+            assert ms >= 0.0
+    L = DV.lib()
+    ctx = DV.context()
+    t = ThreadDeviceTransport(1).transports[0]
+    bad = ctypes.c_uint64()
+    assert L.mlh_comm_preflight(ctx, _tp(t), 6, ctypes.byref(bad), None) == _lib.MLH_ERR_INVALID
 
 
 def _sumcheck_oracle(ev, pts, claim):
