@@ -444,8 +444,8 @@ def main():
                             if not sharded else
                             ("sharded x%d (four-step NTT, RCCL all-to-all over xGMI)" % world
                              if BACKEND == "nccl" else
-                             "sharded x%d (four-step NTT, host-staged %s all-to-all; rehearsal, "
-                             "not xGMI)" % (world, BACKEND))),
+                             "sharded x%d (four-step NTT, host-staged %s all-to-all: a rehearsal, "
+                             "not a measurement)" % (world, BACKEND))),
         },
         "ntt_hbm_frac": (32.0 * N / (ms_per_step * 1e-3) / 1e9) / HBM_PEAK_GBS,
         "roofline": {
