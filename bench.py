@@ -230,17 +230,35 @@ def load_valu_profile():
                          "that clock; the clock derivation is good to ~2 %, so issue_frac_raw "
                          "slightly above 1 means at the ceiling (issue_frac caps it at 1)",
            "kernels": {}}
+    mix = {}
+    mpaths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_isa_mix.json")), reverse=True)
+    if mpaths:  # tools/isa_mix.py: the instruction-mix ceiling of each kernel
+        try:
+            mix = json.load(open(mpaths[0])).get("kernels", {})
+            out["mix_source"] = os.path.basename(mpaths[0])
+            out["mix_ceiling"] = ("one wave's static VALU mix weighted by the measured per-instruction "
+                                  "issue rates (profiles/r04_isa.json): issue_frac_vs_mix = issue over "
+                                  "that mix's ceiling at the same clock")
+        except (OSError, ValueError):
+            mix = {}
     for name, k in d.get("kernels", {}).items():
         for key, what in picks.items():
             if name.endswith("mlh::" + key) and k.get("eff_clock_ghz"):
                 clk = k["eff_clock_ghz"] if k["avg_ms"] >= 0.05 else CHIP_MAX_GHZ
                 clk = min(clk, CHIP_MAX_GHZ)
                 ceiling = 256 * 4 * 64 / 4 * clk * 1e9
-                out["kernels"][key] = {"what": what, "avg_ms": k["avg_ms"],
-                                       "lane_instr_per_s": k["lane_instr_per_s"],
-                                       "clock_ghz": clk,
-                                       "issue_frac": min(1.0, k["lane_instr_per_s"] / ceiling),
-                                       "issue_frac_raw": k["lane_instr_per_s"] / ceiling}
+                rec = {"what": what, "avg_ms": k["avg_ms"],
+                       "lane_instr_per_s": k["lane_instr_per_s"],
+                       "clock_ghz": clk,
+                       "issue_frac": min(1.0, k["lane_instr_per_s"] / ceiling),
+                       "issue_frac_raw": k["lane_instr_per_s"] / ceiling}
+                m = mix.get(key)
+                if m and m.get("cycles_per_instr"):
+                    mc = 256 * 4 * 64 * clk * 1e9 / m["cycles_per_instr"]
+                    rec["mix_cycles_per_instr"] = m["cycles_per_instr"]
+                    rec["mix_ceiling_lane_instr_per_s"] = mc
+                    rec["issue_frac_vs_mix"] = k["lane_instr_per_s"] / mc
+                out["kernels"][key] = rec
     return out
 
 

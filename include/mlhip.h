@@ -47,7 +47,8 @@ typedef enum mlh_status {
   MLH_ERR_DEVICE = 10        /* device-side failure inside a prove: a cooperative
                                 kernel's wait timed out, or a challenge the device
                                 drew differs from the host transcript replay; the
-                                outputs of that call are invalid                  */
+                                outputs of that call are invalid and the caller's
+                                transcript is left as it was at the call's entry */
 } mlh_status;
 
 typedef struct mlh_ctx mlh_ctx;               /* device + stream + twiddle caches */

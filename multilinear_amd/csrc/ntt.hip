@@ -316,15 +316,33 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   fe tbv[kTbPerThread][4];
   const uint64_t jl = jrest & ((1ull << g.loga) - 1);
   fe ta_c0, ta_c1;
+  // MLH_TB_COALESCED: the 4R dwordx4 pieces of the tile's TB column are dealt
+  // to the threads in order (piece i = part i mod 4 of row i / 4), so 4
+  // adjacent lanes read one row's 64-B entry and a wave instruction touches 16
+  // entries instead of 64 (each row's entry sits 2^ltcols x 64 B from the
+  // next).  Round 5 counters (profiles/r05_ntt_pass_attrib.json): the
+  // one-row-per-lane form made 256 of pass 0's 672 L1 requests per wave and
+  // kept TA 62 % busy against 27 % in pass 1.  The LDS image is the same.
+#ifndef MLH_TB_COALESCED
+#define MLH_TB_COALESCED 1
+#endif
   auto load_tb = [&]() {
     if constexpr (TW == 0 && MLH_DIAG_TW == 0) {
-      const uint64_t jh = jrest >> g.loga;
+      const uint64_t jh = jrest >> g.loga;  // the same for the whole tile (loga >= 3)
       const uint32_t ltcols = g.lstride - g.loga;
 #pragma unroll
       for (int e = 0; e < kTbPerThread; ++e) {
+#if MLH_TB_COALESCED
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t i = (uint32_t)((e * 4 + k) * NTt + tid);
+          tbv[e][k] = fe_load(tb + ((((uint64_t)(i >> 2) << ltcols) + jh) << 2) + (i & 3));
+        }
+#else
         const fe* q = tb + ((((uint64_t)(e * NTt + tid) << ltcols) + jh) << 2);
 #pragma unroll
         for (int k = 0; k < 4; ++k) tbv[e][k] = fe_load(q + k);
+#endif
       }
     }
   };
@@ -374,7 +392,8 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
 #pragma unroll
     for (int e = 0; e < kTbPerThread; ++e)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) lds[4 * (e * NT + tid) + k] = tbv[e][k];
+      for (int k = 0; k < 4; ++k)
+        lds[MLH_TB_COALESCED ? (e * 4 + k) * NT + tid : 4 * (e * NT + tid) + k] = tbv[e][k];
     __syncthreads();
   }
   uint64_t kbase = 0;

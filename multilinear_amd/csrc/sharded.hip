@@ -324,13 +324,19 @@ mlh_status mlh_sharded_ntt(mlh_ctx* ctx, const mlh_transport* t, const void* dev
   return MLH_OK;
 }
 
-// `count` transforms, pipelined over two streams: stage A (the local NTT of a
-// forward transform, the cross-shard DFT of an inverse one) runs on the
-// context stream, stage B (the all-to-all, then the other local step) on the
-// context's side stream, so the exchange of transform i overlaps stage A of
-// transform i + 1.  Two staging buffers: stage A of i + 2 waits for stage B of
-// i to have sent its buffer.  On return the context stream is ordered after
-// every transform.  With a host-side transport the stages run in turn.
+// `count` transforms, pipelined over two streams.  Only the exchange runs on
+// the context's side stream; both compute steps run on the context stream in
+// the order A(0) A(1) C(0) A(2) C(1) ... A(n-1) C(n-2) C(n-1), where A is the
+// first local step (forward: the local NTT; inverse: the cross-shard DFT) and
+// C the second (forward: the cross-shard DFT; inverse: the local INTT).  The
+// all-to-all of transform i therefore overlaps A(i+1) and C(i-1), and a step
+// costs max(A + C, all-to-all) instead of max(A, all-to-all + C) with C on the
+// exchange's stream (at P = 8 the 235 MB exchange is the longer
+// one).  Buffers: z[k] (A's output, sent) and recv[k] (received, C's input),
+// k = i mod 2; A(i+2) reuses z[k] only after C(i) (issued after the exchange
+// of i completed) and the exchange of i+2 reuses recv[k] only after C(i) read
+// it.  On return the context stream is ordered after every transform.  With a
+// host-side transport the transforms run one after another.
 mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const void* const* dev_in,
                                  void* const* dev_out, uint32_t count, uint32_t log_n,
                                  const uint8_t gen[16], int inverse) {
@@ -353,27 +359,27 @@ mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const voi
   uint8_t gp[16];
   store_fe(gp, h_pow(h_load(gen), (u128)tp.P));
   Bufs b(ctx);
-  fe *z[2], *recv;
-  MLH_TRY(b.get(M * 16, &z[0]));
-  MLH_TRY(b.get(M * 16, &z[1]));
-  MLH_TRY(b.get(M * 16, &recv));
-  hipEvent_t a_done[2], b_done[2];
+  fe *z[2], *recv[2];
+  for (int k = 0; k < 2; ++k) {
+    MLH_TRY(b.get(M * 16, &z[k]));
+    MLH_TRY(b.get(M * 16, &recv[k]));
+  }
+  hipEvent_t a_done[2], x_done[2], c_done[2];
   for (int k = 0; k < 2; ++k) {
     a_done[k] = take_event(ctx);
-    b_done[k] = take_event(ctx);
+    x_done[k] = take_event(ctx);
+    c_done[k] = take_event(ctx);
   }
   struct Recycle {  // the events go back to the context's free list
     mlh_ctx* c;
     hipEvent_t* e;
     ~Recycle() {
-      for (int k = 0; k < 5; ++k) c->ev_free.push_back(e[k]);
+      for (int k = 0; k < 7; ++k) c->ev_free.push_back(e[k]);
     }
   };
-  hipEvent_t evs[5] = {a_done[0], a_done[1], b_done[0], b_done[1], take_event(ctx)};
+  hipEvent_t evs[7] = {a_done[0], a_done[1], x_done[0], x_done[1], c_done[0], c_done[1], take_event(ctx)};
   Recycle rec{ctx, evs};
   hipStream_t main = ctx->stream, side = ctx->side;
-  HIP_TRY(ctx, hipEventRecord(b_done[1], main));  // the side stream starts after the caller's work
-  HIP_TRY(ctx, hipStreamWaitEvent(side, b_done[1], 0));
   // On every exit, error paths included, the context stream waits for all the
   // side stream's work: the pooled buffers (Bufs, released after this guard)
   // and the events are reused only behind it.
@@ -384,22 +390,32 @@ mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const voi
       (void)hipEventRecord(e, side);
       (void)hipStreamWaitEvent(main, e, 0);
     }
-  } join{main, side, evs[4]};
-  for (uint32_t i = 0; i < count; ++i) {
+  } join{main, side, evs[6]};
+  auto step_a = [&](uint32_t i) -> mlh_status {
     const int k = i & 1;
-    if (i >= 2) HIP_TRY(ctx, hipStreamWaitEvent(main, b_done[k], 0));  // z[k] was sent
     if (!inverse) MLH_TRY(mlh_ntt(ctx, dev_in[i], z[k], log_n - tp.p, gp));
     else MLH_TRY(mlh_shard_ntt_cross(ctx, dev_in[i], z[k], log_n, tp.p, tp.rank, gen, 1));
     HIP_TRY(ctx, hipEventRecord(a_done[k], main));
     HIP_TRY(ctx, hipStreamWaitEvent(side, a_done[k], 0));
-    {
-      StreamSwap sw(ctx, side);
-      MLH_TRY(tp.all_to_all(z[k], recv, M / tp.P * 16, "ntt_all_to_all"));
-      if (!inverse) MLH_TRY(mlh_shard_ntt_cross(ctx, recv, dev_out[i], log_n, tp.p, tp.rank, gen, 0));
-      else MLH_TRY(mlh_intt(ctx, recv, dev_out[i], log_n - tp.p, gp));
-    }
-    HIP_TRY(ctx, hipEventRecord(b_done[k], side));
+    StreamSwap sw(ctx, side);  // recv[k] is free: C(i - 2) finished (c_done waited below)
+    MLH_TRY(tp.all_to_all(z[k], recv[k], M / tp.P * 16, "ntt_all_to_all"));
+    HIP_TRY(ctx, hipEventRecord(x_done[k], side));
+    return MLH_OK;
+  };
+  auto step_c = [&](uint32_t i) -> mlh_status {
+    const int k = i & 1;
+    HIP_TRY(ctx, hipStreamWaitEvent(main, x_done[k], 0));
+    if (!inverse) MLH_TRY(mlh_shard_ntt_cross(ctx, recv[k], dev_out[i], log_n, tp.p, tp.rank, gen, 0));
+    else MLH_TRY(mlh_intt(ctx, recv[k], dev_out[i], log_n - tp.p, gp));
+    HIP_TRY(ctx, hipEventRecord(c_done[k], main));
+    HIP_TRY(ctx, hipStreamWaitEvent(side, c_done[k], 0));  // before the exchange of i + 2 fills recv[k]
+    return MLH_OK;
+  };
+  for (uint32_t i = 0; i < count; ++i) {
+    MLH_TRY(step_a(i));  // (z[i & 1] was sent: C(i - 2) waited for that exchange)
+    if (i >= 1) MLH_TRY(step_c(i - 1));
   }
+  MLH_TRY(step_c(count - 1));
   return MLH_OK;  // (join: main waits for the side stream)
 }
 

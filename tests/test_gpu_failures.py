@@ -69,9 +69,13 @@ def test_sumcheck_spin_timeout_is_an_error(n):
     ev, pts, total = _sumcheck_case(n, 700 + n)
     with spin_limit(1):
         t = MS.SumcheckTables.build_tables_for_pcs(pts, D.to_device(D.ints_to_limbs(ev)))
+        bad_tr = Transcript()
+        bad_tr.absorb(b"prefix")
+        before = bad_tr.random()
         with pytest.raises(_lib.MlhError) as ei:
-            t.compute_sumcheck_polynomials(total, Transcript())
+            t.compute_sumcheck_polynomials(total, bad_tr)
         assert ei.value.status == _lib.MLH_ERR_DEVICE
+        assert bad_tr.random() == before  # a rejected prove leaves the transcript untouched
     # the same context at the default limit: bit-exact, and no stale error
     want_polys, want_rs, otr = _oracle_rounds(ev, pts, total)
     t = MS.SumcheckTables.build_tables_for_pcs(pts, D.to_device(D.ints_to_limbs(ev)))
@@ -149,3 +153,37 @@ def test_gen_pows_verify_large_table_from_device():
     raw[16 * i] ^= 1
     st, _, _, msg = _verify(bytes(raw))
     assert st == _lib.MLH_ERR_INVALID and "gen_pows[%d]" % i in msg, msg
+
+
+def test_batched_pcs_device_failure_restores_transcript():
+    """The batched PCS absorbs its claim on the host before the device rounds;
+    when those rounds fail (cooperative path forced, spin limit of one sleep)
+    the caller's transcript is restored to its state at entry (mlhip.h), and
+    the next prove at the default limit equals the oracle-checked one."""
+    from multilinear_amd.batched import BatchedPCSProof
+
+    n, m = 13, 2
+    r = random.Random(79)
+    polys = [[r.randrange(F.M) for _ in range(1 << n)] for _ in range(m)]
+    pts = [r.randrange(F.M) for _ in range(n)]
+    outs = [OPL.mle_evaluate(p, pts) for p in polys]
+    evd = D.to_device(D.ints_to_limbs([v for p in polys for v in p]))
+    ctx = D.context()
+    D.check(D.lib().mlh_set_pcs_fused_max(ctx, 0), ctx)
+    try:
+        with spin_limit(1):
+            tr = Transcript()
+            tr.absorb(b"abc")
+            before = tr.random()
+            with pytest.raises(_lib.MlhError) as ei:
+                BatchedPCSProof.prove(pts, outs, evd, tr)
+            assert ei.value.status == _lib.MLH_ERR_DEVICE
+            assert tr.random() == before
+            with pytest.raises(_lib.MlhError) as ei:
+                MP.PCSProof.prove(pts, outs[0], evd[: 1 << n], tr)
+            assert ei.value.status == _lib.MLH_ERR_DEVICE
+            assert tr.random() == before
+        good = BatchedPCSProof.prove(pts, outs, evd, Transcript())
+        assert good.verify(Transcript())
+    finally:
+        D.check(D.lib().mlh_set_pcs_fused_max(ctx, 24), ctx)
