@@ -380,6 +380,38 @@ mlh_status mlh_batched_fri_prove(mlh_ctx* ctx, const void* dev_codes, uint32_t n
                                  mlh_batched_fri_proof* proof);
 /* BatchedFriProof::verify (batched_fri.rs:313-388), host side. */
 mlh_status mlh_batched_fri_verify(const mlh_batched_fri_proof* proof);
+/* BatchedFriProverData step by step (batched_fri.rs:9-224), the transcript on
+ * the host: what BatchedFriProverData::fold (:178-205) and BatchedPCSProverData
+ * (batched_pcs.rs:80-125) call.
+ *  - init (:41-98): batch layer of the m codes' RS pairs (dev_codes = the codes
+ *    back to back, 2^log_code each, kept by the caller while the prover lives),
+ *    absorb its root, fingerprint_r = next_challenge(), absorb LE16 of it;
+ *  - fold_step_gp = batched_fold_step(&mut self, gen_pows, r, transcript)
+ *    (:100-176): fingerprinted pairs folded with k = 0 and twiddle
+ *    gen_pows[len - i], then the folded layer's tree (or, at 4 elements, the
+ *    last element) into fri_data, and its root (last element) absorbed; a
+ *    second call is MLH_ERR_INVALID (the reference would fold the batch layer
+ *    again);
+ *  - inner = &mut self.fri_data: the FriProverData whose fold_step(gen_pows, k,
+ *    r, tr) the reference calls for k >= 1 (:200) -- pass it to
+ *    mlh_fri_prover_fold_step(_gp), _roots, _last_element, _open_query(ies);
+ *    owned by the batched prover (do not destroy it);
+ *  - open_query = open_query_at (:207-224): one record in the
+ *    mlh_batched_fri_query_bytes layout (inner part zero where fri_data has
+ *    no tree yet). */
+typedef struct mlh_batched_fri_prover mlh_batched_fri_prover;
+mlh_status mlh_batched_fri_prover_init(mlh_ctx* ctx, const void* dev_codes, uint32_t num_codes,
+                                       uint32_t log_code, mlh_transcript* tr,
+                                       mlh_batched_fri_prover** out);
+mlh_status mlh_batched_fri_prover_fold_step_gp(mlh_ctx* ctx, mlh_batched_fri_prover* bp,
+                                               const uint8_t gen_pows_1[16], uint32_t log_gen_pows,
+                                               const uint8_t r[16], mlh_transcript* tr);
+mlh_fri_prover* mlh_batched_fri_prover_inner(mlh_batched_fri_prover* bp);
+mlh_status mlh_batched_fri_prover_batch_root(const mlh_batched_fri_prover* bp, uint8_t out[32]);
+mlh_status mlh_batched_fri_prover_fingerprint_r(const mlh_batched_fri_prover* bp, uint8_t out[16]);
+mlh_status mlh_batched_fri_prover_open_query(mlh_ctx* ctx, const mlh_batched_fri_prover* bp,
+                                             uint64_t index, uint8_t* out);
+void mlh_batched_fri_prover_destroy(mlh_batched_fri_prover* bp);
 typedef struct mlh_batched_pcs_proof {
   mlh_batched_fri_proof fri;
   uint8_t* sumcheck_polys; /* [n_vars][2][16] */

@@ -161,6 +161,13 @@ SIGNATURES = {
     "mlh_merkle_verify": (_I, [_P, _U64, _P, _U32, _U64, _P, _U64]),
     "mlh_batched_fri_query_bytes": (_U64, [_U32, _U32]),
     "mlh_batched_fri_prove": (_I, [_P, _P, _U32, _U32, _P, ctypes.POINTER(BatchedFriProofC)]),
+    "mlh_batched_fri_prover_init": (_I, [_P, _P, _U32, _U32, _P, ctypes.POINTER(_P)]),
+    "mlh_batched_fri_prover_fold_step_gp": (_I, [_P, _P, _P, _U32, _P, _P]),
+    "mlh_batched_fri_prover_inner": (_P, [_P]),
+    "mlh_batched_fri_prover_batch_root": (_I, [_P, _P]),
+    "mlh_batched_fri_prover_fingerprint_r": (_I, [_P, _P]),
+    "mlh_batched_fri_prover_open_query": (_I, [_P, _P, ctypes.c_uint64, _P]),
+    "mlh_batched_fri_prover_destroy": (None, [_P]),
     "mlh_batched_fri_verify": (_I, [ctypes.POINTER(BatchedFriProofC)]),
     "mlh_batched_pcs_prove": (_I, [_P, _P, _U32, _U32, _P, _P, _P,
                                    ctypes.POINTER(BatchedPcsProofC)]),

@@ -6,7 +6,7 @@ include/mlhip.h (mlh_batched_fri_proof)."""
 import ctypes
 
 from . import _lib
-from .device import check, context, fe_from_bytes, lib, ptr
+from .device import check, context, fe_bytes, fe_from_bytes, lib, ptr
 
 NUM_QUERIES = _lib.NUM_QUERIES
 
@@ -129,3 +129,62 @@ class BatchedPCSProof:
         c.sumcheck_polys = ctypes.cast(self._polys, ctypes.c_void_p)
         return lib().mlh_batched_pcs_verify(ctypes.byref(c), self.n_vars, _fes(self.inputs),
                                             _fes(self.outputs), transcript.h) == 0
+
+
+class BatchedFriProverData:
+    """BatchedFriProverData (batched_fri.rs:9-224) step by step on the device,
+    the transcript on the host.  codes: (m * 2^L, 4) device tensor (outlives it)."""
+
+    def __init__(self, handle, codes, m, log_code):
+        self.h, self._codes, self.m, self.log_code = handle, codes, m, log_code
+
+    def __del__(self):
+        try:
+            lib().mlh_batched_fri_prover_destroy(self.h)
+        except Exception:
+            pass
+
+    @staticmethod
+    def init(codes, m, transcript, device=0):
+        """batched_fri.rs:41-98."""
+        ctx = context(device)
+        n = codes.shape[0] // m
+        assert n * m == codes.shape[0]
+        h = ctypes.c_void_p()
+        check(lib().mlh_batched_fri_prover_init(ctx, ptr(codes), m, _log2(n), transcript.h,
+                                                ctypes.byref(h)), ctx)
+        return BatchedFriProverData(h.value, codes, m, _log2(n))
+
+    def batched_fold_step(self, gen_pows, r, transcript, device=0):
+        """batched_fold_step(gen_pows, r, transcript) (batched_fri.rs:100-176);
+        gen_pows = (gen_pows[1], log2(gen_pows.len()))."""
+        ctx = context(device)
+        check(lib().mlh_batched_fri_prover_fold_step_gp(ctx, self.h, fe_bytes(gen_pows[0]), gen_pows[1],
+                                                        fe_bytes(r), transcript.h), ctx)
+
+    @property
+    def fri_data(self):
+        """self.fri_data: the inner FriProverData (a view; this object owns it)."""
+        from .fri import FriProverData
+
+        return FriProverData(lib().mlh_batched_fri_prover_inner(self.h), self._codes, owned=False)
+
+    @property
+    def batch_root(self):
+        out = (ctypes.c_uint8 * 32)()
+        check(lib().mlh_batched_fri_prover_batch_root(self.h, out))
+        return bytes(out)
+
+    @property
+    def fingerprint_r(self):
+        out = (ctypes.c_uint8 * 16)()
+        check(lib().mlh_batched_fri_prover_fingerprint_r(self.h, out))
+        return fe_from_bytes(out)
+
+    def open_query_at(self, index, device=0):
+        """batched_fri.rs:207-224 -> the flat record (mlh_batched_fri_query_bytes)."""
+        ctx = context(device)
+        nb = lib().mlh_batched_fri_query_bytes(self.log_code, self.m)
+        buf = (ctypes.c_uint8 * nb)()
+        check(lib().mlh_batched_fri_prover_open_query(ctx, self.h, index, buf), ctx)
+        return bytes(buf)

@@ -2101,6 +2101,164 @@ mlh_status mlh_batched_fri_prove(mlh_ctx* ctx, const void* dev_codes, uint32_t n
   return batched_queries(ctx, lp, tr, proof);
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// BatchedFriProverData step by step (batched_fri.rs:9-224), host transcript:
+// init -> batched_fold_step(gen_pows, r, tr) -> the inner fri_data's
+// fold_step(gen_pows, k, r, tr) for k >= 1 (mlh_fri_prover_fold_step(_gp) on
+// the handle mlh_batched_fri_prover_inner returns) -> open_query_at.  The
+// whole-proof path (mlh_batched_fri_prove) keeps the transcript on the device.
+// ---------------------------------------------------------------------------
+struct mlh_batched_fri_prover {
+  mlh_ctx* ctx;
+  const fe* codes = nullptr;  // caller's [m][N], must outlive the prover
+  uint32_t m = 0, log_code = 0;
+  void* btree = nullptr;      // batch layer: N/2 leaves + levels
+  void* scal = nullptr;       // device [fingerprint_r | r]
+  uint8_t broot[32];
+  uint8_t fr[16];
+  mlh_fri_prover inner;       // fri_data: merkle_trees start at the folded layer
+  ~mlh_batched_fri_prover() {
+    pool_free(ctx, btree);
+    pool_free(ctx, scal);
+  }
+};
+
+extern "C" {
+
+mlh_status mlh_batched_fri_prover_init(mlh_ctx* ctx, const void* dev_codes, uint32_t num_codes,
+                                       uint32_t log_code, mlh_transcript* tr, mlh_batched_fri_prover** out) {
+  if (!ctx || !dev_codes || !tr || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (num_codes == 0) return fail(ctx, MLH_ERR_INVALID, "Codes must not be empty");
+  if (log_code < 2 || log_code > 40)
+    return fail(ctx, MLH_ERR_NOT_POW2, "Code size must be a power of two (>= 4)");
+  std::unique_ptr<mlh_batched_fri_prover> bp(new mlh_batched_fri_prover());
+  bp->ctx = ctx;
+  bp->codes = reinterpret_cast<const fe*>(dev_codes);
+  bp->m = num_codes;
+  bp->log_code = log_code;
+  bp->inner.ctx = ctx;
+  bp->inner.log_code = log_code - 1;  // its first tree is the folded layer's
+  bp->inner.gp_gen = h_pow2_generator(log_code);  // the batched code's domain
+  bp->inner.log_gp = log_code;
+  const uint64_t N = 1ull << log_code, L = N / 2;
+  MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &bp->btree));
+  MLH_TRY(pool_alloc(ctx, 32, &bp->scal));
+  uint8_t* bt = reinterpret_cast<uint8_t*>(bp->btree);
+  HIP_TRY(ctx, launch_batch_pairs_leaves(bp->codes, num_codes, N, bt, ctx->stream));
+  HIP_TRY(ctx, launch_merkle_levels(bt, L, ctx->stream));
+  MLH_TRY(read_root(ctx, bt, L, bp->broot));
+  // batched_fri.rs:82-89: absorb the root, fingerprint_r = next_challenge(),
+  // absorb LE16(fingerprint_r)
+  mlh_transcript_absorb(tr, bp->broot, 32);
+  mlh_transcript_next_challenge(tr, bp->fr);
+  mlh_transcript_absorb(tr, bp->fr, 16);
+  *out = bp.release();
+  return MLH_OK;
+}
+
+mlh_status mlh_batched_fri_prover_fold_step_gp(mlh_ctx* ctx, mlh_batched_fri_prover* bp,
+                                               const uint8_t gen_pows_1[16], uint32_t log_gen_pows,
+                                               const uint8_t r[16], mlh_transcript* tr) {
+  if (!ctx || !bp || !gen_pows_1 || !r || !tr) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  if (log_gen_pows < 1 || log_gen_pows > 40) return fail(ctx, MLH_ERR_INVALID, "gen_pows length");
+  const u128 g = h_load(gen_pows_1);
+  if (!check_generator(g, log_gen_pows))
+    return fail(ctx, MLH_ERR_BAD_GENERATOR, "gen_pows[1] must have order exactly gen_pows.len()");
+  const uint64_t N = 1ull << bp->log_code, half_n = N / 2;
+  if (N <= (1ull << MLH_LOG_BLOWUP)) return MLH_OK;  // batched_fri.rs:104-106
+  if (half_n - 1 > (1ull << log_gen_pows))
+    return fail(ctx, MLH_ERR_INVALID, "gen_pows index len - i underflows (batched_fri.rs:131-136)");
+  // (called again, the reference folds the batch layer again and pushes a
+  // second tree onto fri_data; this binding folds it once)
+  if (!bp->inner.layers.empty() || bp->inner.has_last)
+    return fail(ctx, MLH_ERR_INVALID, "batched_fold_step already applied");
+  const fe *tlo, *thi;
+  MLH_TRY(fold_tables_g(ctx, g, log_gen_pows, &tlo, &thi));
+  memcpy(ctx->pinned, bp->fr, 16);
+  memcpy(ctx->pinned + 16, r, 16);
+  fe* sc = reinterpret_cast<fe*>(bp->scal);
+  HIP_TRY(ctx, hipMemcpyAsync(sc, ctx->pinned, 32, hipMemcpyHostToDevice, ctx->stream));
+  void* vals;
+  MLH_TRY(pool_alloc(ctx, half_n * sizeof(fe), &vals));
+  if (half_n == (1ull << MLH_LOG_BLOWUP)) {  // batched_fri.rs:152-162
+    HIP_TRY(ctx, launch_batched_fold_leaves(bp->codes, bp->m, N, sc, sc + 1, tlo, thi,
+                                            reinterpret_cast<fe*>(vals), nullptr, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, vals, 32, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    pool_free(ctx, vals);
+    if (memcmp(ctx->pinned, ctx->pinned + 16, 16) != 0)
+      return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
+    memcpy(bp->inner.last, ctx->pinned, 16);
+    bp->inner.has_last = true;
+    mlh_transcript_absorb(tr, bp->inner.last, 16);
+    return MLH_OK;
+  }
+  FriLayer nx;
+  nx.log_n = bp->log_code - 1;
+  nx.owned_values = vals;
+  nx.values = reinterpret_cast<const fe*>(vals);
+  const uint64_t leaves = half_n / 2;
+  void* tree;
+  MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(leaves), &tree));
+  nx.tree = reinterpret_cast<uint8_t*>(tree);
+  bp->inner.layers.push_back(nx);  // owned by inner from here on (freed by its destructor)
+  HIP_TRY(ctx, launch_batched_fold_leaves(bp->codes, bp->m, N, sc, sc + 1, tlo, thi,
+                                          reinterpret_cast<fe*>(vals), nx.tree, ctx->stream));
+  HIP_TRY(ctx, launch_merkle_levels(nx.tree, leaves, ctx->stream));
+  MLH_TRY(read_root(ctx, nx.tree, leaves, bp->inner.layers.back().root));
+  mlh_transcript_absorb(tr, bp->inner.layers.back().root, 32);
+  return MLH_OK;
+}
+
+mlh_fri_prover* mlh_batched_fri_prover_inner(mlh_batched_fri_prover* bp) {
+  return bp ? &bp->inner : nullptr;
+}
+
+mlh_status mlh_batched_fri_prover_batch_root(const mlh_batched_fri_prover* bp, uint8_t out[32]) {
+  if (!bp || !out) return MLH_ERR_INVALID;
+  memcpy(out, bp->broot, 32);
+  return MLH_OK;
+}
+
+mlh_status mlh_batched_fri_prover_fingerprint_r(const mlh_batched_fri_prover* bp, uint8_t out[16]) {
+  if (!bp || !out) return MLH_ERR_INVALID;
+  memcpy(out, bp->fr, 16);
+  return MLH_OK;
+}
+
+mlh_status mlh_batched_fri_prover_open_query(mlh_ctx* ctx, const mlh_batched_fri_prover* bp,
+                                             uint64_t index, uint8_t* out) {
+  if (!ctx || !bp || !out) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  const uint32_t L = bp->log_code;
+  if (index >= (1ull << (L - 1))) return fail(ctx, MLH_ERR_INVALID, "index out of bounds");
+  const uint64_t qbytes = mlh_batched_fri_query_bytes(L, bp->m);
+  uint8_t* h;
+  MLH_TRY(query_stage(ctx, qbytes, &h));
+  mlh::QueryIdx qi;
+  memset(&qi, 0, sizeof(qi));
+  qi.v[0] = index;
+  HIP_TRY(ctx, launch_batch_queries(bp->codes, bp->m, 1ull << L, reinterpret_cast<const uint8_t*>(bp->btree),
+                                    qi, 1, qbytes, h, ctx->stream));
+  // the inner paths at index mod N/4 (batched_fri.rs:215-221; the gather
+  // reduces the index per tree); zero where the inner prover has fewer trees
+  const uint64_t base = 32ull * bp->m + 32ull * (L - 1);
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  memset(h + base, 0, qbytes - base);
+  MLH_TRY(gather_queries_dev(ctx, &bp->inner, qi, nullptr, 1, qbytes, base, h));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(out, h, qbytes);
+  return MLH_OK;
+}
+
+void mlh_batched_fri_prover_destroy(mlh_batched_fri_prover* bp) {
+  if (bp) {
+    (void)hipStreamSynchronize(bp->ctx->stream);
+    delete bp;
+  }
+}
+
 mlh_status mlh_batched_pcs_prove(mlh_ctx* ctx, const void* dev_evals, uint32_t num_polys,
                                  uint32_t n_vars, const uint8_t* inputs, const uint8_t* outputs,
                                  mlh_transcript* tr, mlh_batched_pcs_proof* proof) {

@@ -46,11 +46,14 @@ def fold_layer(layer, k, log_domain, r, device=0):
 class FriProverData:
     """fri/mod.rs:10-175, device resident.  The code tensor must outlive it."""
 
-    def __init__(self, handle, code):
+    def __init__(self, handle, code, owned=True):
         self.h = handle
         self._code = code
+        self._owned = owned  # False: a view of a handle another object owns
 
     def __del__(self):
+        if not getattr(self, "_owned", True):
+            return
         try:
             lib().mlh_fri_prover_destroy(self.h)
         except Exception:

@@ -1083,6 +1083,46 @@ def test_batched_fri_prove_matches_oracle(m, log_n):
     assert got.verify()
 
 
+@pytest.mark.parametrize("m,log_n", [(3, 6), (1, 3), (2, 1), (4, 10), (10, 2)])
+def test_batched_fri_prover_step_api_reference_shape(m, log_n):
+    """BatchedFriProverData::fold (batched_fri.rs:178-205) written as the
+    reference writes it, through the step API: init; r = next_challenge;
+    batched_fold_step(gen_pows, r, tr); then fri_data.fold_step(gen_pows, k, r,
+    tr) for k >= 1 (:200) on the inner FriProverData -- against oracle/batched.py
+    after every step (batch root, fingerprint_r, inner roots, last element,
+    transcript) and open_query_at records at both ends and a middle index."""
+    from multilinear_amd.batched import BatchedFriProverData
+    from oracle import batched as OB
+
+    L = log_n + 1
+    gp = F.pow_2_generator_powers(L)
+    codes = [OF.reed_solomon([F.from_i64(7 * i + 3 + 100 * j) for i in range(1 << log_n)], gp[1])
+             for j in range(m)]
+    otr, tr = OT.Transcript(), Transcript()
+    opd = OB.BatchedFriProverData.init(codes, otr)
+    bp = BatchedFriProverData.init(dev([v for c in codes for v in c]), m, tr)
+    assert bp.batch_root == opd.batch_layer.root() and bp.fingerprint_r == opd.fingerprint_r
+    assert tr.random() == otr.random()
+    r = tr.next_challenge()
+    assert r == otr.next_challenge()
+    opd.batched_fold_step(gp, r, otr)
+    bp.batched_fold_step((gp[1], L), r, tr)
+    fd = bp.fri_data
+    assert fd.fold_roots() == opd.fri_data.fold_roots() and tr.random() == otr.random()
+    for k in range(1, L - 1):
+        r = tr.next_challenge()
+        opd.fri_data.fold_step(gp, k, r, otr)
+        fd.fold_step(k, r, tr, gen_pows=(gp[1], L))
+        assert fd.fold_roots() == opd.fri_data.fold_roots(), k
+        assert tr.random() == otr.random(), k
+    assert fd.last_element == opd.fri_data.last_element is not None
+    for idx in sorted({0, (1 << log_n) - 1, (1 << log_n) // 3}):
+        want = _flat_batched_queries(type("P", (), {"queries": [opd.open_query_at(idx)]})())
+        assert bp.open_query_at(idx) == want, idx
+    with pytest.raises(_lib.MlhError):  # a second batched step: rejected, not re-folded
+        bp.batched_fold_step((gp[1], L), r, tr)
+
+
 def test_batched_fri_large_verifies():
     from multilinear_amd.batched import BatchedFriProof
 
