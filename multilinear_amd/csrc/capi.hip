@@ -737,16 +737,15 @@ static mlh_status fold_step_impl(mlh_ctx* ctx, mlh_fri_prover* p, u128 gen, uint
   const fe rr = to_fe(h_load(r));
   FriLayer nx;
   nx.log_n = log_n - 1;
-  void* vals;
-  MLH_TRY(pool_alloc(ctx, half_n * sizeof(fe), &vals));
-  nx.owned_values = vals;
+  PoolBuf vb(ctx), tb(ctx);  // released into the new layer on success only
+  MLH_TRY(vb.alloc(half_n * sizeof(fe)));
+  void* vals = vb.p;
   nx.values = reinterpret_cast<const fe*>(vals);
   if (half_n == blowup) {  // fri/mod.rs:116-126
     HIP_TRY(ctx, launch_fri_fold(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), rr, tlo,
                                  thi, k, 1ull << log_gp, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, vals, 32, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    pool_free(ctx, vals);
     if (memcmp(ctx->pinned, ctx->pinned + 16, 16) != 0)
       return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
     memcpy(p->last, ctx->pinned, 16);
@@ -755,13 +754,14 @@ static mlh_status fold_step_impl(mlh_ctx* ctx, mlh_fri_prover* p, u128 gen, uint
     return MLH_OK;
   }
   const uint64_t L = half_n / 2;
-  void* tree;
-  MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(L), &tree));
-  nx.tree = reinterpret_cast<uint8_t*>(tree);
+  MLH_TRY(tb.alloc(mlh_merkle_layers_bytes(L)));
+  nx.tree = tb.as<uint8_t>();
   HIP_TRY(ctx, launch_fri_fold_commit(cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals),
                                       nx.tree, rr, tlo, thi, k, 1ull << log_gp,
                                       ctx->stream));
   MLH_TRY(read_root(ctx, nx.tree, L, nx.root));
+  nx.owned_values = vb.release();
+  tb.release();
   p->layers.push_back(nx);
   mlh_transcript_absorb(tr, p->layers.back().root, 32);
   return MLH_OK;
@@ -2180,14 +2180,14 @@ mlh_status mlh_batched_fri_prover_fold_step_gp(mlh_ctx* ctx, mlh_batched_fri_pro
   memcpy(ctx->pinned + 16, r, 16);
   fe* sc = reinterpret_cast<fe*>(bp->scal);
   HIP_TRY(ctx, hipMemcpyAsync(sc, ctx->pinned, 32, hipMemcpyHostToDevice, ctx->stream));
-  void* vals;
-  MLH_TRY(pool_alloc(ctx, half_n * sizeof(fe), &vals));
+  PoolBuf vb(ctx), tb(ctx);  // released into fri_data on success only
+  MLH_TRY(vb.alloc(half_n * sizeof(fe)));
+  void* vals = vb.p;
   if (half_n == (1ull << MLH_LOG_BLOWUP)) {  // batched_fri.rs:152-162
     HIP_TRY(ctx, launch_batched_fold_leaves(bp->codes, bp->m, N, sc, sc + 1, tlo, thi,
                                             reinterpret_cast<fe*>(vals), nullptr, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, vals, 32, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    pool_free(ctx, vals);
     if (memcmp(ctx->pinned, ctx->pinned + 16, 16) != 0)
       return fail(ctx, MLH_ERR_NOT_RS_CODE, "not an RS code");
     memcpy(bp->inner.last, ctx->pinned, 16);
@@ -2197,17 +2197,17 @@ mlh_status mlh_batched_fri_prover_fold_step_gp(mlh_ctx* ctx, mlh_batched_fri_pro
   }
   FriLayer nx;
   nx.log_n = bp->log_code - 1;
-  nx.owned_values = vals;
   nx.values = reinterpret_cast<const fe*>(vals);
   const uint64_t leaves = half_n / 2;
-  void* tree;
-  MLH_TRY(pool_alloc(ctx, mlh_merkle_layers_bytes(leaves), &tree));
-  nx.tree = reinterpret_cast<uint8_t*>(tree);
-  bp->inner.layers.push_back(nx);  // owned by inner from here on (freed by its destructor)
+  MLH_TRY(tb.alloc(mlh_merkle_layers_bytes(leaves)));
+  nx.tree = tb.as<uint8_t>();
   HIP_TRY(ctx, launch_batched_fold_leaves(bp->codes, bp->m, N, sc, sc + 1, tlo, thi,
                                           reinterpret_cast<fe*>(vals), nx.tree, ctx->stream));
   HIP_TRY(ctx, launch_merkle_levels(nx.tree, leaves, ctx->stream));
-  MLH_TRY(read_root(ctx, nx.tree, leaves, bp->inner.layers.back().root));
+  MLH_TRY(read_root(ctx, nx.tree, leaves, nx.root));
+  nx.owned_values = vb.release();  // owned by fri_data from here on (its destructor frees them)
+  tb.release();
+  bp->inner.layers.push_back(nx);
   mlh_transcript_absorb(tr, bp->inner.layers.back().root, 32);
   return MLH_OK;
 }

@@ -291,6 +291,11 @@ struct PoolBuf {
   explicit PoolBuf(mlh_ctx* c) : ctx(c) {}
   ~PoolBuf() { pool_free(ctx, p); }
   mlh_status alloc(size_t bytes) { return pool_alloc(ctx, bytes, &p); }
+  void* release() {  // ownership passes to the caller
+    void* q = p;
+    p = nullptr;
+    return q;
+  }
   template <class T>
   T* as() const {
     return reinterpret_cast<T*>(p);
