@@ -21,6 +21,8 @@ import sys
 
 PASSES = {"ntt_pass_kernel<8, 0, 0, 8>": "pass 0", "ntt_pass_kernel<8, 1, 0, 8>": "pass 1",
           "ntt_pass_kernel<8, 2, 0, 8>": "last pass"}
+if os.environ.get("MLH_ATTRIB_KERNELS"):  # e.g. "leaf_pairs_level2_kernel,level2_kernel"
+    PASSES = {k: k for k in os.environ["MLH_ATTRIB_KERNELS"].split(",")}
 
 
 def load(d):
@@ -37,7 +39,9 @@ def load(d):
             dur[int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     out = {}
     for key in PASSES:
-        rows = [(did, cs) for did, cs in per.items() if ("mlh::" + key) in names[did]]
+        rows = [(did, cs) for did, cs in per.items()
+                if ("mlh::" + key + "(") in names[did] or ("mlh::" + key + "<") in names[did]
+                or names[did].endswith("mlh::" + key)]
         if not rows:
             continue
         avg = collections.defaultdict(float)
