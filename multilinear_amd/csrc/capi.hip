@@ -274,6 +274,7 @@ void mlh_context_destroy(mlh_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);  // before anything it may use is freed
+  if (ctx->side2) (void)hipStreamSynchronize(ctx->side2);
   resolve_profile(ctx);
   for (auto e : ctx->ev_free) (void)hipEventDestroy(e);
   for (auto& kv : ctx->tables) (void)hipFree(kv.second.d);
@@ -281,6 +282,7 @@ void mlh_context_destroy(mlh_ctx* ctx) {
   for (auto& kv : ctx->live) (void)hipFree(kv.first);
   (void)hipFree(ctx->ntt_scratch);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  if (ctx->side2) (void)hipStreamDestroy(ctx->side2);
   (void)hipFree(ctx->partials);
   (void)hipFree(ctx->small);
   (void)hipHostFree(ctx->pinned);

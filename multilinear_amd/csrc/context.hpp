@@ -73,6 +73,7 @@ struct mlh_ctx {
   fe* ntt_scratch = nullptr;          // NTT ping-pong buffer (grow-only)
   size_t ntt_scratch_bytes = 0;
   hipStream_t side = nullptr;         // second stream of pipelined calls (lazy)
+  hipStream_t side2 = nullptr;        // third stream (sharded NTT batch: the cross-shard step)
   // debug / test hooks, fixed at creation (MLH_DEBUG_SYNC) or set through the
   // API (mlh_set_ntt_plan): never read from the environment on a hot path
   bool debug_sync = false;

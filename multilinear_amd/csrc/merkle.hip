@@ -157,43 +157,6 @@ __global__ void __launch_bounds__(256)
 level2_kernel(const uint8_t* __restrict__ child, uint8_t* __restrict__ parent,
               uint8_t* __restrict__ grand, uint64_t ngrand) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-#ifndef MLH_L2_STAGED
-#define MLH_L2_STAGED 1
-#endif
-#if MLH_L2_STAGED
-  // A lane's 4 children are 128 consecutive bytes, so loading them directly
-  // makes every dwordx4 instruction touch 64 separate lines.  Each wave loads
-  // its 8 KiB run instead as 8 coalesced instructions (1 KiB each) into LDS,
-  // pieces XOR-swizzled by owner so the 128-B-strided reads spread over the
-  // banks, then takes its own 128 B from there.
-  __shared__ uint4 stg[256 * 8];
-  {
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t first = (uint64_t)blockIdx.x * blockDim.x + 64 * w;  // the wave's first lane
-    const uint64_t nv = first >= ngrand ? 0 : (ngrand - first < 64 ? ngrand - first : 64);
-    const uint4* src = reinterpret_cast<const uint4*>(child + first * 128);
-    uint4* ws = stg + w * 512;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t piece = (uint32_t)i * 64 + lane, owner = piece >> 3, part = piece & 7;
-      if (owner < nv) ws[owner * 8 + (part ^ (owner & 7))] = src[piece];
-    }
-  }
-  __syncthreads();
-  if (j >= ngrand) return;
-  const uint4* mine = stg + (threadIdx.x >> 6) * 512 + (threadIdx.x & 63) * 8;
-  const uint32_t sw = threadIdx.x & 7;
-  auto dig = [&](int d) {  // child d of this lane: parts 2d, 2d + 1
-    const uint4 a = mine[(2 * d) ^ sw], b = mine[(2 * d + 1) ^ sw];
-    return Sha256State{{bswap32(a.x), bswap32(a.y), bswap32(a.z), bswap32(a.w), bswap32(b.x),
-                        bswap32(b.y), bswap32(b.z), bswap32(b.w)}};
-  };
-  const Sha256State c0 = dig(0), c1 = dig(1);
-  const Sha256State p0 = sha256_node(c0, c1);
-  digest_store(parent + (2 * j) * 32, p0);
-  const Sha256State c2 = dig(2), c3 = dig(3);
-  const Sha256State p1 = sha256_node(c2, c3);
-#else
   if (j >= ngrand) return;
   const uint8_t* c = child + j * 128;
   const Sha256State c0 = digest_load(c), c1 = digest_load(c + 32);
@@ -201,7 +164,6 @@ level2_kernel(const uint8_t* __restrict__ child, uint8_t* __restrict__ parent,
   digest_store(parent + (2 * j) * 32, p0);
   const Sha256State c2 = digest_load(c + 64), c3 = digest_load(c + 96);
   const Sha256State p1 = sha256_node(c2, c3);
-#endif
   digest_store(parent + (2 * j + 1) * 32, p1);
   digest_store(grand + j * 32, sha256_node(p0, p1));
 }

@@ -324,19 +324,20 @@ mlh_status mlh_sharded_ntt(mlh_ctx* ctx, const mlh_transport* t, const void* dev
   return MLH_OK;
 }
 
-// `count` transforms, pipelined over two streams.  Only the exchange runs on
-// the context's side stream; both compute steps run on the context stream in
-// the order A(0) A(1) C(0) A(2) C(1) ... A(n-1) C(n-2) C(n-1), where A is the
-// first local step (forward: the local NTT; inverse: the cross-shard DFT) and
-// C the second (forward: the cross-shard DFT; inverse: the local INTT).  The
-// all-to-all of transform i therefore overlaps A(i+1) and C(i-1), and a step
-// costs max(A + C, all-to-all) instead of max(A, all-to-all + C) with C on the
-// exchange's stream (at P = 8 the 235 MB exchange is the longer
-// one).  Buffers: z[k] (A's output, sent) and recv[k] (received, C's input),
-// k = i mod 2; A(i+2) reuses z[k] only after C(i) (issued after the exchange
-// of i completed) and the exchange of i+2 reuses recv[k] only after C(i) read
-// it.  On return the context stream is ordered after every transform.  With a
-// host-side transport the transforms run one after another.
+// `count` transforms, pipelined over three streams: the first local step A
+// (forward: the local NTT; inverse: the cross-shard DFT) on the context
+// stream, the exchange on the side stream, the second local step C
+// (forward: the cross-shard DFT; inverse: the local INTT) on a third stream.
+// So A(i+1), the exchange of i and C(i-1) run at once, and a step costs about
+// max(A || C, exchange): the VALU-bound NTT and the HBM-bound cross-shard DFT
+// share the chip better side by side than in turn (0.566 ms
+// against 0.584 ms for the 2^24 NTT + the P = 8 cross step on one MI355X), and
+// C no longer sits behind the exchange on its stream (0.58-0.74 ms a step at
+// P = 8 for the xGMI rates assumed there).  Buffers: z[k] (A's output, sent)
+// and recv[k] (received, C's input), k = i mod 2; A(i+2) reuses z[k] after
+// the exchange of i sent it; the exchange of i+2 fills recv[k] after C(i) has
+// read it.  On return the context stream is ordered after every transform.
+// With a host-side transport the transforms run one after another.
 mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const void* const* dev_in,
                                  void* const* dev_out, uint32_t count, uint32_t log_n,
                                  const uint8_t gen[16], int inverse) {
@@ -355,6 +356,7 @@ mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const voi
   if (!gen_has_order(h_load(gen), log_n)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != n");
   if (!count) return MLH_OK;
   if (!ctx->side) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  if (!ctx->side2) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking));
   const uint64_t M = 1ull << (log_n - tp.p);
   uint8_t gp[16];
   store_fe(gp, h_pow(h_load(gen), (u128)tp.P));
@@ -374,49 +376,52 @@ mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const voi
     mlh_ctx* c;
     hipEvent_t* e;
     ~Recycle() {
-      for (int k = 0; k < 7; ++k) c->ev_free.push_back(e[k]);
+      for (int k = 0; k < 9; ++k) c->ev_free.push_back(e[k]);
     }
   };
-  hipEvent_t evs[7] = {a_done[0], a_done[1], x_done[0], x_done[1], c_done[0], c_done[1], take_event(ctx)};
+  hipEvent_t evs[9] = {a_done[0], a_done[1], x_done[0], x_done[1], c_done[0], c_done[1],
+                       take_event(ctx), take_event(ctx), take_event(ctx)};
   Recycle rec{ctx, evs};
-  hipStream_t main = ctx->stream, side = ctx->side;
+  hipStream_t main = ctx->stream, side = ctx->side, third = ctx->side2;
+  // the third stream starts after the caller's work (the side stream's first
+  // wait is on a_done, recorded on the context stream)
+  HIP_TRY(ctx, hipEventRecord(evs[8], main));
+  HIP_TRY(ctx, hipStreamWaitEvent(third, evs[8], 0));
   // On every exit, error paths included, the context stream waits for all the
-  // side stream's work: the pooled buffers (Bufs, released after this guard)
+  // side streams' work: the pooled buffers (Bufs, released after this guard)
   // and the events are reused only behind it.
   struct JoinSide {
-    hipStream_t main, side;
-    hipEvent_t e;
+    hipStream_t main, s1, s2;
+    hipEvent_t e1, e2;
     ~JoinSide() {
-      (void)hipEventRecord(e, side);
-      (void)hipStreamWaitEvent(main, e, 0);
+      (void)hipEventRecord(e1, s1);
+      (void)hipStreamWaitEvent(main, e1, 0);
+      (void)hipEventRecord(e2, s2);
+      (void)hipStreamWaitEvent(main, e2, 0);
     }
-  } join{main, side, evs[6]};
-  auto step_a = [&](uint32_t i) -> mlh_status {
+  } join{main, side, third, evs[6], evs[7]};
+  for (uint32_t i = 0; i < count; ++i) {
     const int k = i & 1;
+    if (i >= 2) HIP_TRY(ctx, hipStreamWaitEvent(main, x_done[k], 0));  // z[k] was sent
     if (!inverse) MLH_TRY(mlh_ntt(ctx, dev_in[i], z[k], log_n - tp.p, gp));
     else MLH_TRY(mlh_shard_ntt_cross(ctx, dev_in[i], z[k], log_n, tp.p, tp.rank, gen, 1));
     HIP_TRY(ctx, hipEventRecord(a_done[k], main));
     HIP_TRY(ctx, hipStreamWaitEvent(side, a_done[k], 0));
-    StreamSwap sw(ctx, side);  // recv[k] is free: C(i - 2) finished (c_done waited below)
-    MLH_TRY(tp.all_to_all(z[k], recv[k], M / tp.P * 16, "ntt_all_to_all"));
+    if (i >= 2) HIP_TRY(ctx, hipStreamWaitEvent(side, c_done[k], 0));  // C(i - 2) read recv[k]
+    {
+      StreamSwap sw(ctx, side);
+      MLH_TRY(tp.all_to_all(z[k], recv[k], M / tp.P * 16, "ntt_all_to_all"));
+    }
     HIP_TRY(ctx, hipEventRecord(x_done[k], side));
-    return MLH_OK;
-  };
-  auto step_c = [&](uint32_t i) -> mlh_status {
-    const int k = i & 1;
-    HIP_TRY(ctx, hipStreamWaitEvent(main, x_done[k], 0));
-    if (!inverse) MLH_TRY(mlh_shard_ntt_cross(ctx, recv[k], dev_out[i], log_n, tp.p, tp.rank, gen, 0));
-    else MLH_TRY(mlh_intt(ctx, recv[k], dev_out[i], log_n - tp.p, gp));
-    HIP_TRY(ctx, hipEventRecord(c_done[k], main));
-    HIP_TRY(ctx, hipStreamWaitEvent(side, c_done[k], 0));  // before the exchange of i + 2 fills recv[k]
-    return MLH_OK;
-  };
-  for (uint32_t i = 0; i < count; ++i) {
-    MLH_TRY(step_a(i));  // (z[i & 1] was sent: C(i - 2) waited for that exchange)
-    if (i >= 1) MLH_TRY(step_c(i - 1));
+    HIP_TRY(ctx, hipStreamWaitEvent(third, x_done[k], 0));
+    {
+      StreamSwap sw(ctx, third);
+      if (!inverse) MLH_TRY(mlh_shard_ntt_cross(ctx, recv[k], dev_out[i], log_n, tp.p, tp.rank, gen, 0));
+      else MLH_TRY(mlh_intt(ctx, recv[k], dev_out[i], log_n - tp.p, gp));
+    }
+    HIP_TRY(ctx, hipEventRecord(c_done[k], third));
   }
-  MLH_TRY(step_c(count - 1));
-  return MLH_OK;  // (join: main waits for the side stream)
+  return MLH_OK;  // (join: main waits for both side streams)
 }
 
 mlh_status mlh_sharded_reed_solomon(mlh_ctx* ctx, const mlh_transport* t, const void* dev_coeffs,

@@ -39,8 +39,9 @@ def main():
     ap.add_argument("--variants", default="copyk16,copyk32,copyk64,blit,sdma")
     ap.add_argument("--out", default=None)
     ap.add_argument("--with-cross", type=int, default=1,
-                    help="main-stream step = local NTT + the P-point cross-shard DFT (the "
-                         "mlh_sharded_ntt_batch schedule); 0: the NTT alone")
+                    help="1: main-stream step = local NTT + the P-point cross-shard DFT in turn; "
+                         "2: the cross-shard DFT concurrently on a third stream (of another "
+                         "buffer); 0: the NTT alone")
     ap.add_argument("--rounds", type=int, default=3, help="alternations of alone / variants")
     ap.add_argument("--warm-s", type=float, default=2.0, help="clock warm-up before measuring")
     args = ap.parse_args()
@@ -75,11 +76,19 @@ def main():
     lib.mlh_pow_2_generator(args.log_n + lp, gen_tot)
     crossed = D.empty(N)
 
+    sC = torch.cuda.Stream()
+    out2 = D.empty(N)
+
     def ntt():
         D.check(lib.mlh_ntt(ctx, D.ptr(x), D.ptr(out), args.log_n, gen), ctx)
-        if args.with_cross:  # the new schedule's main stream: local NTT + cross-shard DFT
+        if args.with_cross == 1:  # main stream: local NTT + cross-shard DFT, in turn
             D.check(lib.mlh_shard_ntt_cross(ctx, D.ptr(out), D.ptr(crossed), args.log_n + lp, lp, 0, gen_tot, 0),
                     ctx)
+        elif args.with_cross == 2:  # the cross-shard DFT on a stream of its own, concurrent
+            lib.mlh_set_stream(ctx, ctypes.c_void_p(sC.cuda_stream))
+            D.check(lib.mlh_shard_ntt_cross(ctx, D.ptr(out2), D.ptr(crossed), args.log_n + lp, lp, 0, gen_tot, 0),
+                    ctx)
+            lib.mlh_set_stream(ctx, ctypes.c_void_p(sA.cuda_stream))
 
     def copy(kind):
         st = ctypes.c_void_p(sB.cuda_stream)
@@ -129,6 +138,9 @@ def main():
             if with_ntt:
                 ntt()
         evA[1].record(sA)
+        if args.with_cross == 2:
+            sA.wait_stream(sC)
+            evA[1].record(sA)
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / K * 1e3
         lib.mlh_profile_enable(ctx, 0)
@@ -144,8 +156,10 @@ def main():
 
     res = {"tool": "tools/a2a_contention.py", "log_n": args.log_n, "projected_world": P,
            "bytes_per_step": nbytes, "steps": args.steps, "rounds": args.rounds,
-           "main_stream_step": "local NTT 2^%d + shard_dft<%d> (cross-shard DFT)" % (args.log_n, lp)
-           if args.with_cross else "local NTT 2^%d" % args.log_n,
+           "main_stream_step": {0: "local NTT 2^%d" % args.log_n,
+                                1: "local NTT 2^%d + shard_dft<%d> in turn" % (args.log_n, lp),
+                                2: "local NTT 2^%d || shard_dft<%d> on a third stream" % (args.log_n, lp)}
+                               [args.with_cross],
            "device": torch.cuda.get_device_name(0), "variants": {}}
     t_end = time.perf_counter() + args.warm_s  # clock ramp: the first loops run slow
     while time.perf_counter() < t_end:

@@ -95,7 +95,7 @@ def main():
                                                             ("lds_bank_conflict", "SQ_LDS_BANK_CONFLICT"))
                                   if c in a},
             "mean_resident_waves_per_sq": a["SQ_LEVEL_WAVES"] / a["SQ_BUSY_CYCLES"]
-            if a.get("SQ_BUSY_CYCLES") else None,
+            if a.get("SQ_LEVEL_WAVES") and a.get("SQ_BUSY_CYCLES") else None,  # (reads 0 on gfx950)
             "valu_issue_frac_4cycle": a["SQ_INSTS_VALU"] * 64 / (t * 256 * 4 * 16 * clk)
             if "SQ_INSTS_VALU" in a else None,
             "ta_busy_avr": a.get("TA_BUSY_avr"), "ta_busy_max": a.get("TA_BUSY_max"),
