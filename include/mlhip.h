@@ -568,6 +568,17 @@ mlh_status mlh_sharded_ntt(mlh_ctx* ctx, const mlh_transport* tp, const void* de
 mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* tp, const void* const* dev_in,
                                  void* const* dev_out, uint32_t count, uint32_t log_n,
                                  const uint8_t gen[16], int inverse);
+/* The same forward transforms with the rank digit fused into the last pass:
+ * the local passes but the last, ONE all-to-all, one pass over the received
+ * chunks -- three HBM passes per element instead of the local NTT's three plus
+ * the cross-shard DFT's.  Input cyclic (rank g holds x[g + P m]);
+ * output block-cyclic with block 2^(*log_s_out) (the plan's first digit minus
+ * log2 P: 6 at 2^27 over 8 ranks), i.e. local l of rank r is global
+ * ((l >> s) << (s + p)) | (r << s) | (l mod 2^s).  2 <= P <= 8; local size
+ * >= 2^(13 - log2 P).  Pipelined on three streams like mlh_sharded_ntt_batch. */
+mlh_status mlh_sharded_ntt_fused_batch(mlh_ctx* ctx, const mlh_transport* tp, const void* const* dev_in,
+                                       void* const* dev_out, uint32_t count, uint32_t log_n,
+                                       const uint8_t gen[16], uint32_t* log_s_out);
 /* reed_solomon (fri/mod.rs:19-28): 2^log_n coefficients in the cyclic layout,
  * gen of order 2^(log_n + 1) -> the codeword in block 2^(log_n + 1) / P^2. */
 mlh_status mlh_sharded_reed_solomon(mlh_ctx* ctx, const mlh_transport* tp, const void* dev_coeffs,

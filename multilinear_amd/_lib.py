@@ -220,6 +220,8 @@ SIGNATURES = {
     "mlh_gen_pows_verify": (_I, [_P, _P, _U64, _P, ctypes.POINTER(_U32)]),
     "mlh_sharded_ntt_batch": (_I, [_P, ctypes.POINTER(TransportC), ctypes.POINTER(_P),
                                    ctypes.POINTER(_P), _U32, _U32, _P, _I]),
+    "mlh_sharded_ntt_fused_batch": (_I, [_P, ctypes.POINTER(TransportC), ctypes.POINTER(_P),
+                                         ctypes.POINTER(_P), _U32, _U32, _P, ctypes.POINTER(_U32)]),
     "mlh_sharded_reed_solomon": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _P, _P]),
     "mlh_sharded_commit_rs_code": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _P]),
     "mlh_sharded_fri_prove": (_I, [_P, ctypes.POINTER(TransportC), _P, _U32, _U32, _P,

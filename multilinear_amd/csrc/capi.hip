@@ -30,6 +30,7 @@
 #include "host_sha256.hpp"
 #include "host_transcript.hpp"
 #include "context.hpp"
+#include "fused_ntt.hpp"
 #include "merkle.hpp"
 #include "ntt.hpp"
 #include "sha256.hpp"
@@ -124,7 +125,7 @@ static uint64_t hi_count(uint32_t log_n) {
 }
 
 static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool inverse,
-                                 NttTables* tb) {
+                                 NttTables* tb, const uint32_t* plan = nullptr, uint32_t nplan = 0) {
   const uint64_t N = 1ull << log_n;
   const u128 w = inverse ? h_inv(gen) : gen;
   const u128 scale = inverse ? h_inv((u128)N) : (u128)1;
@@ -136,7 +137,10 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
     return MLH_OK;
   }
   tb->debug_sync = ctx->debug_sync;
-  ntt_plan_radices(log_n, &tb->nradix, tb->logr, ctx->forced_plan, ctx->forced_plan_len);
+  if (plan)
+    ntt_plan_radices(log_n, &tb->nradix, tb->logr, plan, nplan);
+  else
+    ntt_plan_radices(log_n, &tb->nradix, tb->logr, ctx->forced_plan, ctx->forced_plan_len);
   for (uint32_t p = 0; p < tb->nradix; ++p) {
     const uint64_t R = 1ull << tb->logr[p];
     MLH_TRY(get_table(ctx, h_pow(w, N / R), R / 2, 1, &tb->tw[p], true));
@@ -198,6 +202,77 @@ static mlh_status ntt_network_core(mlh_ctx* ctx, const fe* in, fe* out, uint32_t
   const u128 scale = inverse ? h_inv((u128)1 << log_n) : (u128)1;
   HIP_TRY(ctx, launch_ntt_network(in, out, scratch, tlo, thi, log_n, zero_top, to_fe(scale), inverse,
                                   ctx->stream));
+  return MLH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Sharded NTT with the rank digit fused into the last pass (fused_ntt.hpp):
+// the global 2^L transform runs the plan (local digits..., c + p) where the
+// local 2^(L-p) array of rank g (cyclic: global index P m + g) takes the
+// passes before the last one exactly as a local NTT with plan (local digits...,
+// c) would, except that each inter-pass table row k carries the extra factor
+// (w_N^S)^(k g) (the global column index is P j + g); the last pass transforms
+// the low (c + p) bits of the global index -- c local bits and the p rank bits
+// -- on the all-to-all's receive buffer.  Three HBM passes instead of the
+// local NTT's three plus the cross-shard DFT's one.
+FusedNtt::~FusedNtt() {
+  for (void* q : scaled) pool_free(ctx, q);
+}
+
+mlh_status FusedNtt::prepare(mlh_ctx* c, u128 gen, uint32_t log_n, uint32_t log_p, uint32_t rank_) {
+  ctx = c;
+  L = log_n;
+  p = log_p;
+  rank = rank_;
+  const uint32_t Lloc = L - p;
+  const uint32_t cl = 9 - p;  // local bits of the last digit: the fused radix is 2^9
+  if (p < 1 || p > 4 || cl < 4 || Lloc < cl + 4 || Lloc > 40) return fail(ctx, MLH_ERR_INVALID, "fused plan");
+  uint32_t npre = 0, pre[kMaxPasses];
+  ntt_plan_radices(Lloc - cl, &npre, pre);
+  if (npre + 1 > (uint32_t)kMaxPasses || pre[0] < p + 3) return fail(ctx, MLH_ERR_INVALID, "fused plan");
+  uint32_t plan[kMaxPasses];
+  for (uint32_t i = 0; i < npre; ++i) plan[i] = pre[i];
+  plan[npre] = cl;
+  // the local plan as a forced plan needs digits 4..9 (ntt_plan_radices)
+  for (uint32_t i = 0; i <= npre; ++i)
+    if (plan[i] < 4 || plan[i] > 9) return fail(ctx, MLH_ERR_INVALID, "fused plan");
+  const u128 gl = h_pow(gen, (u128)1 << p);  // the local generator w_N^P
+  MLH_TRY(get_ntt_tables(ctx, gl, Lloc, false, &loc, plan, npre + 1));
+  if (loc.nradix != npre + 1) return fail(ctx, MLH_ERR_INVALID, "fused plan");
+  nglob = npre + 1;
+  for (uint32_t i = 0; i < npre; ++i) logr[i] = plan[i];
+  logr[npre] = cl + p;
+  // rank twist of the pre-exchange passes' TA rows: (w_N^S)^(k rank)
+  uint64_t S = 1;
+  for (uint32_t i = 0; i < npre; ++i) {
+    const uint64_t R = 1ull << plan[i];
+    void* q;
+    MLH_TRY(pool_alloc(ctx, (R << loc.loga[i]) * sizeof(fe), &q));
+    scaled.push_back(q);
+    const u128 rb = h_pow(gen, (u128)S * rank);
+    HIP_TRY(ctx, launch_scale_rows(loc.ta[i], reinterpret_cast<fe*>(q), R, loc.loga[i], to_fe(rb), ctx->stream));
+    loc.ta[i] = reinterpret_cast<const fe*>(q);
+    S <<= plan[i];
+  }
+  // the fused last pass's stage twiddles: w_N^(N / 2^9), expanded
+  const uint64_t Rl = 1ull << logr[npre];
+  MLH_TRY(get_table(ctx, h_pow(gen, (u128)(1ull << (L - logr[npre]))), Rl / 2, 1, &tw_last, true));
+  return MLH_OK;
+}
+
+mlh_status FusedNtt::run_pre(const void* in, void* out) {
+  ProfScope ps(ctx, "ntt_fused_pre");
+  HIP_TRY(ctx, launch_ntt_passes_pre(reinterpret_cast<const fe*>(in), reinterpret_cast<fe*>(out), loc, L - p,
+                                     nglob - 1, ctx->stream));
+  ps.end();
+  return MLH_OK;
+}
+
+mlh_status FusedNtt::run_last(const void* recv, void* out) {
+  ProfScope ps(ctx, "ntt_fused_last");
+  HIP_TRY(ctx, launch_ntt_shard_last(reinterpret_cast<const fe*>(recv), reinterpret_cast<fe*>(out), tw_last,
+                                     logr, nglob, L, p, rank, ctx->stream));
+  ps.end();
   return MLH_OK;
 }
 

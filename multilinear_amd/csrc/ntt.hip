@@ -57,6 +57,9 @@ struct PassGeom {
   uint32_t ltpv;        // tiles per vector (batched transforms: blockIdx.x = b*2^ltpv + tile)
   uint32_t lin_v;       // elements between consecutive input vectors
   uint32_t lout_v;      // elements between consecutive output vectors
+  // TW 4 (the sharded NTT's fused last pass, mlh_sharded_ntt_fused_batch):
+  // log2 P, this rank, log2 of the per-source chunk of the receive buffer
+  uint32_t sh_p = 0, sh_rank = 0, sh_lchunk = 0;
 };
 
 // Last pass: natural output index is K = k_1 + R_1*rev(mid) + (N/R_P)*k_P,
@@ -76,7 +79,11 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 
 // TW: 0 = two-table twiddle (TA * TB), 1 = one table (TA), 2 = none (last pass),
 // 3 = one table on pass 0 (same code as 1; its own kernel so that rocprof and
-// the kernel timer tell the first pass from the middle ones)
+// the kernel timer tell the first pass from the middle ones), 4 = the last
+// pass of a sharded transform (as 2, over this rank's share of the global
+// tiles, reading the all-to-all's receive buffer: global storage index V lives
+// at ((V mod P) << sh_lchunk) | ((V >> p) mod 2^sh_lchunk); writing the
+// block-cyclic local output, K with bits [logr0 - p, logr0) removed)
 // waves per SIMD the LDS tile allows (160 KiB/CU): caps VGPRs to match
 #ifndef MLH_WPS8
 #define MLH_WPS8 4  // R = 2^8: 32 KiB tile + 8 KiB twiddle copy -> 4 workgroups per CU
@@ -105,13 +112,22 @@ constexpr int pass_waves_per_simd(int logr, int ept) {
 // one LDS exchange fewer at R = 2^8, twice the VGPRs).
 template <int LOGR, int TW, int ZT, int EPT = kEPT>
 __global__ void __launch_bounds__(kCols * (1 << LOGR) / EPT,
-                                  TW == 2 ? 1 : pass_waves_per_simd(LOGR, EPT))
+                                  (TW == 2 || TW == 4) ? 1 : pass_waves_per_simd(LOGR, EPT))
 ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
                 const fe* __restrict__ ta, const fe* __restrict__ tb, PassGeom g) {
   constexpr int R = 1 << LOGR;
   constexpr int LQ = EPT == 16 ? 4 : 3;  // stages per register phase
   constexpr int TPC = R / EPT;  // threads per column
-  constexpr bool LAST = TW == 2;
+  constexpr bool LAST = TW == 2 || TW == 4;
+  constexpr bool SH = TW == 4;
+  // sharded last pass: global storage index -> receive-buffer position
+  auto phys = [&](uint64_t v) -> uint64_t {
+    if constexpr (SH)
+      return ((v & ((1ull << g.sh_p) - 1)) << g.sh_lchunk) |
+             ((v >> g.sh_p) & ((1ull << g.sh_lchunk) - 1));
+    else
+      return v;
+  };
   __shared__ fe lds[R * kCols];
 #if MLH_LDS_TW
   // The expanded stage twiddles (R/2 entries x 4 limb-shifted multiples, 2R
@@ -133,7 +149,12 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   const int c = tid % kCols;
   const int t = tid / kCols;
   const uint64_t vec = (uint64_t)blockIdx.x >> g.ltpv;
-  const uint64_t tile = blockIdx.x & ((1ull << g.ltpv) - 1);
+  uint64_t tile = blockIdx.x & ((1ull << g.ltpv) - 1);
+  if constexpr (SH) {  // this rank's tiles: first-digit columns whose top p bits are the rank
+    const uint32_t lmid = g.log_n - g.logr[0] - LOGR;
+    const uint32_t ld1 = g.logr[0] - kLogCols - g.sh_p;  // local first-digit column groups
+    tile = ((((uint64_t)g.sh_rank << ld1) | (tile >> lmid)) << lmid) | (tile & ((1ull << lmid) - 1));
+  }
   in += vec << g.lin_v;
   out += vec << g.lout_v;
 
@@ -174,19 +195,31 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     // (the staged tile's columns are XOR-swizzled by row: lanes 0..7 write 8
     // consecutive rows of one column, which unswizzled sit 128 B apart on the
     // same LDS banks; the reads take one row's 8 columns, a permutation either way)
+    // SH: a row's low p bits are its source rank, so the 8 lanes of a column
+    // take rows P apart (consecutive in that source's chunk), and the swizzle
+    // mixes in the bits above the rank bits.
+    auto swz = [&](uint32_t row) -> uint32_t {
+      if constexpr (SH) return (row ^ (row >> g.sh_p)) & (kCols - 1);
+      else return row & (kCols - 1);
+    };
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
       const uint32_t idx = (uint32_t)(e * NT + tid);
       const uint32_t l = idx & 63, grp = idx >> 6;
-      const uint32_t row = grp * 8 + (l & 7), col = l >> 3;
-      lds[row * kCols + (col ^ (row & (kCols - 1)))] =
-          fe_load(in + base + ((uint64_t)col << cshift) + row);
+      uint32_t row = grp * 8 + (l & 7);
+      if constexpr (SH) {
+        const uint32_t lq = LOGR - g.sh_p - 3;  // groups of 8 rows per source rank: 2^lq
+        const uint32_t src = grp >> lq, q0 = grp & ((1u << lq) - 1);
+        row = ((((q0 << 3) + (l & 7)) << g.sh_p)) | src;
+      }
+      const uint32_t col = l >> 3;
+      lds[row * kCols + (col ^ swz(row))] = fe_load(in + phys(base + ((uint64_t)col << cshift) + row));
     }
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
       const uint32_t row = bitrev((uint32_t)(t * EPT + e), LOGR);
-      x[e] = lds[row * kCols + (c ^ (row & (kCols - 1)))];
+      x[e] = lds[row * kCols + (c ^ swz(row))];
     }
   } else
 #endif
@@ -203,6 +236,8 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
       const uint32_t logw = g.log_n - LOGR;
       const uint64_t colr = __builtin_bitreverse64(jrest) >> (64 - logw);
       x[e] = fe_load(in + (colr << (LOGR - 1)) + ((uint32_t)(t * EPT + e) >> 1));
+    } else if constexpr (SH) {
+      x[e] = fe_load(in + phys(base + ((uint64_t)c << cshift) + ((uint64_t)row << rshift)));
     } else {
       x[e] = fe_load(src + ((uint64_t)row << rshift));
     }
@@ -430,7 +465,14 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
 #pragma unroll
     for (int e = 0; e < EPT; e += 4) bfly_cccc_v(x[e], x[e + 1], x[e + 2], x[e + 3]);
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) fe_store(out + kbase + ((uint64_t)pos[e] << kshift), x[e]);
+    for (int e = 0; e < EPT; ++e) {
+      uint64_t K = kbase + ((uint64_t)pos[e] << kshift);
+      if constexpr (SH) {  // drop the rank bits [logr0 - p, logr0) of K
+        const uint32_t lo = g.logr[0] - g.sh_p;
+        K = ((K >> g.logr[0]) << lo) | (K & ((1ull << lo) - 1));
+      }
+      fe_store(out + K, x[e]);
+    }
   }
   (void)TPC;
 }
@@ -805,6 +847,97 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
   }
   if (ev) (void)hipEventRecord(ev[tb.nradix], st);
   return hipSuccess;
+}
+
+// out[k][j] = in[k][j] * rowbase^k (k < rows, j < 2^lcols): an inter-pass
+// twiddle table with a per-row factor (the sharded fused NTT's rank twist)
+__global__ void __launch_bounds__(256)
+scale_rows_kernel(const fe* __restrict__ in, fe* __restrict__ out, uint64_t n, uint32_t lcols, fe rowbase) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k = i >> lcols;
+  fe f = fe_one(), b = rowbase;
+  while (k) {
+    if (k & 1) f = fe_mul(f, b);
+    b = fe_mul(b, b);
+    k >>= 1;
+  }
+  fe_store(out + i, fe_mul(fe_load(in + i), f));
+}
+
+hipError_t launch_scale_rows(const fe* in, fe* out, uint64_t rows, uint32_t lcols, fe rowbase,
+                             hipStream_t st) {
+  const uint64_t n = rows << lcols;
+  hipLaunchKernelGGL(scale_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, out, n,
+                     lcols, rowbase);
+  return hipGetLastError();
+}
+
+hipError_t launch_ntt_passes_pre(const fe* in, fe* out, const NttTables& tb, uint32_t log_n,
+                                 uint32_t npasses, hipStream_t st) {
+  if (npasses == 0 || npasses >= tb.nradix) return hipErrorInvalidValue;
+  PassGeom g;
+  g.log_n = log_n;
+  g.nradix = tb.nradix;
+  for (uint32_t p = 0; p < tb.nradix; ++p) g.logr[p] = tb.logr[p];
+  const uint64_t N = 1ull << log_n;
+  uint64_t W = N;
+  for (uint32_t p = 0; p < npasses; ++p) {
+    const uint32_t lr = tb.logr[p];
+    W >>= lr;
+    g.p = p;
+    g.lstride = (uint32_t)__builtin_ctzll(W);
+    g.loga = tb.loga[p];
+    g.ltpv = log_n - kLogCols - lr;
+    g.lin_v = g.lout_v = log_n;
+    const uint64_t tiles = N >> (kLogCols + lr);
+    const fe* src = p == 0 ? in : out;  // pass 0: in -> out; then in place on out
+    hipError_t e;
+    switch (lr) {
+      case 4: e = launch_pass<4>(false, 0, src, out, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 5: e = launch_pass<5>(false, 0, src, out, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 6: e = launch_pass<6>(false, 0, src, out, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 7: e = launch_pass<7>(false, 0, src, out, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 8: e = launch_pass<8>(false, 0, src, out, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 9: e = launch_pass<9>(false, 0, src, out, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      default: return hipErrorInvalidValue;
+    }
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_ntt_shard_last(const fe* recv, fe* out, const fe* tw, const uint32_t* logr,
+                                 uint32_t nradix, uint32_t log_n, uint32_t log_p, uint32_t rank,
+                                 hipStream_t st) {
+  if (nradix < 2 || nradix > (uint32_t)kMaxPasses) return hipErrorInvalidValue;
+  const uint32_t lr = logr[nradix - 1];
+  if (lr < log_p + 3 || logr[0] < kLogCols + log_p) return hipErrorInvalidValue;
+  PassGeom g;
+  g.log_n = log_n;
+  g.nradix = nradix;
+  for (uint32_t p = 0; p < nradix; ++p) g.logr[p] = logr[p];
+  g.p = nradix - 1;
+  g.lstride = 0;
+  g.loga = 0;
+  g.ltpv = log_n - kLogCols - lr - log_p;  // this rank's tiles
+  g.lin_v = g.lout_v = log_n;
+  g.sh_p = log_p;
+  g.sh_rank = rank;
+  g.sh_lchunk = log_n - 2 * log_p;
+  const dim3 grid((unsigned)(1ull << g.ltpv));
+#define MLH_SHL(LR)                                                                                 \
+  hipLaunchKernelGGL((ntt_pass_kernel<LR, 4, 0, kEPT>), grid, dim3(kCols * (1 << LR) / kEPT), MLH_LDS_PAD, \
+                     st, recv, out, tw, nullptr, nullptr, g)
+  switch (lr) {
+    case 6: MLH_SHL(6); break;
+    case 7: MLH_SHL(7); break;
+    case 8: MLH_SHL(8); break;
+    case 9: MLH_SHL(9); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef MLH_SHL
+  return hipGetLastError();
 }
 
 hipError_t launch_pow_table(fe* out, fe base, fe scale, uint64_t count, hipStream_t st,

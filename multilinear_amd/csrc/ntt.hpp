@@ -64,6 +64,21 @@ hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n,
 hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables& tb,
                              uint32_t log_n, int zero_top, hipStream_t st,
                              hipEvent_t* ev = nullptr, uint64_t batch = 1);
+// out[k][j] = in[k][j] * rowbase^k for a rows x 2^lcols table
+hipError_t launch_scale_rows(const fe* in, fe* out, uint64_t rows, uint32_t lcols, fe rowbase,
+                             hipStream_t st);
+// Passes 0 .. npasses-1 of tb's plan (npasses < nradix): pass 0 in -> out, the
+// others in place on out (the sharded fused NTT's local part).
+hipError_t launch_ntt_passes_pre(const fe* in, fe* out, const NttTables& tb, uint32_t log_n,
+                                 uint32_t npasses, hipStream_t st);
+// The last pass of a 2^log_n transform with plan logr[0..nradix) sharded over
+// 2^log_p ranks (ntt_pass_kernel TW 4): this rank's tiles, reading the
+// all-to-all receive buffer (2^log_p chunks of 2^(log_n - 2 log_p)), writing
+// the block-cyclic output (block 2^(logr[0] - log_p)); tw: the pass's stage
+// twiddles (expanded).  Needs logr[last] >= log_p + 3, logr[0] >= log_p + 3.
+hipError_t launch_ntt_shard_last(const fe* recv, fe* out, const fe* tw, const uint32_t* logr,
+                                 uint32_t nradix, uint32_t log_n, uint32_t log_p, uint32_t rank,
+                                 hipStream_t st);
 // rocprof-style kernel label of pass p ("ntt_pass<8,0,0>")
 void ntt_pass_label(const NttTables& tb, uint32_t p, int zero_top, char* buf, size_t n);
 // The reference's radix-2 network for any generator (ntt.hip "general-generator

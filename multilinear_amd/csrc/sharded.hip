@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "context.hpp"
+#include "fused_ntt.hpp"
 #include "host_sha256.hpp"
 #include "host_transcript.hpp"
 
@@ -422,6 +423,97 @@ mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const voi
     HIP_TRY(ctx, hipEventRecord(c_done[k], third));
   }
   return MLH_OK;  // (join: main waits for both side streams)
+}
+
+// `count` forward transforms with the rank digit fused into the last pass
+// (FusedNtt, capi.hip): per transform the local passes but the last (context
+// stream), ONE all-to-all of their output (side stream), and one fused last
+// pass over the received chunks (third stream) -- three HBM passes per element
+// against four for mlh_sharded_ntt_batch's local NTT + cross-shard DFT.  Input:
+// the cyclic layout (rank g holds x[g + P m]); output: block-cyclic with block
+// 2^out_log_s (*log_s_out), out_log_s = the plan's first digit - log2 P, e.g. 6
+// for 2^27 over 8 ranks.  Pipelined like mlh_sharded_ntt_batch.  Needs
+// 2 <= P <= 8 and 2^(log_n - log P) >= 2^(13 - log P) local elements, else
+// MLH_ERR_INVALID (use mlh_sharded_ntt_batch).
+mlh_status mlh_sharded_ntt_fused_batch(mlh_ctx* ctx, const mlh_transport* t, const void* const* dev_in,
+                                       void* const* dev_out, uint32_t count, uint32_t log_n,
+                                       const uint8_t gen[16], uint32_t* log_s_out) {
+  if (!ctx || (count && (!dev_in || !dev_out)) || !gen) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  MLH_TRY(check_transport(ctx, t));
+  for (uint32_t i = 0; i < count; ++i)
+    if (!dev_in[i] || !dev_out[i]) return fail(ctx, MLH_ERR_INVALID, "null argument");
+  Tp tp(ctx, t);
+  if (tp.P < 2 || tp.P > 8) return fail(ctx, MLH_ERR_INVALID, "fused sharded NTT: 2 <= P <= 8");
+  if (log_n > 40) return fail(ctx, MLH_ERR_INVALID, "log_n");
+  if (!gen_has_order(h_load(gen), log_n)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != n");
+  FusedNtt fz;
+  MLH_TRY(fz.prepare(ctx, h_load(gen), log_n, tp.p, tp.rank));
+  if (log_s_out) *log_s_out = fz.out_log_s();
+  if (!count) return MLH_OK;
+  const uint64_t M = 1ull << (log_n - tp.p);
+  if (t->host_side) {  // transforms in turn
+    Bufs b(ctx);
+    fe *z, *recv;
+    MLH_TRY(b.get(M * 16, &z));
+    MLH_TRY(b.get(M * 16, &recv));
+    for (uint32_t i = 0; i < count; ++i) {
+      MLH_TRY(fz.run_pre(dev_in[i], z));
+      MLH_TRY(tp.all_to_all(z, recv, M / tp.P * 16, "ntt_all_to_all"));
+      MLH_TRY(fz.run_last(recv, dev_out[i]));
+    }
+    return MLH_OK;
+  }
+  if (!ctx->side) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  if (!ctx->side2) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking));
+  Bufs b(ctx);
+  fe *z[2], *recv[2];
+  for (int k = 0; k < 2; ++k) {
+    MLH_TRY(b.get(M * 16, &z[k]));
+    MLH_TRY(b.get(M * 16, &recv[k]));
+  }
+  hipEvent_t evs[9];
+  for (auto& e : evs) e = take_event(ctx);
+  struct Recycle {
+    mlh_ctx* c;
+    hipEvent_t* e;
+    ~Recycle() {
+      for (int k = 0; k < 9; ++k) c->ev_free.push_back(e[k]);
+    }
+  } rec{ctx, evs};
+  hipEvent_t *a_done = evs, *x_done = evs + 2, *c_done = evs + 4;
+  hipStream_t main = ctx->stream, side = ctx->side, third = ctx->side2;
+  HIP_TRY(ctx, hipEventRecord(evs[8], main));  // the third stream starts after the caller's work
+  HIP_TRY(ctx, hipStreamWaitEvent(third, evs[8], 0));
+  struct JoinSide {  // every exit: the context stream waits for both side streams
+    hipStream_t main, s1, s2;
+    hipEvent_t e1, e2;
+    ~JoinSide() {
+      (void)hipEventRecord(e1, s1);
+      (void)hipStreamWaitEvent(main, e1, 0);
+      (void)hipEventRecord(e2, s2);
+      (void)hipStreamWaitEvent(main, e2, 0);
+    }
+  } join{main, side, third, evs[6], evs[7]};
+  for (uint32_t i = 0; i < count; ++i) {
+    const int k = i & 1;
+    if (i >= 2) HIP_TRY(ctx, hipStreamWaitEvent(main, x_done[k], 0));  // z[k] was sent
+    MLH_TRY(fz.run_pre(dev_in[i], z[k]));
+    HIP_TRY(ctx, hipEventRecord(a_done[k], main));
+    HIP_TRY(ctx, hipStreamWaitEvent(side, a_done[k], 0));
+    if (i >= 2) HIP_TRY(ctx, hipStreamWaitEvent(side, c_done[k], 0));  // recv[k] was read
+    {
+      StreamSwap sw(ctx, side);
+      MLH_TRY(tp.all_to_all(z[k], recv[k], M / tp.P * 16, "ntt_all_to_all"));
+    }
+    HIP_TRY(ctx, hipEventRecord(x_done[k], side));
+    HIP_TRY(ctx, hipStreamWaitEvent(third, x_done[k], 0));
+    {
+      StreamSwap sw(ctx, third);
+      MLH_TRY(fz.run_last(recv[k], dev_out[i]));
+    }
+    HIP_TRY(ctx, hipEventRecord(c_done[k], third));
+  }
+  return MLH_OK;
 }
 
 mlh_status mlh_sharded_reed_solomon(mlh_ctx* ctx, const mlh_transport* t, const void* dev_coeffs,

@@ -184,6 +184,57 @@ def test_ntt_batch_pipelined_vs_c_oracle(P, log_n, count):
             assert np.array_equal(res[r][1][i], res[r][2][i]), "inverse of transform %d, rank %d" % (i, r)
 
 
+@pytest.mark.parametrize("P,log_n,count", [(2, 15, 3), (4, 16, 3), (8, 18, 3), (8, 21, 2), (2, 25, 2),
+                                           pytest.param(8, 27, 2, marks=pytest.mark.slow)])
+def test_ntt_fused_batch_vs_c_oracle(P, log_n, count):
+    """mlh_sharded_ntt_fused_batch (the rank digit fused into the last pass;
+    local passes, one all-to-all, one pass over the received chunks; three
+    streams, device-ordered exchanges): every transform equals the C oracle's
+    NTT once the block-cyclic outputs (block 2^log_s, log_s reported by the
+    call) are put back in order.  (8, 27) is the bench's N = 8 shape: 2^24 per
+    rank."""
+    L = DV.lib()
+    xs = [DV.random_limbs(1 << log_n, seed=300 + i) for i in range(count)]
+    g = _gen(log_n)
+
+    def body(r, ctx, st, t):
+        ins = [DV.to_device(S.shard_cyclic(x, P, r)) for x in xs]
+        outs = [DV.empty(ins[0].shape[0]) for _ in range(count)]
+        pi = (ctypes.c_void_p * count)(*[i.data_ptr() for i in ins])
+        po = (ctypes.c_void_p * count)(*[o.data_ptr() for o in outs])
+        ls = ctypes.c_uint32()
+        torch.cuda.current_stream().synchronize()
+        DV.check(L.mlh_sharded_ntt_fused_batch(ctx, _tp(t), pi, po, count, log_n, DV.fe_bytes(g),
+                                               ctypes.byref(ls)), ctx)
+        DV.check(L.mlh_synchronize(ctx), ctx)
+        return [DV.from_device(o) for o in outs], ls.value
+
+    res = _run_ranks(P, body)
+    log_s = res[0][1]
+    assert all(res[r][1] == log_s for r in range(P)) and 3 <= log_s < log_n
+    for i, x in enumerate(xs):
+        want = C.ntt_par(x, log_n, g) if log_n > 22 else C.ntt(x, log_n, g)
+        got = S.unshard_blocks([res[r][0][i] for r in range(P)], log_s)
+        assert np.array_equal(got, want), "transform %d" % i
+
+
+def test_ntt_fused_batch_rejects_unsupported():
+    """P = 16 and local sizes below the fused plan's minimum are refused
+    (mlh_sharded_ntt_batch covers them); a generator of the wrong order too."""
+    L = DV.lib()
+
+    def body(r, ctx, st, t):
+        x = DV.empty(1 << 8)
+        pi = (ctypes.c_void_p * 1)(x.data_ptr())
+        st1 = L.mlh_sharded_ntt_fused_batch(ctx, _tp(t), pi, pi, 1, 12, DV.fe_bytes(_gen(12)), None)
+        st2 = L.mlh_sharded_ntt_fused_batch(ctx, _tp(t), pi, pi, 1, 12, DV.fe_bytes(_gen(11)), None)
+        return st1, st2
+
+    for P, want2 in ((16, _lib.MLH_ERR_INVALID), (8, _lib.MLH_ERR_BAD_GENERATOR)):
+        for st1, st2 in _run_ranks(P, body):
+            assert st1 == _lib.MLH_ERR_INVALID and st2 == want2
+
+
 def test_ntt_spot_check_logic_vs_c_oracle_p8():
     """The bench's in-run check of the sharded headline (bench.py
     sharded_ntt_check) at P = 8 device-ordered ranks: the per-rank terms
