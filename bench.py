@@ -418,24 +418,34 @@ def main():
     # dominant kernel timing (HIP events on the launch stream, timed region)
     kernels = {}
     labels = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(4)
-              for z in range(3)] + ["shard_dft<%d,0>" % p for p in range(1, 5)] + ["ntt_all_to_all"]
+              for z in range(3)] + ["shard_dft<%d,0>" % p for p in range(1, 5)] + ["ntt_all_to_all",
+                                                                                     "ntt_fused_pre",
+                                                                                     "ntt_fused_last"]
     for lab in labels:
         cnt = ctypes.c_uint64()
         tot = ctypes.c_double()
         lib.mlh_profile_get(ctx, lab.encode(), ctypes.byref(cnt), ctypes.byref(tot))
         if cnt.value:
             kernels[lab] = {"launches": cnt.value, "avg_ms": tot.value / cnt.value}
-    dom = max(((k, v) for k, v in kernels.items() if k.startswith("ntt_pass")),
+    fused = batch is not None and sharded and batch.fused
+    pref = "ntt_fused" if fused else "ntt_pass"
+    dom = max(((k, v) for k, v in kernels.items() if k.startswith(pref)),
               key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
     dom_name, dom_stat = dom
     # the NTT's algorithmic bytes are 2 x 16 x N for the whole
     # transform; a pass is credited with its share (passes = NTT launches per step)
-    passes = max(1, round(sum(v["launches"] for k, v in kernels.items() if k.startswith("ntt_pass"))
-                          / dom_stat["launches"]))
-    alg_bytes = 32.0 * N / passes
+    if fused:  # the fused pre launch runs npre passes, the last launch one
+        npre = (log_n - (9 - log_p) + 8) // 9
+        passes = npre + 1
+        share = npre if dom_name == "ntt_fused_pre" else 1
+    else:
+        passes = max(1, round(sum(v["launches"] for k, v in kernels.items() if k.startswith("ntt_pass"))
+                              / dom_stat["launches"]))
+        share = 1
+    alg_bytes = 32.0 * N * share / passes
     achieved_gbs = alg_bytes / (dom_stat["avg_ms"] * 1e-3) / 1e9
     traffic = load_pmc(dom_name, log_n)
-    valu = load_valu(dom_name) if log_n == 24 else None
+    valu = load_valu(dom_name) if log_n == 24 and dom_name.startswith("ntt_pass") else None
     valu_frac = (valu[0] * 64 / (dom_stat["avg_ms"] * 1e-3) / VALU_PEAK) if valu else None
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -482,7 +492,7 @@ def main():
                                  "every step" if args.prof_every <= 1
                                  else "every %dth step" % args.prof_every, dom_stat["launches"]),
             "alg_bytes_per_launch": alg_bytes,
-            "alg_bytes_rule": "32 B x 2^%d / %d passes (SURVEY.md 8(d))" % (log_n, passes),
+            "alg_bytes_rule": "32 B x 2^%d x %d / %d passes (SURVEY.md 8(d))" % (log_n, share, passes),
             "valu_frac": valu_frac,
         },
         "kernels": kernels,
@@ -506,6 +516,8 @@ def main():
         result["rccl_ranks"] = tinfo["ranks"] if tinfo["transport"] == "rccl" else None
         if sharded:
             result["sharded_phases"] = sharded_phases(kernels, log_n, log_p, passes)
+            result["sharded_algorithm"] = batch.algorithm
+            result["sharded_output_block_log"] = batch.log_s if batch.fused else log_n - log_p
             try:
                 result["sharded_ntt_verified"] = sharded_ntt_check(batch, log_n, log_p, rank, world,
                                                                    local)
@@ -879,13 +891,25 @@ class _ShardedBatch:
     call (C ABI, csrc/sharded.hip): outputs alternate between two buffers;
     the pointer arrays are built once per k, outside any timed region."""
 
-    def __init__(self, lib, ctx, transport, x, out, log_total, local):
+    def __init__(self, lib, ctx, transport, x, out, log_total, local, fused=True):
         from multilinear_amd import device as D
 
         self.lib, self.ctx, self.tp, self.log_total = lib, ctx, transport, log_total
         self.x, self.outs = x, [out, D.empty(x.shape[0], local)]
         self.gen = D.fe_bytes(int.from_bytes(bytes(_gen(lib, log_total)), "little"))
         self.arrays = {}
+        # the fused schedule (rank digit in the last pass) where it applies;
+        # else the local NTT + all-to-all + cross-shard DFT batch
+        self.fused, self.log_s = False, None
+        if fused:
+            ls = ctypes.c_uint32()
+            st = lib.mlh_sharded_ntt_fused_batch(ctx, ctypes.byref(transport.transport), None, None, 0,
+                                                 log_total, self.gen, ctypes.byref(ls))
+            if st == 0:
+                self.fused, self.log_s = True, ls.value
+        self.algorithm = ("fused: local passes, one all-to-all, the last pass over the received chunks "
+                          "(mlh_sharded_ntt_fused_batch)" if self.fused else
+                          "local NTT, one all-to-all, cross-shard DFT (mlh_sharded_ntt_batch)")
 
     def prepare(self, k):
         if k not in self.arrays:
@@ -900,8 +924,12 @@ class _ShardedBatch:
         if k <= 0:
             return
         ins, outs = self.prepare(k)
-        D.check(self.lib.mlh_sharded_ntt_batch(self.ctx, ctypes.byref(self.tp.transport), ins, outs, k,
-                                               self.log_total, self.gen, 0), self.ctx)
+        if self.fused:
+            D.check(self.lib.mlh_sharded_ntt_fused_batch(self.ctx, ctypes.byref(self.tp.transport), ins, outs,
+                                                         k, self.log_total, self.gen, None), self.ctx)
+        else:
+            D.check(self.lib.mlh_sharded_ntt_batch(self.ctx, ctypes.byref(self.tp.transport), ins, outs, k,
+                                                   self.log_total, self.gen, 0), self.ctx)
 
 
 def sharded_phases(kernels, log_n, log_p, passes):
@@ -914,8 +942,10 @@ def sharded_phases(kernels, log_n, log_p, passes):
     ((P - 1) / P of its 16 x 2^log_n-byte shard) per all-to-all duration."""
     P = 1 << log_p
     loc = [v["avg_ms"] for k, v in kernels.items() if k.startswith("ntt_pass")]
+    if not loc and "ntt_fused_pre" in kernels:  # fused: the local passes but the last, one launch set
+        loc = [kernels["ntt_fused_pre"]["avg_ms"]]
     a2a = kernels.get("ntt_all_to_all")
-    dft = kernels.get("shard_dft<%d,0>" % log_p)
+    dft = kernels.get("shard_dft<%d,0>" % log_p) or kernels.get("ntt_fused_last")
     sent = 16.0 * (1 << log_n) * (P - 1) / P
     return {
         "local_ntt_ms": sum(loc) if loc else None,
@@ -924,6 +954,8 @@ def sharded_phases(kernels, log_n, log_p, passes):
         "all_to_all_bytes_sent_per_rank": sent,
         "all_to_all_gbs": sent / (a2a["avg_ms"] * 1e-3) / 1e9 if a2a else None,
         "shard_dft_ms": dft["avg_ms"] if dft else None,
+        "shard_dft_what": ("the fused last pass (rank digit + the last local digit, on the received "
+                           "chunks)" if "ntt_fused_last" in kernels else "the cross-shard DFT"),
         "timing": "HIP events around every sampled launch (mlh_profile_*), per rank 0",
     }
 
@@ -955,7 +987,7 @@ def sharded_ntt_check(batch, log_n, log_p, rank, world, local, samples=8):
     bad = 0
     for i, j in enumerate(js):
         want = sum(t[i] for t in allt) % D.M
-        owner, l = SH.ntt_block_owner(j, LT, log_p)
+        owner, l = SH.ntt_block_owner(j, LT, log_p, batch.log_s)
         if owner == rank:
             got = D.limbs_to_ints(D.from_device(batch.outs[0][l:l + 1]))[0]
             bad += int(got != want)

@@ -243,10 +243,12 @@ def preflight(transport, bytes_per_rank, device=0):
     return bad.value, ms.value
 
 
-def ntt_block_owner(j, log_total, log_p):
-    """(rank, local index) holding X[j] of a sharded forward NTT (block
-    2^(log_total - 2 log_p) output layout)."""
-    log_s = log_total - 2 * log_p
+def ntt_block_owner(j, log_total, log_p, log_s=None):
+    """(rank, local index) holding X[j] of a sharded forward NTT: block
+    2^(log_total - 2 log_p) output layout (mlh_sharded_ntt(_batch), DESIGN.md
+    section 6), or block 2^log_s (mlh_sharded_ntt_fused_batch reports it)."""
+    if log_s is None:
+        log_s = log_total - 2 * log_p
     r = (j >> log_s) & ((1 << log_p) - 1)
     return r, ((j >> (log_s + log_p)) << log_s) | (j & ((1 << log_s) - 1))
 
