@@ -128,6 +128,25 @@ struct Bufs {
 void store_fe(uint8_t out[16], u128 v) { h_store(out, v); }
 
 // gen has order exactly 2^log_n (the cross-shard DFT needs a DFT generator)
+// The exchange stream of the pipelined sharded calls: the device's highest
+// stream priority (MLH_EXCHANGE_PRIORITY=0 at build time: default priority),
+// so the collective's workgroups are dispatched ahead of the local passes'
+// when both are queued (tools/shard_step_emul.py).
+#ifndef MLH_EXCHANGE_PRIORITY
+#define MLH_EXCHANGE_PRIORITY 1
+#endif
+mlh_status ensure_side_streams(mlh_ctx* ctx) {
+  if (!ctx->side) {
+    int lo = 0, hi = 0;
+    if (MLH_EXCHANGE_PRIORITY && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      HIP_TRY(ctx, hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, hi));
+    else
+      HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  }
+  if (!ctx->side2) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking));
+  return MLH_OK;
+}
+
 bool gen_has_order(u128 gen, uint32_t log_n) {
   if (gen >= kModulus) return false;
   if (log_n == 0) return gen == 1;
@@ -356,8 +375,7 @@ mlh_status mlh_sharded_ntt_batch(mlh_ctx* ctx, const mlh_transport* t, const voi
     return fail(ctx, MLH_ERR_INVALID, "sharded NTT needs 2^log_n >= 2 P^2");
   if (!gen_has_order(h_load(gen), log_n)) return fail(ctx, MLH_ERR_BAD_GENERATOR, "generator order != n");
   if (!count) return MLH_OK;
-  if (!ctx->side) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-  if (!ctx->side2) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking));
+  MLH_TRY(ensure_side_streams(ctx));
   const uint64_t M = 1ull << (log_n - tp.p);
   uint8_t gp[16];
   store_fe(gp, h_pow(h_load(gen), (u128)tp.P));
@@ -463,8 +481,7 @@ mlh_status mlh_sharded_ntt_fused_batch(mlh_ctx* ctx, const mlh_transport* t, con
     }
     return MLH_OK;
   }
-  if (!ctx->side) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-  if (!ctx->side2) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking));
+  MLH_TRY(ensure_side_streams(ctx));
   Bufs b(ctx);
   fe *z[2], *recv[2];
   for (int k = 0; k < 2; ++k) {
