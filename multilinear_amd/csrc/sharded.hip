@@ -128,21 +128,11 @@ struct Bufs {
 void store_fe(uint8_t out[16], u128 v) { h_store(out, v); }
 
 // gen has order exactly 2^log_n (the cross-shard DFT needs a DFT generator)
-// The exchange stream of the pipelined sharded calls: the device's highest
-// stream priority (MLH_EXCHANGE_PRIORITY=0 at build time: default priority),
-// so the collective's workgroups are dispatched ahead of the local passes'
-// when both are queued (tools/shard_step_emul.py).
-#ifndef MLH_EXCHANGE_PRIORITY
-#define MLH_EXCHANGE_PRIORITY 1
-#endif
+// The side streams of the pipelined sharded calls (lazy).  (Giving the
+// exchange stream the device's highest priority measured no change in
+// tools/shard_step_emul.py: 0.766-0.769 vs 0.763 ms a step; not kept.)
 mlh_status ensure_side_streams(mlh_ctx* ctx) {
-  if (!ctx->side) {
-    int lo = 0, hi = 0;
-    if (MLH_EXCHANGE_PRIORITY && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-      HIP_TRY(ctx, hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, hi));
-    else
-      HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-  }
+  if (!ctx->side) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
   if (!ctx->side2) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking));
   return MLH_OK;
 }
