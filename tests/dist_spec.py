@@ -599,3 +599,86 @@ def sumcheck_prove(m, d, n, total_sum, transcript, tp, ops):
         out_p.append((int.from_bytes(c1, "little"), int.from_bytes(c2, "little")))
         out_r.append(int.from_bytes(raw_r[16 * k:16 * k + 16], "little"))
     return out_p, out_r
+
+
+# ---------------------------------------------------------------------------
+# fused sharded NTT (mlh_sharded_ntt_fused_batch): the rank digit in the last pass
+# ---------------------------------------------------------------------------
+
+def plan_radices(log_n):
+    """ntt.hip ntt_plan_radices: ceil(log_n / 9) digits, larger first."""
+    P = (log_n + 8) // 9
+    out, rem = [], log_n
+    for p in range(P):
+        r = (rem + (P - p) - 1) // (P - p)
+        out.append(r)
+        rem -= r
+    return out
+
+
+def fused_plan(log_n, log_p):
+    """(c, pre digits, output log_s) of the fused plan (capi.hip FusedNtt::prepare):
+    the last global digit is c + p = 9 bits, c of them local."""
+    c = 9 - log_p
+    pre = plan_radices(log_n - log_p - c)
+    return c, pre, pre[0] - log_p
+
+
+def ntt_fused(x_local, log_n, gen, tp):
+    """The fused sharded forward NTT on Python ints (the executable spec of
+    mlh_sharded_ntt_fused_batch, at oracle sizes).  N = Mhi * Q with
+    Q = 2^(c + p) (the last pass) and Mhi = 2^(log_n - c - p):
+      X[kA + Mhi kB] = sum_{nB < Q} wQ^(nB kB) w^(nB kA) sum_{nA} x[nA Q + nB] wMhi^(nA kA).
+    Rank g holds x[g + P m] (cyclic), i.e. nB = g + P mc, m = nA 2^c + mc, so the
+    inner DFTs and the twiddle are local.  ONE all-to-all: (mc, kA) goes to the
+    rank named by bits [a - p, a) of kA (a = the first local digit: the top
+    bits of the first output digit, as the local passes store it).  The last
+    stage: a Q-point DFT over nB for each received kA; X[K] lands at local index
+    K with bits [a - p, a) removed (block-cyclic, block 2^(a - p)).
+    x_local: list of ints; returns (list of ints, log_s)."""
+    from oracle import ntt as ON
+
+    P, g = tp.world, tp.rank
+    p = _log2(P)
+    N = 1 << log_n
+    c, pre, log_s = fused_plan(log_n, p)
+    a = pre[0]
+    Q = 1 << (c + p)
+    Mhi = N // Q
+    C2 = 1 << c
+    wM = pow(gen, Q, M)
+    # local stage: for every mc, the Mhi-point DFT over nA, times w^(nB kA)
+    Z = {}
+    for mc in range(C2):
+        nB = g + P * mc
+        Y = ON.ntt([x_local[nA * C2 + mc] for nA in range(Mhi)], wM) if Mhi > 1 else [x_local[mc]]
+        for kA in range(Mhi):
+            Z[(mc, kA)] = Y[kA] * pow(gen, nB * kA, M) % M
+    # all-to-all: destination h = bits [a - p, a) of kA; a fixed (mc, kA) order per chunk
+    dest = lambda kA: (kA >> (a - p)) & (P - 1)  # noqa: E731
+    chunks = [[] for _ in range(P)]
+    for kA in range(Mhi):
+        for mc in range(C2):
+            chunks[dest(kA)].append(Z[(mc, kA)])
+    per = len(chunks[0])
+    assert all(len(ch) == per for ch in chunks)
+    import torch
+
+    send = torch.tensor([[v & 0xFFFFFFFF, (v >> 32) & 0xFFFFFFFF, (v >> 64) & 0xFFFFFFFF, v >> 96]
+                         for ch in chunks for v in ch], dtype=torch.int64).to(torch.int32)
+    recv = tp.all_to_all(send).to(torch.int64) & 0xFFFFFFFF
+    vals = [int(r[0]) | int(r[1]) << 32 | int(r[2]) << 64 | int(r[3]) << 96 for r in recv.tolist()]
+    mine = [kA for kA in range(Mhi) if dest(kA) == g]  # this rank's kA, in the senders' order
+    wQ = pow(gen, Mhi, M)
+    out = [0] * (N // P)
+    for i, kA in enumerate(mine):
+        col = [0] * Q
+        for src in range(P):
+            for mc in range(C2):
+                col[src + P * mc] = vals[src * per + i * C2 + mc]  # nB = src + P mc
+        XB = ON.ntt(col, wQ)
+        for kB in range(Q):
+            K = kA + Mhi * kB
+            lo = a - p
+            out[((K >> a) << lo) | (K & ((1 << lo) - 1))] = XB[kB]
+    return out, log_s

@@ -234,3 +234,60 @@ def test_sharded_merkle_commit_root(world, log_c):
         p.join(timeout=60)
     for r in res:
         assert r[1] is True, r
+
+
+def _fused_worker(rank, world, port, log_n, q):
+    import torch.distributed as tdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import random
+
+        from oracle import field as F
+        from oracle import ntt as ON
+        from tests import dist_spec as D
+
+        rr = random.Random(log_n)
+        x = [rr.randrange(F.M) for _ in range(1 << log_n)]
+        gen = F.pow_2_generator(log_n)
+        out, log_s = D.ntt_fused(x[rank::world], log_n, gen, D.Transport())
+        q.put((rank, out, log_s, ON.ntt(x, gen) if rank == 0 else None))
+    except Exception:
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc(), None))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,log_n", [(2, 14), (4, 14), (8, 15)])
+def test_fused_sharded_ntt_spec_matches_oracle(world, log_n):
+    """The fused sharded NTT's schedule (tests/dist_spec.py ntt_fused: local
+    DFTs + twiddle, ONE gloo all-to-all by the first output digit's top bits,
+    the last Q-point stage on the received columns) at world 2/4/8: the
+    block-cyclic outputs (block 2^(a - p), the layout mlh_sharded_ntt_fused_batch
+    reports) put back in order equal the oracle NTT."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fused_worker, args=(r, world, port, log_n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r[2]
+    log_s = res[0][2]
+    from tests import dist_spec as D
+
+    assert log_s == D.fused_plan(log_n, world.bit_length() - 1)[2]
+    S = 1 << log_s
+    got = []
+    n_local = len(res[0][1])
+    for blk in range(n_local // S):
+        for r in range(world):
+            got.extend(res[r][1][blk * S:(blk + 1) * S])
+    assert got == res[0][3]
