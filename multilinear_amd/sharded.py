@@ -232,11 +232,12 @@ class HostTransport:
                 "transport": "host-staged torch.distributed (%s)" % self.tp.dist.get_backend(self.tp.group)}
 
 
-def preflight(transport, bytes_per_rank, device=0):
+def preflight(transport, bytes_per_rank, device=0, ctx=None):
     """mlh_comm_preflight: one all-to-all and one all-gather of a rank-tagged
     pattern through the transport, checked on the device -> (mismatched words
-    on this rank, ms of the two collectives)."""
-    ctx = context(device)
+    on this rank, ms of the two collectives).  ctx: the rank's own context when
+    several ranks share a process (a context is not thread-safe)."""
+    ctx = ctx or context(device)
     bad, ms = ctypes.c_uint64(), ctypes.c_float()
     check(lib().mlh_comm_preflight(ctx, _tp(transport), bytes_per_rank, ctypes.byref(bad),
                                    ctypes.byref(ms)), ctx)

@@ -286,7 +286,7 @@ def test_comm_preflight_pattern_p8(P):
     per = (1 << 20) // P
 
     def body(r, ctx, st, t):
-        return S.preflight(t, per)
+        return S.preflight(t, per, ctx=ctx)
 
     for shift, want in ((0, 0), (1, per // 4 * P)):
         res = _run_ranks(P, body, ThreadDeviceTransport(P, a2a_shift=shift))
