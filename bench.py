@@ -479,7 +479,11 @@ def main():
         },
         "ntt_hbm_frac": (32.0 * N / (ms_per_step * 1e-3) / 1e9) / HBM_PEAK_GBS,
         "roofline": {
-            "bound": "valu" if (valu_frac or 0) > achieved_gbs / HBM_PEAK_GBS else "hbm",
+            "bound": ("valu" if valu_frac > achieved_gbs / HBM_PEAK_GBS else "hbm") if valu_frac is not None
+                     else ("valu" if dom_name.startswith("ntt_") else "hbm"),
+            "bound_source": "SQ_INSTS_VALU of this kernel (valu_frac)" if valu_frac is not None else
+                            ("the ntt_pass kernels this phase launches, VALU-issue bound per their "
+                             "N = 1 counters (valu_profile)" if dom_name.startswith("ntt_") else None),
             "kernel": dom_name,
             "achieved": achieved_gbs,
             "peak": HBM_PEAK_GBS,
