@@ -230,11 +230,11 @@ subtree_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restric
     __syncthreads();
     // levels after the first have at most half a node per thread: a lane
     // pair per node (two-lane SHA-256, ~20 % less latency per level)
-    const uint32_t node = t >> 1;
+    const uint32_t node = sha2l_pair(t);
     const bool active = node < mp;
     if (active) r = sha2l_node(s[2 * node], s[2 * node + 1]);
     __syncthreads();
-    if (active && (t & 1) == 0) {
+    if (active && sha2l_lead(t)) {
       s[node] = r;
       digest_store(out + (off + b * mp + node) * 32, r);
     }

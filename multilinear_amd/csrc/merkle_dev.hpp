@@ -39,11 +39,11 @@ __device__ __forceinline__ void lds_tree_levels(Sha256State* s, uint64_t n, uint
     const uint64_t np = n / 2;
     Sha256State r;
     const bool two = 2 * np <= blockDim.x;
-    const uint32_t node = two ? threadIdx.x >> 1 : threadIdx.x;
+    const uint32_t node = two ? sha2l_pair(threadIdx.x) : threadIdx.x;
     const bool active = node < np;
     if (active) r = two ? sha2l_node(s[2 * node], s[2 * node + 1]) : sha256_node(s[2 * node], s[2 * node + 1]);
     __syncthreads();
-    if (active && (!two || (threadIdx.x & 1) == 0)) {
+    if (active && (!two || sha2l_lead(threadIdx.x))) {
       s[node] = r;
       digest_store(out + (off + node) * 32, r);
     }

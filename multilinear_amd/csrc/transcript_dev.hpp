@@ -286,49 +286,81 @@ __device__ __forceinline__ void sha256_rounds_from(uint32_t (&v)[8], uint32_t w[
 
 // ---- two-lane SHA-256 rounds ------------------------------------------------
 // A one-lane compression issues ~14 VALU per round (6 v_alignbit, 4 v_bitop3,
-// 4 adds).  Lane pairs (2i, 2i+1) share a round in SIMT form: the even lane
-// holds (e, f, g, h) and the odd lane (a, b, c, d) of the working state, and
-// one instruction stream computes Sigma1(e) | Sigma0(a) (v_alignbit with
-// per-lane counts), Ch(e, f, g) | Maj(a, b, c) (= bfi(e, f, g) | bfi(a ^ c,
-// b, c)), T1 = h + Sigma1 + Ch + K + W | T2 = Sigma0 + Maj, and the new e |
-// new a = d + T1 | T1 + T2 through one quad_perm DPP exchange: 11 VALU per
-// round.  Every lane pair computes the same compression; inputs are
-// wave-uniform.
+// 4 adds).  Two lanes share a round in SIMT form: lanes k and 7 - k of each
+// 8-lane half row (k < 4; the row_half_mirror DPP swaps them), the "e side"
+// (banks 0 and 2 of a row) holding (e, f, g, h) and the "a side" (banks 1 and
+// 3) (a, b, c, d).  One instruction stream computes Sigma1(e) | Sigma0(a)
+// (v_alignbit with per-lane counts), Ch(e, f, g) | Maj(a, b, c) (= bfi(e, f,
+// g) | bfi(a ^ c, b, c)) and u = Sigma + Ch|Maj + x with x = h + K + W + d on
+// the e side and -d on the a side: u is the new e (T1 + d) on the e side and
+// T2 - d on the a side, and ONE bank-masked DPP add (a side only) forms the
+// new a = u_e + u_a = T1 + T2 while the e side keeps u.  The dependency chain
+// of a round is v_alignbit, xor3, add3, DPP add; the next round's x (n = -c on
+// every lane, then c(partner) + g + K + W on the e side through a second
+// bank-masked DPP add) is off it.  11 VALU per round; a dependent node hash
+// on one wave 7.5k cycles against 8.5k with the earlier adjacent-lane pairs,
+// whose select of (T1 | d) sat on the chain (tools/sha_hm_bench.hip).  Every
+// lane pair computes the same compression; inputs are wave-uniform.
+constexpr int kSha2lDpp = 0x141;  // row_half_mirror
+__device__ __forceinline__ bool sha2l_aside(uint32_t lane) { return (lane >> 2) & 1u; }
+// node of thread t when the nodes of a workgroup are hashed on lane pairs
+// (32 per wave), and whether t is its e-side lane (the one that stores it)
+__device__ __forceinline__ uint32_t sha2l_pair(uint32_t t) {
+  const uint32_t k = t & 7;
+  return ((t >> 3) << 2) | (k < 4 ? k : 7 - k);
+}
+__device__ __forceinline__ bool sha2l_lead(uint32_t t) { return !sha2l_aside(t); }
 struct Sha2L {
-  uint32_t r0, r1, r2, r3;  // even lane: e f g h; odd lane: a b c d
-  uint32_t m;               // odd lane ~0, even lane 0
+  uint32_t r0, r1, r2, r3;  // e side: e f g h; a side: a b c d
+  uint32_t m;               // a side ~0, e side 0
   uint32_t s1, s2, s3;      // the lane's Sigma rotation counts
 };
 __device__ __forceinline__ void sha2l_init(Sha2L& q, const uint32_t (&v)[8]) {
-  const bool odd = __lane_id() & 1u;
-  q.m = odd ? ~0u : 0u;
+  const bool a = sha2l_aside(__lane_id());
+  q.m = a ? ~0u : 0u;
   // opaque to the compiler: p = r0 ^ (r2 & m) stays one v_bitop3 (as a select
   // of constants it lowers to v_cndmask + v_xor)
   asm("" : "+v"(q.m));
-  q.r0 = odd ? v[0] : v[4];
-  q.r1 = odd ? v[1] : v[5];
-  q.r2 = odd ? v[2] : v[6];
-  q.r3 = odd ? v[3] : v[7];
-  q.s1 = odd ? 2u : 6u;
-  q.s2 = odd ? 13u : 11u;
-  q.s3 = odd ? 22u : 25u;
+  q.r0 = a ? v[0] : v[4];
+  q.r1 = a ? v[1] : v[5];
+  q.r2 = a ? v[2] : v[6];
+  q.r3 = a ? v[3] : v[7];
+  q.s1 = a ? 2u : 6u;
+  q.s2 = a ? 13u : 11u;
+  q.s3 = a ? 22u : 25u;
 }
-// The working state a..h, wave-uniform (read from lanes 1 and 0).
+// The working state a..h, wave-uniform (read from an a-side and an e-side lane).
 __device__ __forceinline__ void sha2l_state(const Sha2L& q, uint32_t (&v)[8]) {
-  v[0] = __builtin_amdgcn_readlane(q.r0, 1);
-  v[1] = __builtin_amdgcn_readlane(q.r1, 1);
-  v[2] = __builtin_amdgcn_readlane(q.r2, 1);
-  v[3] = __builtin_amdgcn_readlane(q.r3, 1);
+  v[0] = __builtin_amdgcn_readlane(q.r0, 4);
+  v[1] = __builtin_amdgcn_readlane(q.r1, 4);
+  v[2] = __builtin_amdgcn_readlane(q.r2, 4);
+  v[3] = __builtin_amdgcn_readlane(q.r3, 4);
   v[4] = __builtin_amdgcn_readlane(q.r0, 0);
   v[5] = __builtin_amdgcn_readlane(q.r1, 0);
   v[6] = __builtin_amdgcn_readlane(q.r2, 0);
   v[7] = __builtin_amdgcn_readlane(q.r3, 0);
 }
+// e side: src(partner) + y; a side keeps old.  The DPP source must not be
+// written by either of the two instructions before (gfx950 DPP hazard, not
+// seen through inline asm): the rounds pass r2, written two rounds earlier (or
+// by sha2l_init before round T0's 11 instructions), and tools/
+// dpp_hazard_check.py, run by build(), verifies every DPP of the built
+// library.  (Round T0 through the compiler's own DPP instead reschedules the
+// whole block: 8.0k instead of 7.5k cycles per node hash.)
+__device__ __forceinline__ uint32_t sha2l_dpp_add_eside(uint32_t old, uint32_t src, uint32_t y) {
+  asm("v_add_u32_dpp %0, %1, %2 row_half_mirror row_mask:0xf bank_mask:0x5" : "+v"(old) : "v"(src), "v"(y));
+  return old;
+}
 // Rounds T0..T1-1; kwf(t) returns K[t] + W[t] (wave-uniform) and is called
 // once per t in increasing order (so it may extend the message schedule).
 template <int T0, int T1, class KWF>
 __device__ __forceinline__ void sha2l_rounds(Sha2L& q, KWF&& kwf) {
-  uint32_t x = (q.r3 + kwf(T0)) & ~q.m;  // even lane: h + K + W; odd lane: 0
+  uint32_t x;  // e side: h + K + W + d (d from the partner); a side: -d
+  {
+    const uint32_t hk = q.r3 + kwf(T0);
+    const uint32_t d = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r3, kSha2lDpp, 0xF, 0xF, false);
+    x = q.m ? 0u - q.r3 : hk + d;
+  }
 #pragma unroll
   for (int t = T0; t < T1; ++t) {
     const uint32_t sg = xor3(__builtin_amdgcn_alignbit(q.r0, q.r0, q.s1),
@@ -336,14 +368,19 @@ __device__ __forceinline__ void sha2l_rounds(Sha2L& q, KWF&& kwf) {
                              __builtin_amdgcn_alignbit(q.r0, q.r0, q.s3));
     const uint32_t p = q.r0 ^ (q.r2 & q.m);       // e | a ^ c
     const uint32_t f = (p & q.r1) | (~p & q.r2);  // Ch | Maj
-    const uint32_t u = sg + f + x;                // T1 | T2
-    const uint32_t y = (q.m & q.r3) | (~q.m & u); // T1 | d
-    if (t + 1 < T1) x = (q.r2 + kwf(t + 1)) & ~q.m;  // the next round's h + K + W
+    const uint32_t u = sg + f + x;                // e' | T2 - d
+    uint32_t xn = 0;
+    if (t + 1 < T1) {  // the next round's x: r2 becomes r3 (g -> h, c -> d)
+      const uint32_t hk = q.r2 + kwf(t + 1);
+      xn = sha2l_dpp_add_eside(0u - q.r2, q.r2, hk);
+    }
     q.r3 = q.r2;
     q.r2 = q.r1;
     q.r1 = q.r0;
-    // pair swap (quad_perm [1,0,3,2]) folded into the add: d + T1 | T1 + T2
-    q.r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)y, 0xB1, 0xF, 0xF, true) + u;
+    // a side: u_e (partner) + u_a; the e side keeps u (bank mask; old 0 is
+    // the add's identity, so this is one v_add_u32_dpp)
+    q.r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, kSha2lDpp, 0xF, 0xA, false) + u;
+    x = xn;
   }
 }
 // Message-schedule word t (t >= 16) in place in w[16].
@@ -355,29 +392,29 @@ __device__ __forceinline__ uint32_t sha_sched(uint32_t* w, int t) {
 }
 
 // Message-schedule word t (t >= 16) in place in w[16] on a lane pair whose two
-// lanes hold the same w: the even lane computes sigma0(w[t-15]) and the odd
-// lane sigma1(w[t-2]) in one instruction stream (per-lane v_alignbit and
-// v_lshrrev counts) and one quad_perm DPP add sums them: 7 VALU per word
-// instead of the one-lane 10.
+// lanes hold the same w: the e side computes sigma0(w[t-15]) and the a side
+// sigma1(w[t-2]) in one instruction stream (per-lane v_alignbit and
+// v_lshrrev counts) and one DPP add sums them: 7 VALU per word instead of the
+// one-lane 10.
 struct Sched2L {
-  uint32_t m;           // odd lane ~0, even lane 0
-  uint32_t c1, c2, c3;  // even: 7, 18, 3 (sigma0); odd: 17, 19, 10 (sigma1)
+  uint32_t m;           // a side ~0, e side 0
+  uint32_t c1, c2, c3;  // e side: 7, 18, 3 (sigma0); a side: 17, 19, 10 (sigma1)
 };
 __device__ __forceinline__ Sched2L sched2l_init() {
-  const bool odd = __lane_id() & 1u;
+  const bool a = sha2l_aside(__lane_id());
   Sched2L c;
-  c.m = odd ? ~0u : 0u;
+  c.m = a ? ~0u : 0u;
   asm("" : "+v"(c.m));
-  c.c1 = odd ? 17u : 7u;
-  c.c2 = odd ? 19u : 18u;
-  c.c3 = odd ? 10u : 3u;
+  c.c1 = a ? 17u : 7u;
+  c.c2 = a ? 19u : 18u;
+  c.c3 = a ? 10u : 3u;
   return c;
 }
 __device__ __forceinline__ uint32_t sha2l_sched(uint32_t* w, int t, const Sched2L& c) {
   const uint32_t x = (w[(t - 2) & 15] & c.m) | (w[(t - 15) & 15] & ~c.m);
   const uint32_t sg = xor3(__builtin_amdgcn_alignbit(x, x, c.c1), __builtin_amdgcn_alignbit(x, x, c.c2),
                            x >> c.c3);
-  uint32_t both = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sg, 0xB1, 0xF, 0xF, true) + sg;
+  uint32_t both = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sg, kSha2lDpp, 0xF, 0xF, true) + sg;
   asm("" : "+v"(both));  // one v_add_u32_dpp (else: v_mov_dpp + a reassociated add)
   return w[t & 15] = both + w[(t - 7) & 15] + w[t & 15];
 }
@@ -385,19 +422,19 @@ __device__ __forceinline__ uint32_t sha2l_sched(uint32_t* w, int t, const Sched2
 // The working state a..h of each lane pair, on both lanes of the pair (one
 // DPP swap per word), for lane pairs that hash different messages.
 __device__ __forceinline__ void sha2l_state_pair(const Sha2L& q, uint32_t (&v)[8]) {
-  const bool odd = q.m != 0u;
-  const uint32_t o0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r0, 0xB1, 0xF, 0xF, true);
-  const uint32_t o1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r1, 0xB1, 0xF, 0xF, true);
-  const uint32_t o2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r2, 0xB1, 0xF, 0xF, true);
-  const uint32_t o3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r3, 0xB1, 0xF, 0xF, true);
-  v[0] = odd ? q.r0 : o0;
-  v[1] = odd ? q.r1 : o1;
-  v[2] = odd ? q.r2 : o2;
-  v[3] = odd ? q.r3 : o3;
-  v[4] = odd ? o0 : q.r0;
-  v[5] = odd ? o1 : q.r1;
-  v[6] = odd ? o2 : q.r2;
-  v[7] = odd ? o3 : q.r3;
+  const bool a = q.m != 0u;
+  const uint32_t o0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r0, kSha2lDpp, 0xF, 0xF, true);
+  const uint32_t o1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r1, kSha2lDpp, 0xF, 0xF, true);
+  const uint32_t o2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r2, kSha2lDpp, 0xF, 0xF, true);
+  const uint32_t o3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q.r3, kSha2lDpp, 0xF, 0xF, true);
+  v[0] = a ? q.r0 : o0;
+  v[1] = a ? q.r1 : o1;
+  v[2] = a ? q.r2 : o2;
+  v[3] = a ? q.r3 : o3;
+  v[4] = a ? o0 : q.r0;
+  v[5] = a ? o1 : q.r1;
+  v[6] = a ? o2 : q.r2;
+  v[7] = a ? o3 : q.r3;
 }
 // sha256_node (SHA-256 of the 64 bytes left || right) on a lane pair: both
 // lanes of the pair pass the same children and get the digest (~20 % less
