@@ -91,6 +91,14 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 #ifndef MLH_LAST_STAGED
 #define MLH_LAST_STAGED 1  // last pass loads through LDS (coalesced runs): pass -3..6 %
 #endif
+#ifndef MLH_LAST_DIRECT
+// last pass (not sharded, full input): phase 1 runs with the lanes of a
+// column on consecutive rows (coalesced 16 B x TPC runs straight from HBM),
+// the first exchange switches to the 8-columns-per-row lane map the later
+// phases and the natural-order stores use: no staged tile, one LDS round trip
+// and one barrier fewer
+#define MLH_LAST_DIRECT 1
+#endif
 #ifndef MLH_LDS_PAD
 #define MLH_LDS_PAD 0  // extra dynamic LDS per pass workgroup (occupancy experiments)
 #endif
@@ -146,8 +154,18 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
 #endif
 
   const int tid = threadIdx.x;
-  const int c = tid % kCols;
-  const int t = tid / kCols;
+  // kDirect: phase 1 with column cA = tid / TPC and t = bitrev(tid mod TPC),
+  // so lane l of a column loads row rev(8t + e) = rev3(e) TPC + l (consecutive
+  // across lanes); the first exchange switches to c = tid mod 8, t = tid / 8
+  constexpr bool kDirect = MLH_LAST_DIRECT && LAST && !SH && ZT == 0 && EPT == 8 && LOGR >= 6;
+  constexpr int kLTPC = LOGR - 3;  // log2 threads per column (EPT = 8)
+  const int cB = tid % kCols;
+  int c = cB;
+  int t = tid / kCols;
+  if constexpr (kDirect) {
+    c = tid >> kLTPC;
+    t = (int)bitrev((uint32_t)tid & ((1u << kLTPC) - 1), kLTPC);
+  }
   const uint64_t vec = (uint64_t)blockIdx.x >> g.ltpv;
   uint64_t tile = blockIdx.x & ((1ull << g.ltpv) - 1);
   if constexpr (SH) {  // this rank's tiles: first-digit columns whose top p bits are the rank
@@ -166,7 +184,7 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     const uint32_t lw = g.lstride;  // W >= kCols
     const uint64_t hi = tile >> (lw - kLogCols), lo = tile & ((1ull << (lw - kLogCols)) - 1);
     base = (hi << (LOGR + lw)) + (lo << kLogCols);
-    jrest = (lo << kLogCols) + c;
+    jrest = (lo << kLogCols) + cB;
     rshift = lw;
     cshift = 0;
   } else {
@@ -175,12 +193,12 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     const uint64_t d1hi = tile >> lmid;
     mid = tile & ((1ull << lmid) - 1);
     base = (d1hi << (kLogCols + lw1)) + (mid << LOGR);
-    k1 = (d1hi << kLogCols) + c;
+    k1 = (d1hi << kLogCols) + cB;
     rshift = 0;
     cshift = lw1;
   }
-  const fe* src = in + base + ((uint64_t)c << cshift);
-  fe* dst = out + base + ((uint64_t)c << cshift);
+  const fe* src = in + base + ((uint64_t)c << cshift);  // phase 1's column
+  fe* dst = out + base + ((uint64_t)cB << cshift);
 
 
   // ---- phase 1: load bit-reversed rows, stages 0..2 in registers ---------
@@ -190,7 +208,7 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   // rows scatter one wave's loads over 64 separate 16-B pieces.  Load the tile
   // as 8 x 128-B runs per wave instruction (8 consecutive rows x 8 columns)
   // into LDS, then read the bit-reversed rows from there.
-  if constexpr (LAST && ZT == 0) {
+  if constexpr (LAST && ZT == 0 && !kDirect) {
     constexpr int NT = kCols * R / EPT;
     // (the staged tile's columns are XOR-swizzled by row: lanes 0..7 write 8
     // consecutive rows of one column, which unswizzled sit 128 B apart on the
@@ -399,7 +417,27 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   constexpr bool kEarly = MLH_P0_EARLY_TB && TW == 0 && LOGR > 2 * LQ;
   if constexpr (LOGR > LQ) {
     constexpr int Q2 = (LOGR - LQ) < LQ ? (LOGR - LQ) : LQ;
-    exchange_and_run(std::integral_constant<int, LQ>{}, std::integral_constant<int, Q2>{});
+    if constexpr (kDirect) {
+      // written in the phase-1 map, read in the 8-columns-per-row map; the
+      // column slot is XORed with the row's top 3 bits, so the 8 lanes of a
+      // write group (consecutive l: distinct top bits of t) and of a read
+      // group (8 columns of one row) each hit 8 distinct 16-B slots
+      auto slot = [&](uint32_t row, int col) -> uint32_t {
+        return row * kCols + ((uint32_t)col ^ ((row >> (LOGR - 3)) & (kCols - 1)));
+      };
+      __syncthreads();  // (the twiddle copy's writes, before the phase-2 reads of lds_tw)
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) fe_store(&lds[slot(pos[e], c)], x[e]);
+      __syncthreads();
+      c = cB;
+      t = tid / kCols;
+      positions(std::integral_constant<int, LQ>{}, std::integral_constant<int, Q2>{}, pos);
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) x[e] = fe_load(&lds[slot(pos[e], c)]);
+      run_phase(std::integral_constant<int, LQ>{}, std::integral_constant<int, Q2>{});
+    } else {
+      exchange_and_run(std::integral_constant<int, LQ>{}, std::integral_constant<int, Q2>{});
+    }
     if constexpr (LOGR > 2 * LQ) {
       constexpr int Q3 = LOGR - 2 * LQ;
       static_assert(Q3 <= LQ, "LOGR <= 3 * LQ");
