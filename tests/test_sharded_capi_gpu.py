@@ -260,3 +260,44 @@ def test_rccl_comm_world1_transport():
         p.join(timeout=60)
     assert "error" not in res, res.get("error")
     assert all(res.values()), res
+
+
+def _rccl_nccl_worker(port, q):
+    """As the driver's N > 1 bench: torch.distributed on its nccl (RCCL)
+    backend, eagerly initialised on the device, and libmlhip's own RCCL
+    communicator beside it (one librccl.so.1 in the process)."""
+    import torch.distributed as tdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        comm = S.RcclComm.from_torch()
+        info = comm.info()
+        bad, ms = S.preflight(comm, 1 << 20)
+        v = torch.ones(1024, device="cuda")
+        tdist.all_reduce(v)  # torch's communicator still works after ours ran
+        torch.cuda.synchronize()
+        comm.close()
+        q.put(dict(info=info, bad=bad, ms=ms, torch_ok=bool(torch.all(v == 1.0))))
+    except Exception:
+        import traceback
+
+        q.put({"error": traceback.format_exc()})
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_rccl_comm_beside_torch_nccl_backend():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_nccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        res = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+    assert "error" not in res, res.get("error")
+    assert res["info"]["ranks"] == 1 and res["info"]["transport"] == "rccl"
+    assert res["bad"] == 0 and res["ms"] >= 0.0 and res["torch_ok"]
