@@ -997,26 +997,39 @@ namespace mlh {
 // Lane-0 round step: (s1, s2) = p(1), p(2) and the claim p(0) + p(1) ->
 // interpolate (closed form on x = 0,1,2), store (c1, c2), absorb them, draw
 // r (stored to r_out) and advance the claim to p(r).
-__device__ __forceinline__ fe round_step(const fe& s1, const fe& s2, fe& claim, DevSha& s,
-                                         uint32_t* stage, fe* poly_out, fe* r_out) {
+// round_step on wave 0 (s1, s2, claim: thread 0's, made wave-uniform): the
+// closed-form interpolation, the absorb and the challenge on the lane pair
+// (dsha2l_step); thread 0 writes the polynomial and returns with the claim p(r).
+__device__ __forceinline__ uint32_t lane0_u32(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ fe lane0_fe(const fe& x) {
+  fe y;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y.w[i] = lane0_u32(x.w[i]);
+  return y;
+}
+__device__ __forceinline__ fe round_step_wave(fe s1, fe s2, fe& claim, DevSha& s, uint32_t* stage,
+                                              fe* poly_out, fe* r_out) {
+  s1 = lane0_fe(s1);
+  s2 = lane0_fe(s2);
+  claim = lane0_fe(claim);
   const fe e0 = fe_sub(claim, s1);
   const fe c2 = fe_half(fe_add(fe_sub(s2, fe_add(s1, s1)), e0));
   const fe c1 = fe_sub(fe_sub(s1, e0), c2);
-  fe_store(poly_out, c1);
-  fe_store(poly_out + 1, c2);
+  if (threadIdx.x == 0) {
+    fe_store(poly_out, c1);
+    fe_store(poly_out + 1, c2);
+  }
   const uint32_t w[8] = {c1.w[0], c1.w[1], c1.w[2], c1.w[3], c2.w[0], c2.w[1], c2.w[2], c2.w[3]};
-  dsha_absorb<8>(s, w, stage);  // LE16(c1) || LE16(c2)
-  const fe r = dsha_challenge(s);
-  fe_store(r_out, r);
+  const fe r = dsha2l_step<8>(s, w, stage, r_out);  // LE16(c1) || LE16(c2), next_challenge()
   claim = fe_add(e0, fe_mul(r, fe_add(c1, fe_mul(c2, r))));
   return r;
 }
 // One two-table round (mlh_sumcheck_prove's per-round path, the PCS's rounds
 // after the eq-factored head, mlh_device_sumcheck_round): reduce the
-// per-workgroup partial (s1, s2) = p(1), p(2) pairs, then lane 0 runs
-// round_step (the closed-form interpolation on x = 0,1,2 of polynomials.rs:51-87,
-// absorb LE16(c1) || LE16(c2) as sumcheck.rs:188-199, r = next_challenge(),
-// claim = p(r)).
+// per-workgroup partial (s1, s2) = p(1), p(2) pairs, then wave 0 runs
+// round_step_wave (the closed-form interpolation on x = 0,1,2 of
+// polynomials.rs:51-87, absorb LE16(c1) || LE16(c2) as sumcheck.rs:188-199,
+// r = next_challenge() on the lane pair, claim = p(r)).
 __global__ void __launch_bounds__(kRedThreads)
 sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev, DevSha* t,
                       fe* poly_out, fe* r_out) {
@@ -1036,10 +1049,12 @@ sumcheck_round_kernel(const fe* __restrict__ partials, uint32_t nparts, fe* prev
     s2 = fe_add(s2, fe_load(partials + 2 * i + 1));
   }
   block_reduce2(s1, s2);  // (its barriers also publish the staged state)
-  if (threadIdx.x != 0) return;
-  round_step(s1, s2, p, s, stage, poly_out, r_out);
-  *t = s;
-  fe_store(prev, p);
+  if (threadIdx.x >= 64) return;
+  round_step_wave(s1, s2, p, s, stage, poly_out, r_out);
+  if (threadIdx.x == 0) {
+    *t = s;
+    fe_store(prev, p);
+  }
 }
 
 // out = P + Q (R + S T): the one two-modmul form every lane-parallel step of

@@ -557,23 +557,25 @@ __device__ __forceinline__ void sha2l_compress_into(uint32_t (&h)[8], const uint
 }
 
 // Transcript step on a lane pair, for a caller whose whole wave runs it
-// (uniform control flow; lanes 0 and 1 carry the two-lane SHA-256, the others
-// compute the same): absorb the NW words w (memory byte order, wave-uniform)
-// into s (shared memory; lane 0 writes it), then (r_out) write
-// next_challenge() to r_out.  Same state and challenge as dsha_absorb +
+// (uniform control flow; every lane pair carries the two-lane SHA-256 of the
+// same words): absorb the NW words w (memory byte order, wave-uniform) into s
+// (shared memory; lane 0 writes it), then (r_out) write next_challenge() to
+// r_out and return it (wave-uniform; lane 0's on the one-lane path).  Same
+// state and challenge as dsha_absorb +
 // dsha_challenge, with the compressions at ~2.5 instead of ~4.3 us.  A
 // length not a multiple of 4 (bytes absorbed on the host) takes the one-lane
 // path.
 template <int NW>
-__device__ void dsha2l_step(DevSha& s, const uint32_t (&w)[NW], uint32_t* stage, fe* r_out) {
+__device__ fe dsha2l_step(DevSha& s, const uint32_t (&w)[NW], uint32_t* stage, fe* r_out) {
   const uint32_t lane = __lane_id();
   const uint64_t len0 = s.len;
   if (len0 & 3) {
+    fe r = fe_zero();
     if (lane == 0) {
       dsha_absorb<NW>(s, w, stage);
-      if (r_out) fe_store(r_out, dsha_challenge(s));
+      if (r_out) fe_store(r_out, r = dsha_challenge(s));
     }
-    return;
+    return r;  // (lane 0's)
   }
   uint32_t* bw = reinterpret_cast<uint32_t*>(s.buf);
   uint32_t h[8], blk[16];
@@ -612,7 +614,7 @@ __device__ void dsha2l_step(DevSha& s, const uint32_t (&w)[NW], uint32_t* stage,
     for (int i = 0; i < 16; ++i) bw[i] = bswap32(blk[i]);
     s.len = len;
   }
-  if (!r_out) return;
+  if (!r_out) return fe_zero();
   // next_challenge(): finalize a copy -- 0x80, zeros, the bit length
   const uint64_t bits = len * 8;
 #pragma unroll
@@ -629,7 +631,9 @@ __device__ void dsha2l_step(DevSha& s, const uint32_t (&w)[NW], uint32_t* stage,
   fe v;
 #pragma unroll
   for (int i = 0; i < 4; ++i) v.w[i] = bswap32(h[i]);
-  if (lane == 0) fe_store(r_out, canon_with_carry(v, 0u));
+  const fe r = canon_with_carry(v, 0u);
+  if (lane == 0) fe_store(r_out, r);
+  return r;
 }
 
 // absorb n bytes from device memory, then (if r_out) write next_challenge();
