@@ -291,9 +291,10 @@ __device__ __forceinline__ Sha256State shah_node(const Sha256State& l, const Sha
 }
 
 // MODE 1: lane pairs (node = lane >> 1), MODE 3: half mirror (node = 4 (lane >> 3) + min(k, 7 - k), k = lane & 7)
-template <int MODE>
+template <int MODE, int ACTIVE = 64>
 __global__ void __launch_bounds__(64) chain(int iters, uint32_t* out, unsigned long long* clk) {
   const uint32_t lane = threadIdx.x;
+  if (lane >= (uint32_t)ACTIVE) return;  // a partly active wave (the tree tail's small levels)
   const uint32_t hk = lane & 7;  // half mirror: lanes k and 7 - k of a half row share a node
   const uint32_t id = MODE == 1 ? lane >> 1 : (((lane >> 3) << 2) | (hk < 4 ? hk : 7 - hk));
   const bool lead = MODE == 1 ? (lane & 1) == 0 : ((lane >> 2) & 1) == 0;  // MODE 2: the library's (half mirror)
@@ -312,20 +313,21 @@ __global__ void __launch_bounds__(64) chain(int iters, uint32_t* out, unsigned l
     for (int i = 0; i < 8; ++i) out[id * 8 + i] = a.h[i];
 }
 
-template <int MODE>
+template <int MODE, int ACTIVE = 64>
 int run(const char* name, int iters, uint32_t* d, unsigned long long* clk, uint32_t* host) {
-  hipLaunchKernelGGL(chain<MODE>, dim3(1), dim3(64), 0, 0, iters, d, clk);
+  hipLaunchKernelGGL((chain<MODE, ACTIVE>), dim3(1), dim3(64), 0, 0, iters, d, clk);
   CHECK(hipDeviceSynchronize());
   unsigned long long best = ~0ull;
   for (int r = 0; r < 7; ++r) {
-    hipLaunchKernelGGL(chain<MODE>, dim3(1), dim3(64), 0, 0, iters, d, clk);
+    hipLaunchKernelGGL((chain<MODE, ACTIVE>), dim3(1), dim3(64), 0, 0, iters, d, clk);
     CHECK(hipDeviceSynchronize());
     unsigned long long h;
     CHECK(hipMemcpy(&h, clk, 8, hipMemcpyDeviceToHost));
     if (h < best) best = h;
   }
   CHECK(hipMemcpy(host, d, 32 * 8 * 4, hipMemcpyDeviceToHost));
-  printf("{\"layout\": \"%s\", \"cycles_per_node\": %.0f}\n", name, (double)best / iters);
+  printf("{\"layout\": \"%s\", \"active_lanes\": %d, \"cycles_per_node\": %.0f}\n", name, ACTIVE,
+         (double)best / iters);
   return 0;
 }
 
@@ -341,6 +343,12 @@ int main() {
   static uint32_t h2[256], h4[256];
   if (run<2>("library sha2l_node", it, d, clk, h2)) return 1;
   if (run<4>("half mirror, first round's x through the compiler's DPP", it, d, clk, h4)) return 1;
+  static uint32_t hx[256];
+  for (int a = 0; a < 3; ++a) {  // partly active waves: 32, 16, 8 lanes
+    if (a == 0 && (run<1, 32>("lane pair", it, d, clk, hx) || run<2, 32>("library sha2l_node", it, d, clk, hx))) return 1;
+    if (a == 1 && (run<1, 16>("lane pair", it, d, clk, hx) || run<2, 16>("library sha2l_node", it, d, clk, hx))) return 1;
+    if (a == 2 && (run<1, 8>("lane pair", it, d, clk, hx) || run<2, 8>("library sha2l_node", it, d, clk, hx))) return 1;
+  }
   int bad = 0;
   for (int i = 0; i < 256; ++i) bad += (h1[i] != h3[i]) + (h2[i] != h3[i]) + (h4[i] != h3[i]);
   printf("{\"digests_equal\": %s, \"mismatched_words\": %d}\n", bad ? "false" : "true", bad);
