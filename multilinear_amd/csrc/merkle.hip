@@ -229,12 +229,14 @@ subtree_kernel(const uint8_t* __restrict__ level, uint64_t n, uint8_t* __restric
     const uint32_t mp = m / 2;
     __syncthreads();
     // levels after the first have at most half a node per thread: a lane
-    // pair per node (two-lane SHA-256, ~20 % less latency per level)
-    const uint32_t node = sha2l_pair(t);
+    // pair per node (two-lane SHA-256, ~20 % less latency per level) once the
+    // pairs fit one wave per SIMD (pair_level), one lane per node before
+    const bool two = pair_level(mp);
+    const uint32_t node = two ? sha2l_pair(t) : t;
     const bool active = node < mp;
-    if (active) r = sha2l_node(s[2 * node], s[2 * node + 1]);
+    if (active) r = two ? sha2l_node(s[2 * node], s[2 * node + 1]) : sha256_node(s[2 * node], s[2 * node + 1]);
     __syncthreads();
-    if (active && sha2l_lead(t)) {
+    if (active && (!two || sha2l_lead(t))) {
       s[node] = r;
       digest_store(out + (off + b * mp + node) * 32, r);
     }
@@ -305,7 +307,10 @@ hipError_t launch_merkle_levels_from(uint8_t* layers, uint64_t off, uint64_t n, 
     }
   }
   if (n > 1) {
-    const unsigned threads = n / 2 < 64 ? 64 : (unsigned)(n / 2);
+    // n <= the pair limit: a thread per digest, so that the first level runs
+    // on lane pairs too
+    const unsigned threads = n <= MLH_PAIR_LEVELS_MAX ? (n < 64 ? 64 : (unsigned)n)
+                                                       : (n / 2 < 64 ? 64 : (unsigned)(n / 2));
     hipLaunchKernelGGL(top_kernel, dim3(1), dim3(threads), 0, st, layers + off * 32, n,
                        layers + (off + n) * 32, ra);
   } else if (ra.t) {  // the level is the root already (one leaf)

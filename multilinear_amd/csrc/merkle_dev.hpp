@@ -27,9 +27,18 @@ extern __device__ uint64_t g_tree_ts[4][64];
   } while (0)
 #endif
 
+#ifndef MLH_PAIR_LEVELS_MAX
+// a level is hashed on lane pairs only while its 2 np lanes are at most one
+// wave per SIMD of the CU (4 x 64): beyond that the pairs' 22 lane-instructions
+// per round-node lose to the single lane's 14 (the level is issue-bound)
+#define MLH_PAIR_LEVELS_MAX 256
+#endif
+__device__ __forceinline__ bool pair_level(uint64_t np) {
+  return 2 * np <= blockDim.x && 2 * np <= MLH_PAIR_LEVELS_MAX;
+}
 // The levels above the n digests in s (shared memory, n a power of two) up to
 // the root s[0], each level written to out consecutively (level order); a
-// level with at most half a node per thread hashes each node on a lane pair
+// level of few nodes (pair_level) hashes each node on a lane pair
 // (sha2l_node).  Every thread of the workgroup calls it.
 __device__ __forceinline__ void lds_tree_levels(Sha256State* s, uint64_t n, uint8_t* __restrict__ out,
                                                 int ts_k = 1) {
@@ -38,7 +47,7 @@ __device__ __forceinline__ void lds_tree_levels(Sha256State* s, uint64_t n, uint
   while (n > 1) {
     const uint64_t np = n / 2;
     Sha256State r;
-    const bool two = 2 * np <= blockDim.x;
+    const bool two = pair_level(np);
     const uint32_t node = two ? sha2l_pair(threadIdx.x) : threadIdx.x;
     const bool active = node < np;
     if (active) r = two ? sha2l_node(s[2 * node], s[2 * node + 1]) : sha256_node(s[2 * node], s[2 * node + 1]);
