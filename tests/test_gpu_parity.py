@@ -188,8 +188,11 @@ def test_reed_solomon_matches_oracle(log_n):
     assert host(MF.reed_solomon(dev(vals), g)) == OF.reed_solomon(vals, g)
 
 
-@pytest.mark.parametrize("log_code", [1, 2, 3, 11, 13])
+@pytest.mark.parametrize("log_code", [1, 2, 3, 9, 10, 11, 12, 13, 15, 19])
 def test_merkle_commit_pairs_matches_oracle(log_code):
+    """Every layer against the oracle; the sizes walk the tree tails' level
+    policy: top_kernel with 64..1024 digests (pairs for n <= 256, single lanes
+    above), subtree_kernel chunks below and at 2^16 digests."""
     code = rand_vals(1 << log_code, 31 + log_code)
     want = OF.commit_rs_code(code)
     got = MM.Merkle.commit_pairs(dev(code))
