@@ -167,7 +167,8 @@ class BatchedFriProverData:
         """self.fri_data: the inner FriProverData (a view; this object owns it)."""
         from .fri import FriProverData
 
-        return FriProverData(lib().mlh_batched_fri_prover_inner(self.h), self._codes, owned=False)
+        return FriProverData(lib().mlh_batched_fri_prover_inner(self.h), self._codes, owned=False,
+                             owner=self)
 
     @property
     def batch_root(self):

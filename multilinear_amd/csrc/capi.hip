@@ -800,6 +800,11 @@ mlh_status mlh_fri_prover_init_gp(mlh_ctx* ctx, const void* dev_code, uint32_t l
 // underflows (a panic, MLH_ERR_INVALID here); its callers pass k in sequence.
 static mlh_status fold_step_impl(mlh_ctx* ctx, mlh_fri_prover* p, u128 gen, uint32_t log_gp,
                                  uint32_t k, const uint8_t r[16], mlh_transcript* tr) {
+  // a batched prover's inner view has no tree before batched_fold_step, nor
+  // after a step that produced the last element directly (log_code 2); the
+  // reference panics on merkle_trees.last().unwrap() there
+  if (p->layers.empty())
+    return fail(ctx, MLH_ERR_INVALID, "fold_step before any tree (batched_fold_step not applied)");
   const FriLayer& cur = p->layers.back();
   const uint32_t log_n = cur.log_n;  // n = 2 * pairs
   const uint64_t blowup = 1ull << MLH_LOG_BLOWUP;
@@ -807,7 +812,9 @@ static mlh_status fold_step_impl(mlh_ctx* ctx, mlh_fri_prover* p, u128 gen, uint
   // (after the last element, the reference folds its last tree again and
   // re-absorbs the element: layers.back() is still that tree here, too)
   const uint64_t half_n = 1ull << (log_n - 1);
-  if (k > 40 || ((half_n - 1) << k) > (1ull << log_gp))
+  // (log space first: half_n - 1 < 2^(log_n - 1), so with (log_n - 1) + k <= 62
+  // the shift cannot wrap 64 bits; beyond it the product exceeds any table)
+  if (k > 40 || (log_n - 1) + k > 62 || ((half_n - 1) << k) > (1ull << log_gp))
     return fail(ctx, MLH_ERR_INVALID, "gen_pows index len - i*2^k underflows (fri/mod.rs:106-110)");
   const fe *tlo, *thi;
   MLH_TRY(fold_tables_g(ctx, gen, log_gp, &tlo, &thi));

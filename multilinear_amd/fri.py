@@ -46,10 +46,11 @@ def fold_layer(layer, k, log_domain, r, device=0):
 class FriProverData:
     """fri/mod.rs:10-175, device resident.  The code tensor must outlive it."""
 
-    def __init__(self, handle, code, owned=True):
+    def __init__(self, handle, code, owned=True, owner=None):
         self.h = handle
         self._code = code
         self._owned = owned  # False: a view of a handle another object owns
+        self._owner = owner  # that object, kept alive as long as the view
 
     def __del__(self):
         if not getattr(self, "_owned", True):

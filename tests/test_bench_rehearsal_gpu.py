@@ -18,14 +18,14 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(extra_env, args, timeout):
+def _run(extra_env, args, timeout, nproc=2):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     env = dict(os.environ, MLH_BENCH_BACKEND="gloo", **extra_env)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2"] + args
+           "--gpus", str(nproc)] + args
     t0 = time.time()
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -56,3 +56,33 @@ def test_rehearsal_n2_stalled_all_to_all_reports_phase():
     assert "did not finish within 20 s" in d["headline_error"]
     assert d["comm"]["ranks"] == 2 and d["rccl_ranks"] is None
     assert dt < 100
+
+
+_CHECKS = ("config5_matches_single_gpu", "config3_sharded_matches_single_gpu",
+           "config4_sharded_matches_single_gpu")
+
+
+@pytest.mark.timeout(320)
+@pytest.mark.parametrize("nproc,corrupt", [(2, None), (4, None), (2, "1")])
+def test_rehearsal_extras_certify_against_single_gpu(nproc, corrupt):
+    """Every N > 1 extra carries an in-run parity bit against a single-GPU
+    recompute on rank 0 (config 5: the sharded proof's wire bytes vs
+    reed_solomon + FriProof::prove of the gathered coefficients; config 3
+    sharded: the root vs commit_rs_code of the gathered code; config 4 sharded:
+    every round polynomial and challenge vs the single-GPU prove; strong NTT:
+    the headline's spot check).  With one rank's shard altered after the timed
+    loops (MLH_BENCH_TEST_CORRUPT_SHARD) every bit is false and the line is
+    still printed."""
+    env = {} if corrupt is None else {"MLH_BENCH_TEST_CORRUPT_SHARD": corrupt}
+    p, lines, _ = _run(env, ["--log-n", "16", "--steps", "3", "--warmup", "1", "--spinup-s", "0",
+                             "--no-cpu", "--fri-log", "20", "--strong-log", "20", "--extra-reps", "1"],
+                       300, nproc)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines) == 1, p.stdout + p.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == nproc and d["sharded_ntt_verified"] is True
+    want = corrupt is None
+    for k in _CHECKS:
+        assert d.get(k) is want, (k, d.get(k), {x: d.get(x) for x in d if x.endswith("_error")})
+    assert d["strong_ntt"]["verified"] is want
+    assert d["config5_verified"] is True  # the host verifier accepts either proof

@@ -1126,6 +1126,56 @@ def test_batched_fri_prover_step_api_reference_shape(m, log_n):
         bp.batched_fold_step((gp[1], L), r, tr)
 
 
+def test_batched_inner_fold_step_without_tree_rejected():
+    """fri_data.fold_step on a batched prover whose inner FriProverData holds no
+    tree -- before batched_fold_step, and at log_code 2 where that step wrote
+    the last element directly -- is MLH_ERR_INVALID (the reference panics on
+    merkle_trees.last().unwrap()); a fri_data view keeps its parent alive."""
+    import gc
+
+    from multilinear_amd.batched import BatchedFriProverData
+
+    for log_n in (1, 3):
+        L = log_n + 1
+        gp = F.pow_2_generator_powers(L)
+        codes = [OF.reed_solomon([F.from_i64(5 * i + j) for i in range(1 << log_n)], gp[1])
+                 for j in range(2)]
+        tr = Transcript()
+        bp = BatchedFriProverData.init(dev([v for c in codes for v in c]), 2, tr)
+        fd = bp.fri_data
+        with pytest.raises(_lib.MlhError) as e:
+            fd.fold_step(1, 5, tr, gen_pows=(gp[1], L))
+        assert e.value.status == _lib.MLH_ERR_INVALID
+        bp.batched_fold_step((gp[1], L), tr.next_challenge(), tr)
+        if log_n == 1:  # last element written, still no tree
+            assert fd.last_element is not None
+            with pytest.raises(_lib.MlhError) as e:
+                fd.fold_step(1, 5, tr, gen_pows=(gp[1], L))
+            assert e.value.status == _lib.MLH_ERR_INVALID
+        else:
+            del bp
+            gc.collect()
+            before = fd.fold_roots()
+            fd.fold_step(1, tr.next_challenge(), tr, gen_pows=(gp[1], L))
+            assert fd.fold_roots()[:len(before)] == before and len(fd.fold_roots()) == len(before) + 1
+
+
+def test_fri_fold_step_huge_k_rejected():
+    """k large enough that (n/2 - 1) 2^k wraps 64 bits is still rejected
+    (MLH_ERR_INVALID, the reference's usize index underflow), not folded."""
+    L = 12
+    g = F.pow_2_generator(L)
+    code = OF.reed_solomon([F.from_i64(7 * i + 3) for i in range(1 << (L - 1))], g)
+    tr = Transcript()
+    pd = MF.FriProverData.init(dev(code), tr)
+    n0 = len(pd.fold_roots())
+    for k in (2, 40, 41):
+        with pytest.raises(_lib.MlhError) as e:
+            pd.fold_step(k, 3, tr)
+        assert e.value.status == _lib.MLH_ERR_INVALID
+    assert len(pd.fold_roots()) == n0
+
+
 def test_batched_fri_large_verifies():
     from multilinear_amd.batched import BatchedFriProof
 

@@ -60,13 +60,18 @@ class ThreadDeviceTransport:
         self.done = [self._event() for _ in range(P)]
         self.send = [None] * P
         self.error = []
+        self.calls = []  # rank 0's collectives in order: ("a2a", bytes per peer) / ("ag", bytes)
 
         def a2a(user, send, recv, per, stream):  # (void* arguments arrive as int or None)
             me = user or 0
+            if me == 0:
+                self.calls.append(("a2a", per))
             return self._run(me, send, stream, lambda s, src: self._copy(
                 (recv or 0) + s * per, (src or 0) + ((me + a2a_shift) % P) * per, per, stream))
 
         def ag(user, send, recv, nbytes, stream):
+            if (user or 0) == 0:
+                self.calls.append(("ag", nbytes))
             return self._run(user or 0, send, stream, lambda s, src: self._copy(
                 (recv or 0) + s * nbytes, src, nbytes, stream))
 
@@ -395,3 +400,94 @@ def test_fri_and_sumcheck_device_ordered_vs_oracle(P, log_code, gather_log, n_sc
         for q, gq in enumerate(res[0][5]):
             for (gv, gs), (wv, wpath) in zip(gq, want.queries[q]):
                 assert gv == wv and gs == [s for s, _ in wpath]
+
+
+# ---- config 5 at its production shape (bench.config5 at N = 8 / 4 / 2) ----
+
+_C5 = {}
+
+
+def _config5_reference():
+    """The 2^27 coefficients, the C oracle's RS code and FRI commit, and the
+    single-GPU proof (mlh_reed_solomon + mlh_fri_prove) of the same code --
+    computed once for the three world sizes."""
+    if not _C5:
+        import gc
+
+        from multilinear_amd import fri as MF
+
+        log_c = 27
+        coeffs = DV.random_limbs(1 << log_c, seed=5151)
+        g = _gen(log_c + 1)
+        dcode = MF.reed_solomon(DV.to_device(coeffs), g)
+        single = MF.FriProof.prove(dcode, Transcript())
+        code1 = DV.from_device(dcode)
+        del dcode
+        gc.collect()
+        torch.cuda.empty_cache()
+        want = C.reed_solomon_par(coeffs, log_c, g)
+        assert np.array_equal(code1, want), "single-GPU RS 2^27 -> 2^28 differs from the C oracle"
+        del code1
+        roots, last, lr, rc = C.fri_commit_par(want, log_c + 1)
+        assert rc == 0
+        _C5.update(coeffs=coeffs, g=g, want=want, roots=roots, last=last, single=single,
+                   single_bytes=single.to_bytes())
+        # the single-GPU proof against the oracle commit: every root, the last element
+        assert single.commitments == roots and single.last_elem == last
+        assert single.verify()
+    return _C5
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("P", [8, 4, 2])
+def test_config5_sharded_prove_production_shape(P):
+    """bench.config5's exact calls at N = P: mlh_sharded_reed_solomon of the
+    2^27 cyclic coefficients, then mlh_sharded_fri_prove(log_code 28,
+    gather_log 16) through device-ordered collectives.  The unsharded code
+    equals the C oracle's RS code; every rank's proof equals, byte for byte
+    (bincode wire form: all 27 commitments, the 128 query records, the last
+    element, the final digest), the single-GPU mlh_fri_prove of the same
+    natural-order code, whose commitments and last element equal the C
+    oracle's fri_commit.  At P = 8 the path runs the re-deal all-to-alls of
+    the 2^25, 2^22 and 2^19 layers and the all-gather of the 2^16 layer
+    (fri/mod.rs:261-285)."""
+    ref = _config5_reference()
+    L = DV.lib()
+    log_code, gather_log = 28, 16
+    coeffs, g = ref["coeffs"], ref["g"]
+    tr = ThreadDeviceTransport(P)
+
+    def body(r, ctx, st, t):
+        c_loc = DV.to_device(S.shard_cyclic(coeffs, P, r))
+        code = DV.empty(2 * c_loc.shape[0])
+        torch.cuda.current_stream().synchronize()
+        DV.check(L.mlh_sharded_reed_solomon(ctx, _tp(t), DV.ptr(c_loc), log_code - 1, DV.fe_bytes(g),
+                                            DV.ptr(code)), ctx)
+        del c_loc
+        pf = FriProof(log_code)
+        DV.check(L.mlh_sharded_fri_prove(ctx, _tp(t), DV.ptr(code), log_code, gather_log,
+                                         Transcript().h, ctypes.byref(pf.c)), ctx)
+        DV.check(L.mlh_synchronize(ctx), ctx)
+        return DV.from_device(code), pf.to_bytes(), pf.verify()
+
+    res = _run_ranks(P, body, tr)
+    p = P.bit_length() - 1
+    got = S.unshard_blocks([res[r][0] for r in range(P)], log_code - 2 * p)
+    for r in range(P):
+        res[r] = (None,) + tuple(res[r][1:])
+    bad = np.nonzero((got != ref["want"]).any(axis=1))[0]
+    assert bad.size == 0, "sharded RS mismatches at %s of %d" % (bad[:8].tolist(), bad.size)
+    del got
+    for r in range(P):
+        assert res[r][1] == ref["single_bytes"], "rank %d: proof differs from the single-GPU proof" % r
+        assert res[r][2], "rank %d: proof rejected by the verifier" % r
+    # the schedule ran what bench.config5 runs: re-deals of the folded layers
+    # above gather_log (bytes per peer = 16 * 2^log_next / P^2), then one
+    # all-gather of the first layer at or below it (16 * 2^log / P per rank)
+    redeals = sorted({(per // 16).bit_length() - 1 + 2 * p for kind, per in tr.calls if kind == "a2a"})
+    gathers = {(nb // 16).bit_length() - 1 + p for kind, nb in tr.calls if kind == "ag" and nb % 16 == 0}
+    if P == 8:
+        assert {19, 22, 25} <= set(redeals), redeals
+    assert gather_log in gathers, sorted(gathers)
+    assert max(lg for lg in redeals if lg < log_code) > gather_log
