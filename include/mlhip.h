@@ -83,6 +83,8 @@ mlh_status mlh_set_coop_spin_limit(mlh_ctx* ctx, uint32_t sleeps);
 mlh_status mlh_set_pcs_fused_max(mlh_ctx* ctx, uint32_t max_vars);
 mlh_status mlh_set_stream(mlh_ctx* ctx, void* hip_stream);
 mlh_status mlh_synchronize(mlh_ctx* ctx);
+/* The message of ctx's last failure; with ctx == NULL, why this thread's last
+ * mlh_context_create failed. */
 const char* mlh_last_error(const mlh_ctx* ctx);
 mlh_status mlh_malloc(mlh_ctx* ctx, size_t bytes, void** dev);
 mlh_status mlh_free(mlh_ctx* ctx, void* dev);

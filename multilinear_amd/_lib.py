@@ -243,6 +243,12 @@ def load():
             "libmlhip.so not built at %s -- run `python -c 'import __graft_entry__ as g; g.build()'`"
             % LIB_PATH
         )
+    # torch first: its wheel bundles its own HIP runtime (libamdhip64.so.7, the
+    # same soname as /opt/rocm's), and a process must hold ONE of them.  Loaded
+    # before torch, libmlhip would bind /opt/rocm's runtime while torch maps its
+    # own beside it, and that second runtime sees no device.
+    import torch  # noqa: F401
+
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -315,12 +315,26 @@ extern "C" {
 
 const char* mlh_version(void) { return "mlhip 0.1 (gfx950)"; }
 
+// why the last mlh_context_create of this thread failed (no context to hold it):
+// mlh_last_error(NULL) returns it
+static thread_local char g_create_err[160] = "null context";
+
 mlh_status mlh_context_create(int device, void* hip_stream, mlh_ctx** out) {
   if (!out) return MLH_ERR_INVALID;
   *out = nullptr;
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return MLH_ERR_HIP;
-  if (hipSetDevice(device) != hipSuccess) return MLH_ERR_HIP;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= device || device < 0) {
+    snprintf(g_create_err, sizeof g_create_err, "mlh_context_create: hipGetDeviceCount -> %s, %d devices, device %d",
+             hipGetErrorString(e), n, device);
+    return MLH_ERR_HIP;
+  }
+  e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    snprintf(g_create_err, sizeof g_create_err, "mlh_context_create: hipSetDevice(%d) -> %s", device,
+             hipGetErrorString(e));
+    return MLH_ERR_HIP;
+  }
   std::unique_ptr<mlh_ctx> c(new mlh_ctx());
   c->device = device;
   c->stream = reinterpret_cast<hipStream_t>(hip_stream);
@@ -332,6 +346,8 @@ mlh_status mlh_context_create(int device, void* hip_stream, mlh_ctx** out) {
                   hipHostMalloc(&c->pinned, kPinnedBytes, 0) == hipSuccess &&
                   hipHostMalloc(&st, 64, hipHostMallocCoherent) == hipSuccess;
   if (!ok) {  // (hipFree / hipHostFree of a null pointer are no-ops)
+    snprintf(g_create_err, sizeof g_create_err, "mlh_context_create: allocation failed (%s)",
+             hipGetErrorString(hipGetLastError()));
     (void)hipFree(c->partials);
     (void)hipFree(c->small);
     (void)hipHostFree(c->pinned);
@@ -408,7 +424,7 @@ mlh_status mlh_synchronize(mlh_ctx* ctx) {
   return MLH_OK;
 }
 
-const char* mlh_last_error(const mlh_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* mlh_last_error(const mlh_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err; }
 
 mlh_status mlh_malloc(mlh_ctx* ctx, size_t bytes, void** dev) {
   if (!ctx || !dev) return MLH_ERR_INVALID;

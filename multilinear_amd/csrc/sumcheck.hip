@@ -1064,12 +1064,23 @@ __device__ __forceinline__ fe pqrst(const fe& P, const fe& Q, const fe& R, const
                                     const fe& T) {
   return fe_add(P, fe_mul_s(fe_add(R, fe_mul_s(S, T)), Q));
 }
+// A wave-uniform field element kept in VGPRs.  Left in SGPRs, the compiler
+// runs the uniform arithmetic on the one scalar unit of the CU: 128-bit adds
+// as s_add/s_addc with the carry moved through s_cselect / s_cmp per limb
+// (three to four instructions per limb instead of one v_addc), which is most
+// of a helper wave's time per round.
+__device__ __forceinline__ fe fe_vgpr(fe x) {
+  asm volatile("" : "+v"(x.w[0]), "+v"(x.w[1]), "+v"(x.w[2]), "+v"(x.w[3]));
+  return x;
+}
+// An LDS entry every lane reads (a uniform address) into VGPRs.
+__device__ __forceinline__ fe lds_fe(const fe& x) { return fe_vgpr(x); }
 // The same lane's value as a wave-uniform (v_readlane): no LDS round trip.
 __device__ __forceinline__ fe bcast_fe(const fe& x, int src) {
   fe r;
 #pragma unroll
   for (int i = 0; i < 4; ++i) r.w[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.w[i], src);
-  return r;
+  return fe_vgpr(r);
 }
 __device__ __forceinline__ fe shfl_fe(const fe& x, int src) {
   fe r;
@@ -1355,6 +1366,29 @@ __device__ void transcript_rehearsal(CoopSync& S, const DevSha& s, const uint32_
   }
 }
 
+// Lane-keyed choices among wave-uniform values.  Written as one chain of
+// ternaries on the lane index, the compiler turns them into a lookup table in
+// scratch memory (stores of the candidates, a lane-indexed scratch load: an L2
+// round trip on the serial chain, ~1 us per choice).  Each comparison here
+// reads its own opaque copy of the lane index, so every choice stays a
+// v_cndmask.
+__device__ __forceinline__ bool lane_is(uint32_t k) {
+  uint32_t l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l == k;
+}
+__device__ __forceinline__ bool lane_below(uint32_t k) {
+  uint32_t l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l < k;
+}
+__device__ __forceinline__ fe fe_if(bool c, const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.w[i] = c ? a.w[i] : b.w[i];
+  return r;
+}
+
 // Values of round t's four quadratics at r (lane j < 4 evaluates quadratic j).
 // (Cross-lane values move by v_readlane: an LDS round trip measured slower.)
 __device__ __forceinline__ void quad_eval(const fe* q, const fe& r, fe& c1, fe& c2, fe& e0, fe& cs) {
@@ -1370,33 +1404,35 @@ __device__ __forceinline__ void quad_eval(const fe* q, const fe& r, fe& c1, fe& 
 // r B_b, the claim quadratic (cl0, cl1, cl2) = (e0', c1, c2) of round t-1 and
 // its eq scale cs; p = p_t, pp = p_{t-1}.  first: round t is the launch's first
 // (cl0, cs constants; cl1 = cl2 = 0, B_b = 0).  Products on lanes, two deep.
-__device__ void quad_next(bool first, const fe& cl0, const fe& cl1, const fe& cl2, const fe& cs,
+__device__ __forceinline__ void quad_next(bool first, const fe& cl0, const fe& cl1, const fe& cl2, const fe& cs,
                           const fe& A0, const fe& B0, const fe& A1, const fe& B1, const fe& p,
-                          const fe& pp, fe* q) {
+                          const fe& pp, fe* q, uint32_t tq = 0) {
   const uint32_t lane = threadIdx.x & 63;
+  (void)tq;
+  MLH_COOP_TS(9, 32 + 2 * tq);
   const fe one = fe_one();
   const fe p3 = fe_add(fe_dbl(p), p), qq = fe_sub(p3, one);
   const fe D0 = fe_sub(fe_dbl(A1), A0), D1 = fe_sub(fe_dbl(B1), B0);
   // lanes 0..5: U = c (1 - pp), V = c (2 pp - 1), q D0, p A1, q D1, p B1
-  const fe a1 = lane < 2 ? cs : ((lane & 1) ? p : qq);
-  const fe b1 = lane == 0 ? fe_sub(one, pp)
-                          : (lane == 1 ? fe_sub(fe_dbl(pp), one)
-                                       : (lane == 2 ? D0 : (lane == 3 ? A1 : (lane == 4 ? D1 : B1))));
+  const fe a1 = fe_if(lane_below(2), cs, fe_if((lane & 1) != 0, p, qq));
+  const fe b1 = fe_if(lane_is(0), fe_sub(one, pp),
+                      fe_if(lane_is(1), fe_sub(fe_dbl(pp), one),
+                            fe_if(lane_is(2), D0, fe_if(lane_is(3), A1, fe_if(lane_is(4), D1, B1)))));
   fe y = fe_mul_s(a1, b1);
-  if (first && lane < 2) y = lane == 0 ? cs : fe_zero();
+  if (first) y = fe_if(lane_is(0), cs, fe_if(lane_is(1), fe_zero(), y));
   const fe U = bcast_fe(y, 0), V = bcast_fe(y, 1), pA1 = bcast_fe(y, 3), pB1 = bcast_fe(y, 5);
+  MLH_COOP_TS(9, 33 + 2 * tq);
   const fe f0 = fe_sub(bcast_fe(y, 2), fe_add(fe_dbl(pA1), pA1));
   const fe f1 = fe_sub(bcast_fe(y, 4), fe_add(fe_dbl(pB1), pB1));
   // lanes 0..7: U f0, V f0, U f1, V f1, U h0, V h0, U h1, V h1 (h = p A1, p B1)
-  const uint32_t j = (lane >> 1) & 3;
-  const fe b2 = j == 0 ? f0 : (j == 1 ? f1 : (j == 2 ? pA1 : pB1));
-  const fe z = fe_mul_s((lane & 1) ? V : U, b2);
+  const fe b2 = fe_if(lane_below(2), f0, fe_if(lane_below(4), f1, fe_if(lane_below(6), pA1, pB1)));
+  const fe z = fe_mul_s(fe_if((lane & 1) != 0, V, U), b2);
   const fe Uf0 = bcast_fe(z, 0), Vf0 = bcast_fe(z, 1), Uf1 = bcast_fe(z, 2), Vf1 = bcast_fe(z, 3);
   const fe Uh0 = bcast_fe(z, 4), Vh0 = bcast_fe(z, 5), Uh1 = bcast_fe(z, 6), Vh1 = bcast_fe(z, 7);
   // lane k < 3: coefficient k of Y = (U+Vr)(f0+f1 r), X = (U+Vr)(h0+h1 r), the claim
-  const fe Yk = lane == 0 ? Uf0 : (lane == 1 ? fe_add(Uf1, Vf0) : Vf1);
-  const fe Xk = lane == 0 ? Uh0 : (lane == 1 ? fe_add(Uh1, Vh0) : Vh1);
-  const fe Ck = lane == 0 ? cl0 : (lane == 1 ? cl1 : cl2);
+  const fe Yk = fe_if(lane_is(0), Uf0, fe_if(lane_is(1), fe_add(Uf1, Vf0), Vf1));
+  const fe Xk = fe_if(lane_is(0), Uh0, fe_if(lane_is(1), fe_add(Uh1, Vh0), Vh1));
+  const fe Ck = fe_if(lane_is(0), cl0, fe_if(lane_is(1), cl1, cl2));
   const fe c2 = fe_half(fe_add(Yk, Ck));
   const fe c1 = fe_sub(fe_sub(fe_dbl(Xk), Ck), c2);
   const fe e0 = fe_sub(Ck, Xk);
@@ -1404,7 +1440,7 @@ __device__ void quad_next(bool first, const fe& cl0, const fe& cl1, const fe& cl
     q[lane] = c1;
     q[3 + lane] = c2;
     q[6 + lane] = e0;
-    q[9 + lane] = lane == 0 ? U : (lane == 1 ? V : fe_zero());
+    q[9 + lane] = fe_if(lane_is(0), U, fe_if(lane_is(1), V, fe_zero()));
   }
 }
 
@@ -1420,6 +1456,40 @@ __device__ __forceinline__ void bucket_sums(fe x, uint32_t mt, uint32_t me, fe (
     Sb[1] = bcast_fe(x, (int)me);
     Sb[3] = bcast_fe(x, (int)(mt | me));
   }
+}
+
+// K = 2 or 4 values per lane, summed over the lanes that agree on the bits
+// in `excl` (the bucket bits), with ONE value per lane left: the first
+// log2 K of the other bits halve the set (the lane with that bit clear keeps
+// the lower half and sends the upper), the rest are plain butterfly levels --
+// log2 K + (6 - |excl| - log2 K) exchanges instead of K x (6 - |excl|).
+// Value k of bucket pattern e is then on lane e | hb(k): bit hb[0] set iff
+// k >> (log2 K - 1), bit hb[1] (K = 4) iff k & 1.
+template <int K>
+__device__ __forceinline__ fe bucket_halve(const fe (&v)[K], uint32_t excl, uint32_t (&hb)[2]) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t m1 = ~excl & (excl + 1u);                 // lowest bit not in excl
+  const uint32_t m2 = ~(excl | m1) & ((excl | m1) + 1u);  // the next one
+  fe z;
+  uint32_t done = excl | m1;
+  if constexpr (K == 4) {
+    const bool b1 = (lane & m1) != 0;
+    fe k0 = fe_add(fe_if(b1, v[2], v[0]), shfl_xor_fe(fe_if(b1, v[0], v[2]), (int)m1));
+    fe k1 = fe_add(fe_if(b1, v[3], v[1]), shfl_xor_fe(fe_if(b1, v[1], v[3]), (int)m1));
+    const bool b2 = (lane & m2) != 0;
+    z = fe_add(fe_if(b2, k1, k0), shfl_xor_fe(fe_if(b2, k0, k1), (int)m2));
+    hb[0] = m1;
+    hb[1] = m2;
+    done |= m2;
+  } else {
+    const bool b1 = (lane & m1) != 0;
+    z = fe_add(fe_if(b1, v[1], v[0]), shfl_xor_fe(fe_if(b1, v[0], v[1]), (int)m1));
+    hb[0] = m1;
+    hb[1] = 0;
+  }
+  for (uint32_t m = 1; m < 64; m <<= 1)
+    if (!(m & done)) z = fe_add(z, shfl_xor_fe(z, (int)m));
+  return z;
 }
 
 // Suffix products Rs of a group (J <= 6 variables, points pv in HBM) into
@@ -1467,7 +1537,7 @@ __device__ void corner_rounds(CoopSync& S, uint32_t JA, uint32_t JB, uint32_t u0
   {  // the r's of earlier launches (u0 <= 5): loads first, then the products
     fe rk[6];
 #pragma unroll
-    for (uint32_t v = 0; v < 6; ++v) rk[v] = v < u0 ? fe_load(rs_known + v) : one;
+    for (uint32_t v = 0; v < 6; ++v) rk[v] = v < u0 ? fe_vgpr(fe_load(rs_known + v)) : one;
 #pragma unroll
     for (uint32_t v = 0; v < 6; ++v)
       if (v < u0) {
@@ -1480,47 +1550,104 @@ __device__ void corner_rounds(CoopSync& S, uint32_t JA, uint32_t JB, uint32_t u0
     const bool inB = v >= JA;
     const uint32_t J = inB ? JB : JA, u = inB ? v - JA : v, t = v - u0;
     const bool first = t == 0;
+    const uint32_t mt = 1u << (J - 1 - u);
+    // A regular round (variable v - 2 in the same group, its challenge r_{t-2}
+    // the one awaited) is linear in that challenge: with P_c = L_c Rs_u[c]
+    // (L without v - 2's factor), E_b = sum_c P_c g_c(r), g_c = r or 1 - r by
+    // the corner's bit md of v - 2.  So the products and the shuffle levels
+    // over the bits other than (md, me, mt) run BEFORE r_{t-2} is out; after
+    // it, one product, one level and the four broadcasts (the weights' update
+    // follows the publish).
+    const bool regular = u >= 2 && v - 2 >= u0;
+    const uint32_t me_r = 1u << (J - u), md = 1u << (J + 1 - u);
+    fe Pr = fe_zero();
+    if (regular) {
+      fe x = fe_mul_s(L, inB ? S.rsufB[u][c] : S.rsuf[u][c]);
+      for (uint32_t m = 1; m < 64; m <<= 1)
+        if (m != mt && m != me_r && m != md) x = fe_add(x, shfl_xor_fe(x, (int)m));
+      Pr = x;
+    }
+    // Group B's first two rounds are linear in their awaited challenge too.
+    // Round u = 0 (r_4 awaited): the corner sums fold the split table with r_3
+    // (known) and r_4, n_b5 = lo_b5 + r_4 (hi_b5 - lo_b5), so X_a = n_0 and
+    // X_b = n_1 - n_0 are a + r_4 a' and b + r_4 b', and their bucket sums
+    // (split by mt) are taken before r_4.  Round u = 1 (r_5 awaited): L = X_a +
+    // r_5 X_b, the bucket sums of X_a Rs_1 and X_b Rs_1 (split by mt, me) before
+    // r_5.  After the challenge: one product on four lanes.
+    const bool b0r = inB && u == 0, b1r = inB && u == 1;
+    fe Tz = fe_zero(), la = fe_zero(), lb = fe_zero(), ma = fe_zero(), mb = fe_zero();
+    uint32_t hb[2] = {0, 0};
+    if (b0r) {
+      lds_wait_ge(S, &S.r_seq, 4 - u0);  // r_3
+      lds_wait_ge(S, &S.mseq, 1);
+      const fe r3 = lds_fe(S.rsh[3 - u0]);
+      const uint32_t qb = 1u << JB;  // split table: msp[d qb + x], d = bits of variables 3, 4, 5
+      const fe* M = msp + (c < qb ? c : 0);
+      const fe lo0 = lerp_s(M[qb * 0], M[qb * 4], r3), hi0 = lerp_s(M[qb * 2], M[qb * 6], r3);
+      const fe lo1 = lerp_s(M[qb * 1], M[qb * 5], r3), hi1 = lerp_s(M[qb * 3], M[qb * 7], r3);
+      const bool live = c < qb;
+      la = live ? lo0 : fe_zero();
+      ma = live ? fe_sub(hi0, lo0) : fe_zero();
+      lb = live ? fe_sub(lo1, lo0) : fe_zero();
+      mb = live ? fe_sub(fe_sub(hi1, lo1), fe_sub(hi0, lo0)) : fe_zero();
+      const fe R0 = S.rsufB[0][c];
+      const fe vv[4] = {fe_mul_s(la, R0), fe_mul_s(ma, R0), fe_mul_s(lb, R0), fe_mul_s(mb, R0)};
+      Tz = bucket_halve<4>(vv, mt, hb);
+    } else if (b1r) {
+      const fe R1 = S.rsufB[1][c];
+      const fe vv[2] = {fe_mul_s(Xa, R1), fe_mul_s(Xb, R1)};
+      Tz = bucket_halve<2>(vv, mt | me_r, hb);
+    }
     fe rv = fe_zero();
     if (t >= 2) {
       lds_wait_ge(S, &S.r_seq, t - 1);
-      rv = S.rsh[t - 2];
-    }
-    if (inB && u == 0) {  // group B's corner sums: fold the split table with r_3, r_4
-      lds_wait_ge(S, &S.mseq, 1);
-      const fe r3 = S.rsh[3 - u0];
-      const uint32_t qb = 1u << JB;  // split table: msp[d qb + x], d = bits of variables 3, 4, 5
-      fe n[2];
-#pragma unroll
-      for (uint32_t b5 = 0; b5 < 2; ++b5) {
-        const fe* M = msp + (c < qb ? c : 0);
-        const fe lo = lerp_s(M[qb * (0 | b5)], M[qb * (4 | b5)], r3);  // (b4 = 0; b3 = 0, 1)
-        const fe hi = lerp_s(M[qb * (2 | b5)], M[qb * (6 | b5)], r3);  // (b4 = 1)
-        n[b5] = lerp_s(lo, hi, rv);                                     // r_4
-      }
-      const bool live = c < (1u << JB);
-      Xa = live ? n[0] : fe_zero();
-      Xb = live ? fe_sub(n[1], n[0]) : fe_zero();
-      W = one;
-    } else if (inB && u == 1) {
-      L = fe_add(Xa, fe_mul_s(rv, Xb));  // the corner sums at r_5
-      Xact = L;
-    } else if (u >= 2 && v - 2 >= u0) {
-      const fe g = gsel(v - 2, rv);
-      L = fe_mul_s(L, g);
-      W = fe_mul_s(W, g);
+      rv = lds_fe(S.rsh[t - 2]);
     }
     MLH_COOP_TS(6, t);
-    const uint32_t mt = 1u << (J - 1 - u);
     fe Sb[4];
     fe A0, B0 = fe_zero(), A1, B1 = fe_zero();
-    if (inB && u == 0) {
-      const fe R0 = S.rsufB[0][c];
-      bucket_sums(fe_mul_s(Xa, R0), mt, 0, Sb);
-      A0 = Sb[0];
-      A1 = Sb[2];
-      bucket_sums(fe_mul_s(Xb, R0), mt, 0, Sb);
-      B0 = Sb[0];
-      B1 = Sb[2];
+    fe greg = one;
+    if (regular) {
+      greg = (c & md) ? rv : fe_sub(one, rv);  // gsel(v - 2, rv)
+      fe y = fe_mul_s(Pr, greg);
+      y = fe_add(y, shfl_xor_fe(y, (int)md));
+      A0 = bcast_fe(y, 0);
+      A1 = bcast_fe(y, (int)mt);
+      B0 = fe_sub(bcast_fe(y, (int)me_r), A0);
+      B1 = fe_sub(bcast_fe(y, (int)(mt | me_r)), A1);
+    } else if (b0r || b1r) {
+      // lane j < 4: output j = base + r slope, base / slope = bucket sums
+      // (value k, bucket e) on lane e | hb(k)
+      const uint32_t j = c & 3;
+      uint32_t e, kb, ks;  // bucket, base value, slope value
+      if (b0r) {  // A0, A1 from (a, a'), B0, B1 from (b, b'); buckets 0, mt
+        e = (j & 1) ? mt : 0u;
+        kb = (j >> 1) ? 2u : 0u;
+        ks = kb + 1;
+      } else {  // Sb[0..3] over buckets 0, me, mt, mt | me; values X_a (0), X_b (1)
+        e = ((j & 2) ? mt : 0u) | ((j & 1) ? me_r : 0u);
+        kb = 0;
+        ks = 1;
+      }
+      auto at = [&](uint32_t k) -> int {
+        return (int)(e | (b0r ? (((k >> 1) ? hb[0] : 0u) | ((k & 1) ? hb[1] : 0u)) : (k ? hb[0] : 0u)));
+      };
+      const fe o = fe_add(shfl_fe(Tz, at(kb)), fe_mul_s(rv, shfl_fe(Tz, at(ks))));
+      if (b0r) {
+        A0 = bcast_fe(o, 0);
+        A1 = bcast_fe(o, 1);
+        B0 = bcast_fe(o, 2);
+        B1 = bcast_fe(o, 3);
+      } else {
+        Sb[0] = bcast_fe(o, 0);
+        Sb[1] = bcast_fe(o, 1);
+        Sb[2] = bcast_fe(o, 2);
+        Sb[3] = bcast_fe(o, 3);
+        A0 = Sb[0];
+        A1 = Sb[2];
+        B0 = fe_sub(Sb[1], Sb[0]);
+        B1 = fe_sub(Sb[3], Sb[2]);
+      }
     } else {
       const fe x = fe_mul_s(L, inB ? S.rsufB[u][c] : S.rsuf[u][c]);
       const uint32_t me = (first || u == 0) ? 0u : 1u << (J - u);
@@ -1541,6 +1668,17 @@ __device__ void corner_rounds(CoopSync& S, uint32_t JA, uint32_t JB, uint32_t u0
     }
     lds_publish(&S.ab_seq, t + 1);
     MLH_COOP_TS(7, t);
+    if (regular) {  // the weights take v - 2's factor (used from the next round on)
+      L = fe_mul_s(L, greg);
+      W = fe_mul_s(W, greg);
+    } else if (b0r) {  // group B's corner sums at r_4
+      Xa = fe_add(la, fe_mul_s(rv, ma));
+      Xb = fe_add(lb, fe_mul_s(rv, mb));
+      W = one;
+    } else if (b1r) {  // ... and at r_5
+      L = fe_add(Xa, fe_mul_s(rv, Xb));
+      Xact = L;
+    }
   }
   if (!wout && !m_out && !wfold) return;
   // the last round's variables: r of the one before it, then its own
@@ -1548,20 +1686,20 @@ __device__ void corner_rounds(CoopSync& S, uint32_t JA, uint32_t JB, uint32_t u0
   fe rv = fe_zero();
   if (tl >= 1) {
     lds_wait_ge(S, &S.r_seq, tl);
-    rv = S.rsh[tl - 1];
+    rv = lds_fe(S.rsh[tl - 1]);
   }
   if (vl >= JA && ul == 0)
     Xact = fe_add(Xa, fe_mul_s(rv, Xb));  // a one-variable group B: m_6 at r_5
   else if (ul >= 1 && vl - 1 >= u0)
     W = fe_mul_s(W, gsel(vl - 1, rv));    // (the loop took the variables before)
   lds_wait_ge(S, &S.r_seq, tl + 1);
-  W = fe_mul_s(W, gsel(vl, S.rsh[tl]));
+  W = fe_mul_s(W, gsel(vl, lds_fe(S.rsh[tl])));
   if (wout && c < (1u << JA)) fe_store(wout + c, W);
   if (wfold) {  // the fold weights of both groups: W_A at wfold[0..64), W_B at wfold[64..)
     fe WA = W;
     if (JB) {
       WA = one;
-      for (uint32_t v = 0; v < JA; ++v) WA = fe_mul_s(WA, gsel(v, S.rsh[v - u0]));
+      for (uint32_t v = 0; v < JA; ++v) WA = fe_mul_s(WA, gsel(v, lds_fe(S.rsh[v - u0])));
       if (c < (1u << JB)) fe_store(wfold + 64 + c, W);
     }
     if (c < (1u << JA)) fe_store(wfold + c, WA);
@@ -1589,15 +1727,19 @@ __device__ void coef_rounds(CoopSync& S, uint32_t u0, uint32_t vend, fe* prev, f
     fe rv = fe_zero();
     if (t >= 2) {
       lds_wait_ge(S, &S.r_seq, t - 1);
-      rv = S.rsh[t - 2];
+      rv = lds_fe(S.rsh[t - 2]);
     }
     MLH_COOP_TS(5, t);
     if (!first) quad_eval(S.poly[(t - 1) & 1], rv, c1v, c2v, e0v, csv);  // round t-1's values
     lds_wait_ge(S, &S.ab_seq, t + 1);
-    const fe* ab = S.ab[t & 1];
+    const fe* abp = S.ab[t & 1];
+    const fe ab[4] = {lds_fe(abp[0]), lds_fe(abp[1]), lds_fe(abp[2]), lds_fe(abp[3])};
     MLH_COOP_TS(8, t);
-    quad_next(first, first ? claim0 : e0v, c1v, c2v, first ? cs0 : csv, ab[0], ab[1], ab[2], ab[3],
-              S.pg[v], v ? S.pg[v - 1] : fe_zero(), S.poly[t & 1]);
+    // (values, not `first ? claim0 : e0v` bound to a reference: a choice
+    // between two lvalues is a choice of addresses, which puts both in scratch)
+    const fe cl0 = fe_if(first, claim0, e0v), csx = fe_if(first, cs0, csv);
+    const fe pv = lds_fe(S.pg[v]), ppv = v ? lds_fe(S.pg[v - 1]) : fe_zero();
+    quad_next(first, cl0, c1v, c2v, csx, ab[0], ab[1], ab[2], ab[3], pv, ppv, S.poly[t & 1], t);
     lds_publish(&S.coef_seq, t + 1);
     MLH_COOP_TS(4, t);
   }
@@ -1606,12 +1748,12 @@ __device__ void coef_rounds(CoopSync& S, uint32_t u0, uint32_t vend, fe* prev, f
   fe rv = fe_zero();
   if (tl >= 1) {
     lds_wait_ge(S, &S.r_seq, tl);
-    rv = S.rsh[tl - 1];
+    rv = lds_fe(S.rsh[tl - 1]);
   }
   quad_eval(S.poly[tl & 1], rv, c1v, c2v, e0v, csv);
   lds_wait_ge(S, &S.r_seq, tl + 1);
-  const fe r = S.rsh[tl];
-  const fe p = S.pg[vl];
+  const fe r = lds_fe(S.rsh[tl]);
+  const fe p = lds_fe(S.pg[vl]);
   const fe claim = pqrst(e0v, r, c1v, c2v, r);
   const fe scale = fe_mul_s(csv, pqrst(fe_sub(one, p), r, fe_sub(fe_dbl(p), one), fe_zero(), fe_zero()));
   if (c == 0) {
@@ -1824,9 +1966,32 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
       for (uint32_t u = 0; u < 3; ++u) {
         lds_wait_ge(S, &S.r_seq, u + 1);
         MLH_COOP_TS(9, 2 + 2 * u);
-        const fe r = S.rsh[u];
+        const fe r = lds_fe(S.rsh[u]);
         n >>= 1;
-        for (uint32_t i = lane; i < n; i += 64) lm[i] = lerp_s(lm[i], lm[i + n], r);
+        if (n % 256 == 0) {
+          // four lerps per lane per step, loads first (their LDS latency
+          // overlaps), the products as generated butterflies with r expanded
+          // (u + r d, d = hi - lo: 60 VALU per pair half instead of ~100)
+          const fe two32 = fe{{0u, 1u, 0u, 0u}};
+          const fe R1 = fe_mul_s(r, two32), R2 = fe_mul_s(R1, two32), R3 = fe_mul_s(R2, two32);
+          for (uint32_t i0 = lane; i0 < n; i0 += 256) {
+            fe a[4], d[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+              a[k] = lm[i0 + 64 * k];
+              d[k] = lm[i0 + 64 * k + n];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) d[k] = fe_sub(d[k], a[k]);
+            uint64_t rare;
+            bfly_mm_v(a[0], d[0], r, R1, R2, R3, a[1], d[1], r, R1, R2, R3, rare);
+            bfly_mm_v(a[2], d[2], r, R1, R2, R3, a[3], d[3], r, R1, R2, R3, rare);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) lm[i0 + 64 * k] = relaxed_canon(a[k]);
+          }
+        } else {
+          for (uint32_t i = lane; i < n; i += 64) lm[i] = lerp_s(lm[i], lm[i + n], r);
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next level reads other lanes' entries
         MLH_COOP_TS(9, 3 + 2 * u);
       }

@@ -37,7 +37,9 @@ def context(device=0):
     c = _ctx.get(device)
     if c is None:
         h = ctypes.c_void_p()
-        check(lib().mlh_context_create(device, ctypes.c_void_p(st), ctypes.byref(h)))
+        st_ = lib().mlh_context_create(device, ctypes.c_void_p(st), ctypes.byref(h))
+        if st_ != _lib.MLH_OK:
+            raise _lib.MlhError(st_, (lib().mlh_last_error(None) or b"").decode())
         c = h.value
         _ctx[device] = c
     else:

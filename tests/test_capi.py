@@ -41,6 +41,7 @@ def test_no_gpu_means_loud_failure():
     lib = _lib.load()
     h = ctypes.c_void_p()
     assert lib.mlh_context_create(0, None, ctypes.byref(h)) == 4  # MLH_ERR_HIP, no fallback
+    assert b"hipGetDeviceCount" in lib.mlh_last_error(None)  # the reason, without a context
 
 
 def test_generators_match_oracle():

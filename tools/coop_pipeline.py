@@ -58,3 +58,6 @@ for k in range(2, R):
 print("helper: round  eval  ->ab  ->slot")
 for k in range(1, R):
     print("       %5d %6.2f %6.2f %6.2f" % (k, us(T[8][k] - T[5][k]), 0.0, us(T[4][k] - T[8][k])))
+print("quad_next: round  start->y-bcast  y-bcast->published")
+for k in range(R):
+    print("       %5d %8.2f %8.2f" % (k, us(T[9][33 + 2 * k] - T[9][32 + 2 * k]), us(T[4][k] - T[9][33 + 2 * k])))
