@@ -59,6 +59,15 @@ __device__ __forceinline__ fe fe_mul_s(const fe& a, const fe& b) {
   return fe_mul(a, b);
 #endif
 }
+// A wave-uniform field element kept in VGPRs.  Left in SGPRs, the compiler
+// runs the uniform arithmetic on the one scalar unit of the CU: 128-bit adds
+// as s_add/s_addc with the carry moved through s_cselect / s_cmp per limb
+// (three to four instructions per limb instead of one v_addc), which was most
+// of a helper wave's time per round.
+__device__ __forceinline__ fe fe_vgpr(fe x) {
+  asm volatile("" : "+v"(x.w[0]), "+v"(x.w[1]), "+v"(x.w[2]), "+v"(x.w[3]));
+  return x;
+}
 __device__ __forceinline__ fe lerp_s(const fe& lo, const fe& hi, const fe& r) {
   return fe_add(lo, fe_mul_s(fe_sub(hi, lo), r));
 }
@@ -109,14 +118,16 @@ __device__ __forceinline__ void pcs_round_body(const PcsJob& J) {
   }
   block_reduce2(E0, E1);
   if (threadIdx.x != 0) return;
+  // (one lane's serial chain: its operands in VGPRs, fe_vgpr)
   const fe one = fe_one();
-  fe claim = fe_load(&st->claim), c = fe_load(&st->c);
+  fe claim = fe_vgpr(fe_load(&st->claim)), c = fe_vgpr(fe_load(&st->c));
   if (r_prev) {  // the previous round's claim p(r) and eq scale
-    const fe pp = fe_load(p_prev);
-    claim = fe_add(fe_load(&st->e0), fe_mul_s(fe_add(fe_load(&st->c1), fe_mul_s(fe_load(&st->c2), r)), r));
-    c = fe_mul_s(c, fe_add(fe_mul_s(fe_sub(one, r), fe_sub(one, pp)), fe_mul_s(r, pp)));
+    const fe pp = fe_vgpr(fe_load(p_prev)), rv = fe_vgpr(r);
+    claim = fe_add(fe_vgpr(fe_load(&st->e0)),
+                   fe_mul_s(fe_add(fe_vgpr(fe_load(&st->c1)), fe_mul_s(fe_vgpr(fe_load(&st->c2)), rv)), rv));
+    c = fe_mul_s(c, fe_add(fe_mul_s(fe_sub(one, rv), fe_sub(one, pp)), fe_mul_s(rv, pp)));
   }
-  const fe p = fe_load(p_k);
+  const fe p = fe_vgpr(fe_load(p_k));
   const fe s1 = fe_mul_s(c, fe_mul_s(p, E1));
   const fe s2 = fe_mul_s(fe_mul_s(c, fe_sub(fe_add(fe_dbl(p), p), one)), fe_sub(fe_dbl(E1), E0));
   const fe e0 = fe_sub(claim, s1);

@@ -1064,15 +1064,7 @@ __device__ __forceinline__ fe pqrst(const fe& P, const fe& Q, const fe& R, const
                                     const fe& T) {
   return fe_add(P, fe_mul_s(fe_add(R, fe_mul_s(S, T)), Q));
 }
-// A wave-uniform field element kept in VGPRs.  Left in SGPRs, the compiler
-// runs the uniform arithmetic on the one scalar unit of the CU: 128-bit adds
-// as s_add/s_addc with the carry moved through s_cselect / s_cmp per limb
-// (three to four instructions per limb instead of one v_addc), which is most
-// of a helper wave's time per round.
-__device__ __forceinline__ fe fe_vgpr(fe x) {
-  asm volatile("" : "+v"(x.w[0]), "+v"(x.w[1]), "+v"(x.w[2]), "+v"(x.w[3]));
-  return x;
-}
+// (fe_vgpr: sc_dev.hpp)
 // An LDS entry every lane reads (a uniform address) into VGPRs.
 __device__ __forceinline__ fe lds_fe(const fe& x) { return fe_vgpr(x); }
 // The same lane's value as a wave-uniform (v_readlane): no LDS round trip.
@@ -1500,7 +1492,7 @@ __device__ __forceinline__ void suffix_products(uint32_t J, const fe* pv, fe (*r
   const fe one = fe_one();
   fe p[6];
 #pragma unroll
-  for (int u = 0; u < 6; ++u) p[u] = u < (int)J ? fe_load(pv + u) : one;
+  for (int u = 0; u < 6; ++u) p[u] = u < (int)J ? fe_vgpr(fe_load(pv + u)) : one;
   fe acc = one;
 #pragma unroll
   for (int u = 5; u >= 0; --u) {

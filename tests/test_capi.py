@@ -211,8 +211,9 @@ def test_host_pcs_verifier_accepts_oracle_proof():
     pc = _lib.PcsProofC()
     pc.fri = c
     pc.sumcheck_polys = ctypes.cast(polys, ctypes.c_void_p)
-    assert lib.mlh_pcs_verify(ctypes.byref(pc), n, _points(pts), fe_bytes(out), Transcript().h) == 0
-    assert lib.mlh_pcs_verify(ctypes.byref(pc), n, _points(pts), fe_bytes(out + 1), Transcript().h) == 7
+    t1, t2 = Transcript(), Transcript()  # (alive across the calls: the C side takes their pointers)
+    assert lib.mlh_pcs_verify(ctypes.byref(pc), n, _points(pts), fe_bytes(out), t1.h) == 0
+    assert lib.mlh_pcs_verify(ctypes.byref(pc), n, _points(pts), fe_bytes(out + 1), t2.h) == 7
 
 
 def test_fri_proof_wire_format_matches_oracle_encoding():

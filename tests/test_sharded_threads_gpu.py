@@ -15,8 +15,10 @@ cannot.  Every result is compared with the oracle (C restatement
 oracle/c/oracle.c, and oracle/fri.py for whole proofs at small sizes).
 """
 import ctypes
+import os
 import random
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -66,12 +68,14 @@ class ThreadDeviceTransport:
             me = user or 0
             if me == 0:
                 self.calls.append(("a2a", per))
+                _progress("a2a %d" % per)
             return self._run(me, send, stream, lambda s, src: self._copy(
                 (recv or 0) + s * per, (src or 0) + ((me + a2a_shift) % P) * per, per, stream))
 
         def ag(user, send, recv, nbytes, stream):
             if (user or 0) == 0:
                 self.calls.append(("ag", nbytes))
+                _progress("ag %d" % nbytes)
             return self._run(user or 0, send, stream, lambda s, src: self._copy(
                 (recv or 0) + s * nbytes, src, nbytes, stream))
 
@@ -407,6 +411,15 @@ def test_fri_and_sumcheck_device_ordered_vs_oracle(P, log_code, gather_log, n_sc
 _C5 = {}
 
 
+def _progress(msg):
+    """Progress lines for a long GPU test (MLH_TEST_PROGRESS=<file>): the
+    long phases of the config-5 test leave a trace even if it is killed."""
+    path = os.environ.get("MLH_TEST_PROGRESS")
+    if path:
+        with open(path, "a") as f:
+            f.write("%.1f %s\n" % (time.time(), msg))
+
+
 def _config5_reference():
     """The 2^27 coefficients, the C oracle's RS code and FRI commit, and the
     single-GPU proof (mlh_reed_solomon + mlh_fri_prove) of the same code --
@@ -417,6 +430,7 @@ def _config5_reference():
         from multilinear_amd import fri as MF
 
         log_c = 27
+        _progress("config5 reference: start")
         coeffs = DV.random_limbs(1 << log_c, seed=5151)
         g = _gen(log_c + 1)
         dcode = MF.reed_solomon(DV.to_device(coeffs), g)
@@ -425,10 +439,13 @@ def _config5_reference():
         del dcode
         gc.collect()
         torch.cuda.empty_cache()
+        _progress("config5 reference: single-GPU prove done")
         want = C.reed_solomon_par(coeffs, log_c, g)
+        _progress("config5 reference: oracle RS done")
         assert np.array_equal(code1, want), "single-GPU RS 2^27 -> 2^28 differs from the C oracle"
         del code1
         roots, last, lr, rc = C.fri_commit_par(want, log_c + 1)
+        _progress("config5 reference: oracle commit done")
         assert rc == 0
         _C5.update(coeffs=coeffs, g=g, want=want, roots=roots, last=last, single=single,
                    single_bytes=single.to_bytes())
@@ -440,7 +457,7 @@ def _config5_reference():
 
 @pytest.mark.slow
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("P", [8, 4, 2])
+@pytest.mark.parametrize("P", [2, 4, 8])
 def test_config5_sharded_prove_production_shape(P):
     """bench.config5's exact calls at N = P: mlh_sharded_reed_solomon of the
     2^27 cyclic coefficients, then mlh_sharded_fri_prove(log_code 28,
@@ -464,14 +481,24 @@ def test_config5_sharded_prove_production_shape(P):
         torch.cuda.current_stream().synchronize()
         DV.check(L.mlh_sharded_reed_solomon(ctx, _tp(t), DV.ptr(c_loc), log_code - 1, DV.fe_bytes(g),
                                             DV.ptr(code)), ctx)
+        DV.check(L.mlh_synchronize(ctx), ctx)
+        _progress("P=%d rank %d: sharded RS done" % (P, r))
         del c_loc
         pf = FriProof(log_code)
+        trx = Transcript()  # (kept alive across the call: the C side holds its pointer)
         DV.check(L.mlh_sharded_fri_prove(ctx, _tp(t), DV.ptr(code), log_code, gather_log,
-                                         Transcript().h, ctypes.byref(pf.c)), ctx)
+                                         trx.h, ctypes.byref(pf.c)), ctx)
         DV.check(L.mlh_synchronize(ctx), ctx)
-        return DV.from_device(code), pf.to_bytes(), pf.verify()
+        _progress("P=%d rank %d: sharded prove done" % (P, r))
+        host = DV.from_device(code)
+        _progress("P=%d rank %d: code copied out" % (P, r))
+        wire = pf.to_bytes()
+        ok = pf.verify()
+        _progress("P=%d rank %d: proof encoded and verified" % (P, r))
+        return host, wire, ok
 
     res = _run_ranks(P, body, tr)
+    _progress("P=%d: ranks joined" % P)
     p = P.bit_length() - 1
     got = S.unshard_blocks([res[r][0] for r in range(P)], log_code - 2 * p)
     for r in range(P):
@@ -479,6 +506,7 @@ def test_config5_sharded_prove_production_shape(P):
     bad = np.nonzero((got != ref["want"]).any(axis=1))[0]
     assert bad.size == 0, "sharded RS mismatches at %s of %d" % (bad[:8].tolist(), bad.size)
     del got
+    _progress("P=%d: code compared" % P)
     for r in range(P):
         assert res[r][1] == ref["single_bytes"], "rank %d: proof differs from the single-GPU proof" % r
         assert res[r][2], "rank %d: proof rejected by the verifier" % r
