@@ -1848,9 +1848,9 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
   HIP_TRY(ctx, launch_sumcheck_eq_tail(es.B ? es.m : es.src, 0, nullptr, es.a, es.Hs,
                                        es.pts + es.B, es.c, prev, dt, polys + 2 * es.B, rs + es.B,
                                        es.m, dfin, ctx->stream, coop_ctl(ctx),
-                                       es.kw ? es.kw + 64 * es.B : nullptr));
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pinned, polys, 48ull * L + 16, hipMemcpyDeviceToHost,
-                              ctx->stream));
+                                       es.kw ? es.kw + 64 * es.B : nullptr,
+                                       HostOut{reinterpret_cast<const uint8_t*>(polys), ctx->pinned,
+                                               (uint32_t)(48ull * L + 16)}));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   MLH_TRY(device_check(ctx));
   std::vector<uint8_t> host(ctx->pinned, ctx->pinned + 48ull * L + 16);

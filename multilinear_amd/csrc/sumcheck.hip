@@ -803,10 +803,12 @@ eq_setup_kernel(const EqSetupArgs args, fe* __restrict__ pts_out, fe* __restrict
   } else {
     return;
   }
+  // (the chain of products is the launch's critical path, one thread per
+  // entry: the generated asm multiply, operands in VGPRs)
   fe acc = fe_one();
   for (uint32_t i = 0; i < cnt; ++i) {
-    const fe p = q[n - 1 - i];
-    acc = fe_mul(acc, ((j >> i) & 1) ? p : fe_sub(fe_one(), p));
+    const fe p = fe_vgpr(q[n - 1 - i]);
+    acc = fe_mul_s(acc, ((j >> i) & 1) ? p : fe_sub(fe_one(), p));
   }
   fe_store(out, acc);
 }
@@ -1337,7 +1339,8 @@ __device__ void transcript_rounds(CoopSync& S, uint32_t R, DevSha& s, uint32_t* 
 // path), run by wave 0 itself while round 0's coefficients are being built;
 // otherwise the padding-block challenge, run by an idle wave.
 #ifndef MLH_REH
-#define MLH_REH 2  // 0: none; 1: wave 3 a round + the pad challenge; 2: wave 0 a round, wave 3 the pad
+#define MLH_REH 2  // 0: none; 1: wave 3 a round + the pad challenge; 2: wave 0 a round, wave 3 the pad;
+                   // 3: as 2, the eq tail's wave-0 round during its prologue loads
 #endif
 __device__ void transcript_rehearsal(CoopSync& S, const DevSha& s, const uint32_t* kw, bool round) {
   if (round) {  // one half-block round on a scratch state
@@ -1805,7 +1808,7 @@ sumcheck_group_kernel(const fe* __restrict__ partials, uint32_t nb, uint32_t J, 
   __syncthreads();
   MLH_COOP_EDGE(1);
   if (wave == 0) {
-    if (MLH_REH == 2) transcript_rehearsal(S, s, kwx, true);
+    if (MLH_REH >= 2) transcript_rehearsal(S, s, kwx, true);
     transcript_rounds(S, tend - t0, s, stage, polys, rs + t0, kwx, false, S.mid, &S.mid_len);
     if (lane == 0) *t = s;
   } else if (wave == 1) {
@@ -1843,7 +1846,7 @@ __global__ void __launch_bounds__(kRedThreads)
 sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_in, uint32_t a,
                         const fe* __restrict__ e_grp, const fe* __restrict__ pts, fe* cdev, fe* prev,
                         DevSha* t, fe* polys, fe* rs, fe* m_out, fe* d_out,
-                        const uint32_t* __restrict__ kw, fe* wfold, CoopCtl ctl) {
+                        const uint32_t* __restrict__ kw, fe* wfold, CoopCtl ctl, HostOut ho) {
   MLH_COOP_EDGE(0);
   extern __shared__ fe eq_tail_lds[];
   const uint32_t JA = a < 6 ? a : 6, JB = a - JA, QA = 1u << (a - JA);
@@ -1876,6 +1879,11 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
       v[u] = x < S0 ? fe_load(Tin + x) : fe_zero();
     }
   }
+  // wave 0 rehearses a half-block transcript round NOW, while the loads above
+  // are in flight (its inputs are not loaded yet: garbage in, result
+  // discarded -- it only brings the code into the instruction cache), instead
+  // of at the start of the rounds, where it sat before round 0
+  if (MLH_REH == 3 && (threadIdx.x >> 6) == 0) transcript_rehearsal(S, s, kwx, true);
   if (threadIdx.x < sizeof(DevSha) / 4) reinterpret_cast<uint32_t*>(&s)[threadIdx.x] = sw;
   if (threadIdx.x == 0) {
     S.coef_seq = S.r_seq = S.hbar = S.mseq = S.fail = S.ab_seq = 0;
@@ -1992,6 +2000,12 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
     }
   }
   coop_report(S, ctl);
+  if (ho.dst) {  // the prove's results straight into pinned host memory (no copy launch)
+    __syncthreads();  // every role's writes done
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(ho.src);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(ho.dst);
+    for (uint32_t i = threadIdx.x; i < ho.bytes / 4; i += blockDim.x) dst[i] = src[i];
+  }
 }
 
 // The last rounds of a device-resident sumcheck (tables of S <= kTailMax
@@ -2120,13 +2134,13 @@ hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, 
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
-                                   CoopCtl ctl, const uint32_t* kw) {
+                                   CoopCtl ctl, const uint32_t* kw, HostOut ho) {
   if (a == 0 || a > kTailLogMax || Jin > 3) return hipErrorInvalidValue;
   const uint32_t JA = a < 6 ? a : 6, S0 = 1u << a;
   const size_t lds = ((1ull << a) + (1ull << (a - JA))) * sizeof(fe);  // m + e_{JA-1}
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Tin, Jin, rs_in,
                      a, ets + (S0 - (S0 >> (JA - 1))), pts, c, prev, t, polys, rs, m_out, d_out, kw,
-                     (fe*)nullptr, ctl);
+                     (fe*)nullptr, ctl, ho);
   return hipGetLastError();
 }
 
@@ -2196,7 +2210,7 @@ hipError_t launch_sumcheck_eq_head(const fe* Y, uint32_t B, const fe* e_grp, con
   const size_t lds = ((1ull << B) + (1ull << (B - JA))) * sizeof(fe);
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Y, 0u,
                      (const fe*)nullptr, B, e_grp, pts, c, prev, t, polys, rs, (fe*)nullptr,
-                     (fe*)nullptr, kw, wfold, ctl);
+                     (fe*)nullptr, kw, wfold, ctl, HostOut{});
   return hipGetLastError();
 }
 

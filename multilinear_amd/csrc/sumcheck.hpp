@@ -66,10 +66,17 @@ hipError_t launch_sumcheck_group(const fe* partials, uint32_t nb, uint32_t J, ui
 // pending variables with rs_in (2^a entries after it), ets = eq suffix tables
 // of pts (eq_setup_kernel's Hs), c = the running eq scale; round j's
 // outputs at polys + 2j, rs + j; m_out[0] / d_out[0] = the folded tables.
+// A device region the last kernel of a prove copies into pinned host memory
+// at its end (bytes a multiple of 4; dst == nullptr: none).
+struct HostOut {
+  const uint8_t* src = nullptr;
+  uint8_t* dst = nullptr;
+  uint32_t bytes = 0;
+};
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
-                                   CoopCtl ctl, const uint32_t* kw = nullptr);
+                                   CoopCtl ctl, const uint32_t* kw = nullptr, HostOut ho = {});
 // The first B <= 12 rounds of an eq-factored sumcheck of 2^(B + a) entries in
 // one launch each for their corner sums and their rounds: Y[c] = sum_i T[c 2^a
 // + i] lo[i] (the B-variable corner sums, lo = eq of the last a points), then
