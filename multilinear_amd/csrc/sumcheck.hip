@@ -1676,8 +1676,17 @@ __device__ void corner_rounds(CoopSync& S, uint32_t JA, uint32_t JB, uint32_t u0
     }
   }
   if (!wout && !m_out && !wfold) return;
-  // the last round's variables: r of the one before it, then its own
+  // the last round's variables: r of the one before it, then its own.  All
+  // but one product per lane happen before the last challenge is out: group
+  // A's fold weights need only r_0..r_{JA-1}, and the folded entry sum_c W_c
+  // X_c is linear in the last challenge (bucket sums by its bit first).
   const uint32_t vl = vend - 1, tl = vl - u0, ul = vl >= JA ? vl - JA : vl;
+  const uint32_t Jl = vl >= JA ? JB : JA, mb = 1u << (Jl - 1 - ul);
+  fe WA = one;
+  if (wfold && JB) {
+    lds_wait_ge(S, &S.r_seq, JA - u0);
+    for (uint32_t v = 0; v < JA; ++v) WA = fe_mul_s(WA, gsel(v, lds_fe(S.rsh[v - u0])));
+  }
   fe rv = fe_zero();
   if (tl >= 1) {
     lds_wait_ge(S, &S.r_seq, tl);
@@ -1687,23 +1696,28 @@ __device__ void corner_rounds(CoopSync& S, uint32_t JA, uint32_t JB, uint32_t u0
     Xact = fe_add(Xa, fe_mul_s(rv, Xb));  // a one-variable group B: m_6 at r_5
   else if (ul >= 1 && vl - 1 >= u0)
     W = fe_mul_s(W, gsel(vl - 1, rv));    // (the loop took the variables before)
+  fe T = fe_zero();
+  if (m_out) {
+    T = c < (1u << Jl) ? fe_mul_s(W, Xact) : fe_zero();
+    for (uint32_t m = 1; m < 64; m <<= 1)
+      if (m != mb) T = fe_add(T, shfl_xor_fe(T, (int)m));
+  }
   lds_wait_ge(S, &S.r_seq, tl + 1);
-  W = fe_mul_s(W, gsel(vl, lds_fe(S.rsh[tl])));
+  const fe rl = lds_fe(S.rsh[tl]);
+  if (m_out) {  // sum over the last group's corners of W_c X_c
+    const fe T0 = bcast_fe(T, 0);
+    const fe x = fe_add(T0, fe_mul_s(rl, fe_sub(bcast_fe(T, (int)mb), T0)));
+    if (c == 0) fe_store(m_out, x);
+  }
+  if (wout || wfold) W = fe_mul_s(W, gsel(vl, rl));
   if (wout && c < (1u << JA)) fe_store(wout + c, W);
   if (wfold) {  // the fold weights of both groups: W_A at wfold[0..64), W_B at wfold[64..)
-    fe WA = W;
     if (JB) {
-      WA = one;
-      for (uint32_t v = 0; v < JA; ++v) WA = fe_mul_s(WA, gsel(v, lds_fe(S.rsh[v - u0])));
       if (c < (1u << JB)) fe_store(wfold + 64 + c, W);
+    } else {
+      WA = W;
     }
     if (c < (1u << JA)) fe_store(wfold + c, WA);
-  }
-  if (m_out) {  // sum over the last group's corners of W_c X_c
-    const uint32_t Jl = vl >= JA ? JB : JA;
-    fe x = c < (1u << Jl) ? fe_mul_s(W, Xact) : fe_zero();
-    for (int m = 32; m >= 1; m >>= 1) x = fe_add(x, shfl_xor_fe(x, m));
-    if (c == 0) fe_store(m_out, x);
   }
 }
 
@@ -1746,11 +1760,16 @@ __device__ void coef_rounds(CoopSync& S, uint32_t u0, uint32_t vend, fe* prev, f
     rv = lds_fe(S.rsh[tl - 1]);
   }
   quad_eval(S.poly[tl & 1], rv, c1v, c2v, e0v, csv);
+  // before the last challenge: scale = cs ((1 - r)(1 - p) + r p) = al + r be
+  const fe p = lds_fe(S.pg[vl]);
+  const fe al = fe_mul_s(csv, fe_sub(one, p)), be = fe_mul_s(csv, fe_sub(fe_dbl(p), one));
   lds_wait_ge(S, &S.r_seq, tl + 1);
   const fe r = lds_fe(S.rsh[tl]);
-  const fe p = lds_fe(S.pg[vl]);
-  const fe claim = pqrst(e0v, r, c1v, c2v, r);
-  const fe scale = fe_mul_s(csv, pqrst(fe_sub(one, p), r, fe_sub(fe_dbl(p), one), fe_zero(), fe_zero()));
+  // lane 1: the scale; lane 0: c1 + c2 r, then claim = e0 + r (c1 + c2 r)
+  const bool l1 = lane_is(1);
+  const fe z = fe_add(fe_if(l1, al, c1v), fe_mul_s(fe_if(l1, be, c2v), r));
+  const fe scale = bcast_fe(z, 1);
+  const fe claim = fe_add(e0v, fe_mul_s(z, r));
   if (c == 0) {
     fe_store(prev, claim);
     fe_store(cdev, scale);
