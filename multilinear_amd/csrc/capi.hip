@@ -711,6 +711,27 @@ static mlh_status fold_tables(mlh_ctx* ctx, uint32_t log_domain, const fe** tlo,
   return fold_tables_g(ctx, h_pow2_generator(log_domain), log_domain, tlo, thi);
 }
 
+// Every fold layer's twiddles of the domain of g (order 2^L) in one cached
+// table (fri.hip fold_layer_table): a pair's twiddle is one 16-B load instead
+// of a product of two table entries.  Domains up to 2^25 (512 MiB, the size of
+// the reference's own gen_pows table there); *out = nullptr above that.
+#ifndef MLH_FOLD_TABLE_MAX_LOG
+#define MLH_FOLD_TABLE_MAX_LOG 25
+#endif
+static mlh_status fold_layer_table(mlh_ctx* ctx, u128 g, uint32_t L, const fe** out) {
+  *out = nullptr;
+  if (L < 2 || L > MLH_FOLD_TABLE_MAX_LOG) return MLH_OK;
+  const TableKey key{h_inv(g), (1ull << L) - 1, 0, 2};
+  if (table_hit(ctx, key, out)) return MLH_OK;
+  fe* d = nullptr;
+  MLH_TRY(table_alloc(ctx, key, ((1ull << L) - 1) * sizeof(fe), &d));
+  const fe *tlo, *thi;  // (after the big allocation: it cannot evict these)
+  MLH_TRY(fold_tables_g(ctx, g, L, &tlo, &thi));
+  HIP_TRY(ctx, launch_fold_layer_table(d, tlo, thi, L, ctx->stream));
+  *out = d;
+  return MLH_OK;
+}
+
 mlh_status mlh_fri_fold(mlh_ctx* ctx, const void* dev_layer, uint32_t log_layer, uint32_t k,
                         uint32_t log_domain, const uint8_t r[16], void* dev_next) {
   if (!ctx || !dev_layer || !dev_next || !r) return fail(ctx, MLH_ERR_INVALID, "null argument");
@@ -902,6 +923,7 @@ struct FriDevLoop {
   mlh_ctx* ctx;
   mlh_fri_prover* p;
   const fe *tlo = nullptr, *thi = nullptr;
+  const fe* twt = nullptr;  // every fold layer's twiddles (fold_layer_table), or nullptr
   PoolBuf scratch;
   size_t off_r = 128, off_last = 0, off_flag = 0, off_broot = 0, off_fr = 0, off_roots = 0,
          off_polys = 0, off_prev = 0, off_extra = 0;
@@ -935,6 +957,7 @@ struct FriDevLoop {
       p->gp_gen = h_pow2_generator(log_code);
       p->log_gp = log_code;
     }
+    if (p->log_gp == log_code) MLH_TRY(fold_layer_table(ctx, p->gp_gen, log_code, &twt));
     MLH_TRY(fold_tables_g(ctx, p->gp_gen, p->log_gp, &tlo, &thi));
     memcpy(ctx->pinned, &tr->sha, sizeof(DevSha));
     HIP_TRY(ctx, hipMemcpyAsync(dt(), ctx->pinned, sizeof(DevSha), hipMemcpyHostToDevice,
@@ -1055,10 +1078,13 @@ struct FriDevLoop {
     nx.tree = reinterpret_cast<uint8_t*>(tree);
     p->layers.push_back(nx);
     const uint32_t t = (uint32_t)p->layers.size() - 1;
+    const uint32_t Lg = p->log_gp;  // the layer table's part for fold k (pairs of a 2^(Lg - k) layer)
+    const fe* twl = twt && log_n + k == Lg ? twt + ((1ull << Lg) - (1ull << (Lg - k))) : nullptr;
     HIP_TRY(ctx, launch_fri_fold_commit(
                      cur.values, 1ull << log_n, reinterpret_cast<fe*>(vals), nx.tree, fe{}, tlo,
                      thi, k, 1ull << p->log_gp, ctx->stream, ShardMap(), rp,
-                     RootAbsorb{dt(), challenge_next ? r(k + 1) : nullptr, root(t), poly_next}, job));
+                     RootAbsorb{dt(), challenge_next ? r(k + 1) : nullptr, root(t), poly_next}, job,
+                     twl));
     return MLH_OK;
   }
 
@@ -1851,7 +1877,7 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
                                        es.kw ? es.kw + 64 * es.B : nullptr,
                                        HostOut{reinterpret_cast<const uint8_t*>(polys), ctx->pinned,
                                                (uint32_t)(48ull * L + 16)}));
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  HIP_TRY(ctx, prove_wait(ctx));
   MLH_TRY(device_check(ctx));
   std::vector<uint8_t> host(ctx->pinned, ctx->pinned + 48ull * L + 16);
   ReplayCheck rc(ctx, tr);

@@ -163,6 +163,20 @@ inline mlh_status fail(mlh_ctx* ctx, mlh_status st, const std::string& msg) {
   return st;
 }
 
+// The one wait of a prove: poll the stream instead of blocking in
+// hipStreamSynchronize (whose wake-up after the last kernel is several
+// microseconds of a ~0.24 ms prove).  MLH_SYNC_SPIN selects it at build time.
+#ifndef MLH_SYNC_SPIN
+#define MLH_SYNC_SPIN 0
+#endif
+inline hipError_t prove_wait(mlh_ctx* ctx) {
+  if (!MLH_SYNC_SPIN) return hipStreamSynchronize(ctx->stream);
+  hipError_t e;
+  while ((e = hipStreamQuery(ctx->stream)) == hipErrorNotReady) {
+  }
+  return e;
+}
+
 // Device-side failures (MLH_ERR_DEVICE).  device_arm before a prove enqueues
 // its cooperative kernels, device_check after its final sync.
 // The clear is enqueued on ctx->stream (not a host store), so a kernel of an

@@ -26,14 +26,44 @@
 
 namespace mlh {
 
+// ASM: the products through the generated asm multiply (sc_dev.hpp fe_mul_s,
+// 72 VALU against ~85 for the C++ fe_mul): faster in the latency-bound
+// one-workgroup tail steps, slower in the streaming fold + leaves kernel
+// (measured: 39.6 -> 38.7 us and 71.2 -> 74.0 us per launch)
+#ifndef MLH_FOLD_ASM
+#define MLH_FOLD_ASM 2  // 0: C++ products everywhere, 1: asm everywhere, 2: asm in the tail steps only
+#endif
+template <bool ASM>
 __device__ __forceinline__ fe fold_one(const fe& a, const fe& b, const fe& r, const fe& tw) {
   const fe even = fe_add(a, b);
-  const fe odd = fe_mul(fe_sub(a, b), tw);
-  return fe_half(fe_add(even, fe_mul(r, odd)));
+  const fe odd = ASM ? fe_mul_s(fe_sub(a, b), tw) : fe_mul(fe_sub(a, b), tw);
+  return fe_half(fe_add(even, ASM ? fe_mul_s(r, odd) : fe_mul(r, odd)));
 }
 
+template <bool ASM = false>
 __device__ __forceinline__ fe twiddle(const fe* tlo, const fe* thi, uint64_t e) {
-  return fe_mul(tlo[e & 4095], thi[e >> 12]);
+  return ASM ? fe_mul_s(tlo[e & 4095], thi[e >> 12]) : fe_mul(tlo[e & 4095], thi[e >> 12]);
+}
+constexpr bool kFoldAsmStream = MLH_FOLD_ASM == 1, kFoldAsmTail = MLH_FOLD_ASM >= 1;
+
+__global__ void __launch_bounds__(256)
+fold_layer_table_kernel(fe* __restrict__ out, const fe* __restrict__ tlo, const fe* __restrict__ thi,
+                        uint32_t L) {
+  const uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= (1ull << L) - 1) return;
+  const uint64_t y = (1ull << L) - o;  // in [2, 2^L]: layer k has y in (2^(L-1-k), 2^(L-k)]
+  const uint32_t k = L - (64 - __builtin_clzll(y - 1));
+  const uint64_t j = o - ((1ull << L) - (1ull << (L - k)));
+  fe_store(out + o, twiddle(tlo, thi, j << k));
+}
+
+hipError_t launch_fold_layer_table(fe* out, const fe* tlo_inv, const fe* thi_inv, uint32_t L,
+                                   hipStream_t st) {
+  if (L < 2 || L > 40) return hipErrorInvalidValue;
+  const uint64_t n = (1ull << L) - 1;
+  hipLaunchKernelGGL(fold_layer_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out,
+                     tlo_inv, thi_inv, L);
+  return hipGetLastError();
 }
 
 __global__ void __launch_bounds__(256)
@@ -45,8 +75,8 @@ fri_fold_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next,
   const uint64_t h = n / 2;
   if (i >= h) return;
   const fe a = fe_load(layer + i), b = fe_load(layer + i + h);
-  const fe tw = twiddle(tlo, thi, (map.global(i) << k) & (n0 - 1));
-  fe_store(next + i, fold_one(a, b, r, tw));
+  const fe tw = twiddle<kFoldAsmStream>(tlo, thi, (map.global(i) << k) & (n0 - 1));
+  fe_store(next + i, fold_one<kFoldAsmStream>(a, b, r, tw));
 }
 
 // job.st non-null: the grid's last workgroup runs that PCS round instead
@@ -56,7 +86,7 @@ __global__ void __launch_bounds__(256)
 fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next,
                        uint8_t* __restrict__ leaves, fe r, const fe* __restrict__ tlo,
                        const fe* __restrict__ thi, uint32_t k, uint64_t n0, ShardMap map,
-                       const fe* __restrict__ rp, PcsJob job) {
+                       const fe* __restrict__ rp, PcsJob job, const fe* __restrict__ twl) {
   if (job.st && blockIdx.x == gridDim.x - 1) {
     pcs_round_body(job);
     return;
@@ -67,8 +97,16 @@ fri_fold_leaves_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict_
   if (j >= q) return;
   const fe a0 = fe_load(layer + j), b0 = fe_load(layer + j + h);
   const fe a1 = fe_load(layer + j + q), b1 = fe_load(layer + j + q + h);
-  const fe x0 = fold_one(a0, b0, r, twiddle(tlo, thi, (map.global(j) << k) & (n0 - 1)));
-  const fe x1 = fold_one(a1, b1, r, twiddle(tlo, thi, (map.global(j + q) << k) & (n0 - 1)));
+  fe tw0, tw1;
+  if (twl) {
+    tw0 = fe_load(twl + j);
+    tw1 = fe_load(twl + j + q);
+  } else {
+    tw0 = twiddle<kFoldAsmStream>(tlo, thi, (map.global(j) << k) & (n0 - 1));
+    tw1 = twiddle<kFoldAsmStream>(tlo, thi, (map.global(j + q) << k) & (n0 - 1));
+  }
+  const fe x0 = fold_one<kFoldAsmStream>(a0, b0, r, tw0);
+  const fe x1 = fold_one<kFoldAsmStream>(a1, b1, r, tw1);
   fe_store(next + j, x0);
   fe_store(next + j + q, x1);
   uint32_t m[8];
@@ -92,7 +130,8 @@ __global__ void __launch_bounds__(1024)
 fri_fold_commit_small_kernel(const fe* __restrict__ layer, uint64_t n, fe* __restrict__ next,
                              uint8_t* __restrict__ tree, fe r, const fe* __restrict__ tlo,
                              const fe* __restrict__ thi, uint32_t k, uint64_t n0, ShardMap map,
-                             const fe* __restrict__ rp, RootAbsorb ra, PcsJob job) {
+                             const fe* __restrict__ rp, RootAbsorb ra, PcsJob job,
+                             const fe* __restrict__ twl) {
   __shared__ Sha256State s[1024];
   __shared__ DevSha ts;
   __shared__ uint32_t stage[8], pw[8];
@@ -104,8 +143,11 @@ fri_fold_commit_small_kernel(const fe* __restrict__ layer, uint64_t n, fe* __res
   if (j < q) {
     const fe a0 = fe_load(layer + j), b0 = fe_load(layer + j + h);
     const fe a1 = fe_load(layer + j + q), b1 = fe_load(layer + j + q + h);
-    const fe x0 = fold_one(a0, b0, r, twiddle(tlo, thi, (map.global(j) << k) & (n0 - 1)));
-    const fe x1 = fold_one(a1, b1, r, twiddle(tlo, thi, (map.global(j + q) << k) & (n0 - 1)));
+    const fe tw0 = twl ? fe_load(twl + j) : twiddle<kFoldAsmTail>(tlo, thi, (map.global(j) << k) & (n0 - 1));
+    const fe tw1 = twl ? fe_load(twl + j + q)
+                       : twiddle<kFoldAsmTail>(tlo, thi, (map.global(j + q) << k) & (n0 - 1));
+    const fe x0 = fold_one<kFoldAsmTail>(a0, b0, r, tw0);
+    const fe x1 = fold_one<kFoldAsmTail>(a1, b1, r, tw1);
     fe_store(next + j, x0);
     fe_store(next + j + q, x1);
     uint32_t m[8];
@@ -134,7 +176,7 @@ fri_fold_commit_small_kernel(const fe* __restrict__ layer, uint64_t n, fe* __res
 hipError_t launch_fri_fold_commit(const fe* layer, uint64_t n, fe* next, uint8_t* tree, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
                                   hipStream_t st, ShardMap map, const fe* r_dev, RootAbsorb ra,
-                                  const PcsJob* job) {
+                                  const PcsJob* job, const fe* twl) {
 #ifndef MLH_FRI_SMALL_LEAVES
 #define MLH_FRI_SMALL_LEAVES 1024  // trees of at most this many leaves: one fused launch (0: off)
 #endif
@@ -147,11 +189,11 @@ hipError_t launch_fri_fold_commit(const fe* layer, uint64_t n, fe* next, uint8_t
     }
     const unsigned threads = n / 4 < 64 ? 64 : (unsigned)(n / 4);
     hipLaunchKernelGGL(fri_fold_commit_small_kernel, dim3(1), dim3(threads), 0, st, layer, n, next, tree,
-                       r, tlo_inv, thi_inv, k, n0, map, r_dev, ra, pj);
+                       r, tlo_inv, thi_inv, k, n0, map, r_dev, ra, pj, twl);
     return hipGetLastError();
   }
   hipError_t e = launch_fri_fold_leaves(layer, n, next, tree, r, tlo_inv, thi_inv, k, n0, st, map,
-                                        r_dev, job);
+                                        r_dev, job, twl);
   if (e != hipSuccess) return e;
   return launch_merkle_levels(tree, n / 4, st, ra);
 }
@@ -167,7 +209,8 @@ hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe
 
 hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t* leaves, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
-                                  hipStream_t st, ShardMap map, const fe* r_dev, const PcsJob* job) {
+                                  hipStream_t st, ShardMap map, const fe* r_dev, const PcsJob* job,
+                                  const fe* twl) {
   const uint64_t q = n / 4;
   PcsJob pj{};
   if (job) {
@@ -177,7 +220,7 @@ hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t
   }
   const unsigned blocks = (unsigned)((q + 255) / 256) + (job ? 1u : 0u);
   hipLaunchKernelGGL(fri_fold_leaves_kernel, dim3(blocks), dim3(256), 0, st, layer, n, next, leaves,
-                     r, tlo_inv, thi_inv, k, n0, map, r_dev, pj);
+                     r, tlo_inv, thi_inv, k, n0, map, r_dev, pj, twl);
   return hipGetLastError();
 }
 

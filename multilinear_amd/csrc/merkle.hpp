@@ -63,16 +63,25 @@ hipError_t launch_fri_fold(const fe* layer, uint64_t n, fe* next, fe r, const fe
 struct PcsJob;
 // job (optional): one PCS round (sumcheck.hpp PcsJob) run by an extra
 // workgroup of the same launch
+// twl (optional): this layer's twiddles, twl[j] = g^(-j 2^k) for its n/2 pairs
+// (fold_layer_table: every layer of a domain in one table), instead of the
+// product T_lo[e & 4095] * T_hi[e >> 12] per pair
 hipError_t launch_fri_fold_leaves(const fe* layer, uint64_t n, fe* next, uint8_t* leaves, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
                                   hipStream_t st, ShardMap map = ShardMap(),
-                                  const fe* r_dev = nullptr, const PcsJob* job = nullptr);
+                                  const fe* r_dev = nullptr, const PcsJob* job = nullptr,
+                                  const fe* twl = nullptr);
 // Fold and commit the next layer: its whole tree (L = n/4 leaves, 2L-1
 // digests) into `tree` (leaves hashed by the fold lanes).
 hipError_t launch_fri_fold_commit(const fe* layer, uint64_t n, fe* next, uint8_t* tree, fe r,
                                   const fe* tlo_inv, const fe* thi_inv, uint32_t k, uint64_t n0,
                                   hipStream_t st, ShardMap map = ShardMap(),
                                   const fe* r_dev = nullptr, RootAbsorb ra = RootAbsorb(),
-                                  const PcsJob* job = nullptr);
+                                  const PcsJob* job = nullptr, const fe* twl = nullptr);
+// All layers' twiddles of a domain of 2^L (L >= 2) in one table of 2^L - 1
+// entries: layer k (2^(L-1-k) pairs) at offset 2^L - 2^(L-k), entry j =
+// g^(-j 2^k) = T_lo[e & 4095] * T_hi[e >> 12], e = j 2^k.
+hipError_t launch_fold_layer_table(fe* out, const fe* tlo_inv, const fe* thi_inv, uint32_t L,
+                                   hipStream_t st);
 
 }  // namespace mlh

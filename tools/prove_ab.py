@@ -21,7 +21,7 @@ def load(path):
     return lib
 
 
-for rep in range(3):
+for rep in range(int(os.environ.get("AB_REPS", "3"))):
     for path in sys.argv[1:]:
         lib = load(path)
         h = ctypes.c_void_p()
