@@ -66,7 +66,10 @@ void mlh_context_destroy(mlh_ctx* ctx);
  * size and generator) in a bounded LRU cache: default limit 1 GiB; tables the
  * running operation uses are never evicted, so the cache may exceed a very
  * small limit by that operation's tables.  limit 0 frees every table not in
- * use at the next opportunity. */
+ * use at the next opportunity.  The largest: an FRI prove of a codeword of
+ * 2^L <= 2^25 elements caches every fold layer's twiddles in one table of
+ * 2^L - 1 entries (512 MiB at 2^25); above 2^25 the folds form them from two
+ * 4096-entry tables instead. */
 mlh_status mlh_set_table_cache_limit(mlh_ctx* ctx, uint64_t bytes);
 uint64_t mlh_table_cache_bytes(const mlh_ctx* ctx);
 /* Test/tuning hook: force the NTT radix plan of this context (count digits
