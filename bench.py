@@ -495,7 +495,7 @@ def main():
         hw.phase("headline_checks")
     # dominant kernel timing (HIP events on the launch stream, timed region)
     kernels = {}
-    labels = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in range(4)
+    labels = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(4, 10) for tw in (0, 1, 2, 3, 5)
               for z in range(3)] + ["shard_dft<%d,0>" % p for p in range(1, 5)] + ["ntt_all_to_all",
                                                                                      "ntt_fused_pre",
                                                                                      "ntt_fused_last"]

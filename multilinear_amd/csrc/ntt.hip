@@ -78,6 +78,11 @@ __device__ __forceinline__ uint64_t reverse_mid_digits(const PassGeom& g, uint64
 }
 
 // TW: 0 = two-table twiddle (TA * TB), 1 = one table (TA), 2 = none (last pass),
+// 5 = pass 0's twiddle as a progression (ta = P[k0][j] = w_S^(k0 j), k0 < 64;
+// tb = C[j] = w_S^(64 j), expanded): a thread's rows after its last register
+// phase are k0 + 64 i, so w_S^(j (k0 + 64 i)) = P[k0][j] C[j]^i -- one product
+// per step instead of TA * TB per element, no TB staging through LDS, 2 + 4
+// twiddle loads per thread instead of 8 + TB's (LOGR 7 and 8);
 // 3 = one table on pass 0 (same code as 1; its own kernel so that rocprof and
 // the kernel timer tell the first pass from the middle ones), 4 = the last
 // pass of a sharded transform (as 2, over this rank's share of the global
@@ -402,7 +407,9 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
   // the first pair's inter-pass twiddles (the asm products below keep later
   // loads from being hoisted, so each pair's are issued one pair ahead)
   auto load_ta0 = [&](const uint32_t (&pf)[EPT]) {
-    if constexpr (!LAST && MLH_DIAG_TW == 2) {
+    if constexpr (TW == 5) {
+      (void)pf;
+    } else if constexpr (!LAST && MLH_DIAG_TW == 2) {
       ta_c0 = fe{{(uint32_t)jl | 1u, 7u, 9u, 3u}};
       ta_c1 = fe{{(uint32_t)pf[1] | 1u, 5u, 9u, 3u}};
     } else if constexpr (!LAST) {
@@ -475,7 +482,32 @@ ntt_pass_kernel(const fe* in, fe* out, const fe* __restrict__ tw,
     kbase = k1 + (reverse_mid_digits(g, mid) << g.logr[0]);
     kshift = g.log_n - LOGR;
   }
-  if constexpr (!LAST) {
+  if constexpr (TW == 5) {
+    constexpr int Q3 = LOGR - 2 * LQ, NI = 1 << Q3, G = EPT / NI;
+    static_assert(LOGR > 2 * LQ && G % 2 == 0, "progression twiddle: groups in pairs");
+    // (loaded here: issued before the last register phase instead -- P alone,
+    // or P and C with 6 spilled registers -- measured no faster / 8 % slower)
+    fe tv[G];  // P[k0][j] of each group (k0 = pos[g NI]: the group's first row)
+#pragma unroll
+    for (int gq = 0; gq < G; ++gq) tv[gq] = fe_load(ta + ((uint64_t)pos[gq * NI] << g.lstride) + jrest);
+    const fe* cp = tb + 4 * jrest;
+    const fe c0 = fe_load(cp), c1 = fe_load(cp + 1), c2 = fe_load(cp + 2), c3 = fe_load(cp + 3);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      uint64_t rare;
+#pragma unroll
+      for (int gq = 0; gq < G; gq += 2) {
+        const int e0 = gq * NI + i, e1 = (gq + 1) * NI + i;
+        bfly_ff_v(x[e0], tv[gq], x[e1], tv[gq + 1], rare);
+        fe_store(dst + ((uint64_t)pos[e0] << rshift), x[e0]);
+        fe_store(dst + ((uint64_t)pos[e1] << rshift), x[e1]);
+      }
+      if (i + 1 < NI) {
+#pragma unroll
+        for (int gq = 0; gq < G; gq += 2) bfly_pp_v(tv[gq], c0, c1, c2, c3, tv[gq + 1], c0, c1, c2, c3, rare);
+      }
+    }
+  } else if constexpr (!LAST) {
     // w_S^(jrest k) = TA[k][jl] * TB[k][jh]: the 8 columns of a tile are 8
     // consecutive jl, so a wave's lanes read 8 runs of 128 B per table.  The
     // products run two elements per generated asm statement (relaxed result;
@@ -760,7 +792,7 @@ hipError_t launch_ntt_network(const fe* in, fe* out, fe* scratch, const fe* tlo,
 template <int LOGR, int EPT>
 static hipError_t launch_pass_ept(bool last, int zero_top, const fe* in, fe* out, const fe* tw,
                                   const fe* ta, const fe* tb, const PassGeom& g, uint64_t tiles,
-                                  hipStream_t st) {
+                                  hipStream_t st, bool geo = false) {
   constexpr int threads = kCols * (1 << LOGR) / EPT;
   const dim3 grid((unsigned)tiles), blk(threads);
 #define MLH_PASS(TWV, ZTV)                                                                  \
@@ -769,6 +801,14 @@ static hipError_t launch_pass_ept(bool last, int zero_top, const fe* in, fe* out
   if (last) {
     if (zero_top) return hipErrorInvalidValue;  // pass 0 is never the last pass here
     MLH_PASS(2, 0);
+  } else if (geo) {  // TW 5 (pass 0, LOGR 7 / 8; ta = P, tb = C)
+    if constexpr ((LOGR == 7 || LOGR == 8) && EPT == 8) {
+      if (zero_top == 2) MLH_PASS(5, 2);
+      else if (zero_top == 1) MLH_PASS(5, 1);
+      else MLH_PASS(5, 0);
+    } else {
+      return hipErrorInvalidValue;
+    }
   } else if (!tb && g.p == 0) {  // TW 3: as 1, a distinct kernel for the first pass
     if (zero_top == 2) MLH_PASS(3, 2);
     else if (zero_top == 1) MLH_PASS(3, 1);
@@ -791,8 +831,8 @@ static hipError_t launch_pass_ept(bool last, int zero_top, const fe* in, fe* out
 template <int LOGR>
 static hipError_t launch_pass(bool last, int zero_top, const fe* in, fe* out, const fe* tw,
                               const fe* ta, const fe* tb, const PassGeom& g, uint64_t tiles,
-                              hipStream_t st) {
-  return launch_pass_ept<LOGR, kEPT>(last, zero_top, in, out, tw, ta, tb, g, tiles, st);
+                              hipStream_t st, bool geo = false) {
+  return launch_pass_ept<LOGR, kEPT>(last, zero_top, in, out, tw, ta, tb, g, tiles, st, geo);
 }
 
 void ntt_plan_radices(uint32_t log_n, uint32_t* nradix, uint32_t* logr, const uint32_t* forced,
@@ -835,7 +875,7 @@ hipError_t launch_ntt_small(const fe* in, fe* out, const fe* tw, uint32_t log_n,
 
 void ntt_pass_label(const NttTables& tb, uint32_t p, int zero_top, char* buf, size_t n) {
   const bool last = p + 1 == tb.nradix;
-  const int tw = last ? 2 : (tb.tb[p] ? 0 : (p == 0 ? 3 : 1));
+  const int tw = last ? 2 : (tb.gp[p] ? 5 : (tb.tb[p] ? 0 : (p == 0 ? 3 : 1)));
   snprintf(buf, n, "ntt_pass<%u,%d,%d>", tb.logr[p], tw, p == 0 ? zero_top : 0);
 }
 
@@ -868,13 +908,16 @@ hipError_t launch_ntt_passes(const fe* in, fe* out, fe* scratch, const NttTables
     const int zt = p == 0 ? zero_top : 0;
     if (ev) (void)hipEventRecord(ev[p], st);
     hipError_t e;
+    const bool geo = tb.gp[p] != nullptr;  // TW 5: the progression tables instead of TA, TB
+    const fe* ta = geo ? tb.gp[p] : tb.ta[p];
+    const fe* tbb = geo ? tb.gc[p] : tb.tb[p];
     switch (lr) {
-      case 4: e = launch_pass<4>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
-      case 5: e = launch_pass<5>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
-      case 6: e = launch_pass<6>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
-      case 7: e = launch_pass<7>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
-      case 8: e = launch_pass<8>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
-      case 9: e = launch_pass<9>(last, zt, src, dst, tb.tw[p], tb.ta[p], tb.tb[p], g, tiles, st); break;
+      case 4: e = launch_pass<4>(last, zt, src, dst, tb.tw[p], ta, tbb, g, tiles, st, geo); break;
+      case 5: e = launch_pass<5>(last, zt, src, dst, tb.tw[p], ta, tbb, g, tiles, st, geo); break;
+      case 6: e = launch_pass<6>(last, zt, src, dst, tb.tw[p], ta, tbb, g, tiles, st, geo); break;
+      case 7: e = launch_pass<7>(last, zt, src, dst, tb.tw[p], ta, tbb, g, tiles, st, geo); break;
+      case 8: e = launch_pass<8>(last, zt, src, dst, tb.tw[p], ta, tbb, g, tiles, st, geo); break;
+      case 9: e = launch_pass<9>(last, zt, src, dst, tb.tw[p], ta, tbb, g, tiles, st, geo); break;
       default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;

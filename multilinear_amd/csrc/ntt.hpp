@@ -41,6 +41,11 @@ struct NttTables {
   const fe* ta[kMaxPasses] = {nullptr};
   const fe* tb[kMaxPasses] = {nullptr};
   uint32_t loga[kMaxPasses] = {0};
+  // pass 0's twiddle as a progression (ntt_pass_kernel TW 5; single-GPU
+  // launch_ntt_passes only, when set): gp = P[k0][j] = w_S^(k0 j) (x n^-1 on
+  // the inverse), k0 < 64, j < W; gc = C[j] = w_S^(64 j), expanded
+  const fe* gp[kMaxPasses] = {nullptr};
+  const fe* gc[kMaxPasses] = {nullptr};
   const fe* tw_small = nullptr;          // N <= 2^10: w^t, t < N/2
   fe scale;                              // n^-1 (inverse) or 1
   bool inverse = false;

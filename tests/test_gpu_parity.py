@@ -927,6 +927,34 @@ def _forced_plan_vs_c_oracle(plan):
     assert (D.from_device(MF.reed_solomon_brev(D.to_device(brev), g)) == want).all()
 
 
+def _bitrev_perm(bits):
+    i = np.arange(1 << bits, dtype=np.uint64)
+    r = np.zeros_like(i)
+    for b in range(bits):
+        r |= ((i >> np.uint64(b)) & np.uint64(1)) << np.uint64(bits - 1 - b)
+    return r.astype(np.int64)
+
+
+@pytest.mark.parametrize("log_n", [23, pytest.param(24, marks=pytest.mark.slow)])
+def test_default_plan_pass0_progression_vs_c_oracle(log_n):
+    """2^23 and 2^24 (default plans 8,8,7 and 8,8,8): pass 0's inter-pass
+    twiddle, too big for one table, runs as the progression P[k0][j] C[j]^i
+    (ntt_pass_kernel TW 5) in every zero-top mode -- NTT, INTT (the n^-1 scale
+    in P), RS of 2^(n-1) coefficients (implicit zero half) and RS of the
+    bit-reversed coefficients (the PCS path) -- against the C oracle."""
+    C = _c_oracle()
+    g = F.pow_2_generator(log_n)
+    x = D.random_limbs(1 << log_n, 2300 + log_n)
+    assert (D.from_device(MN.Polynomial(D.to_device(x)).ntt(g).evals) == C.ntt(x, log_n, g)).all()
+    assert (D.from_device(MN.LagrangePolynomial(g, D.to_device(x)).intt().coeffs)
+            == C.ntt(x, log_n, g, inverse=True)).all()
+    half = np.ascontiguousarray(x[: 1 << (log_n - 1)])
+    want = C.reed_solomon(half, log_n - 1, g)
+    assert (D.from_device(MF.reed_solomon(D.to_device(half), g)) == want).all()
+    brev = np.ascontiguousarray(half[_bitrev_perm(log_n - 1)])
+    assert (D.from_device(MF.reed_solomon_brev(D.to_device(brev), g)) == want).all()
+
+
 @pytest.mark.parametrize("log_n", [0, 1, 4, 9, 10, 11, 13, 17, 20])
 def test_reed_solomon_brev_vs_c_oracle(log_n):
     """Fused bit reversal (ZT == 2 pass-0 loads / small-kernel path) against

@@ -23,7 +23,7 @@ def load(path):
     return lib
 
 
-labels = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(7, 10) for tw in range(4) for z in range(3)]
+labels = ["ntt_pass<%d,%d,%d>" % (r, tw, z) for r in range(7, 10) for tw in (0, 1, 2, 3, 5) for z in range(3)]
 for rep in range(2):
     for path in sys.argv[1:]:
         lib = load(path)
