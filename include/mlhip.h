@@ -69,7 +69,8 @@ void mlh_context_destroy(mlh_ctx* ctx);
  * use at the next opportunity.  The largest: an FRI prove of a codeword of
  * 2^L <= 2^25 elements caches every fold layer's twiddles in one table of
  * 2^L - 1 entries (512 MiB at 2^25); above 2^25 the folds form them from two
- * 4096-entry tables instead. */
+ * 4096-entry tables instead.  A 2^23 or 2^24 NTT's first pass adds a 64 x 2^16
+ * progression table and its 2^16-entry step table (68 MiB at 2^24). */
 mlh_status mlh_set_table_cache_limit(mlh_ctx* ctx, uint64_t bytes);
 uint64_t mlh_table_cache_bytes(const mlh_ctx* ctx);
 /* Test/tuning hook: force the NTT radix plan of this context (count digits
