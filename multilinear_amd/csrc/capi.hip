@@ -127,6 +127,9 @@ static uint64_t hi_count(uint32_t log_n) {
 #ifndef MLH_P0_GEO
 #define MLH_P0_GEO 1  // 0: pass 0 always multiplies TA * TB
 #endif
+#ifndef MLH_P0_GEO_MAXLOGW
+#define MLH_P0_GEO_MAXLOGW 16  // largest W (columns) of the progression table: 64 W entries
+#endif
 static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool inverse,
                                  NttTables* tb, const uint32_t* plan = nullptr, uint32_t nplan = 0) {
   const uint64_t N = 1ull << log_n;
@@ -162,7 +165,8 @@ static mlh_status get_ntt_tables(mlh_ctx* ctx, u128 gen, uint32_t log_n, bool in
       MLH_TRY(get_table2d(ctx, ws, R, 1ull << (logw - loga), 1ull << loga, 1, &tb->tb[p], true));
     // pass 0 with two tables, R = 2^7 / 2^8, W <= 2^16: the progression form
     // (64 W + 4 W entries: 68 MiB at 2^24)
-    if (MLH_P0_GEO && p == 0 && logw > loga && (tb->logr[0] == 7 || tb->logr[0] == 8) && logw <= 16) {
+    if (MLH_P0_GEO && p == 0 && logw > loga && (tb->logr[0] == 7 || tb->logr[0] == 8) &&
+        logw <= MLH_P0_GEO_MAXLOGW) {
       MLH_TRY(get_table2d(ctx, ws, 64, 1ull << logw, 1, scale, &tb->gp[0]));
       MLH_TRY(get_table(ctx, h_pow(ws, 64), 1ull << logw, 1, &tb->gc[0], true));
     }
