@@ -853,7 +853,9 @@ hipError_t launch_group_sums_eq(const fe* T, uint64_t S, uint32_t J, const fe* H
 hipError_t launch_fold_group_eq(const fe* Tin, uint64_t S, uint32_t J, uint32_t JN, const fe* rs,
                                 const fe* w, fe* Tout, const fe* H, const fe* lo, uint32_t a,
                                 fe* partials, hipStream_t st, uint32_t* nb) {
-  if (J < 1 || J > kMaxGroup || JN > kMaxGroup || a < 8 || (S >> (J + JN)) < (1ull << a) || !w)
+  // (a < 8 only in the tail form: 2^a outputs per corner, e = lo, H = [1])
+  if (J < 1 || J > kMaxGroup || JN > kMaxGroup || (S >> (J + JN)) < (1ull << a) || !w ||
+      (a < 8 && !(JN && (S >> (J + JN)) == (1ull << a))))
     return hipErrorInvalidValue;
 #ifndef MLH_FOLD_SPLIT
 #define MLH_FOLD_SPLIT (1u << 16)  // outputs below which a J > 3 fold splits across lanes
@@ -1865,7 +1867,8 @@ __global__ void __launch_bounds__(kRedThreads)
 sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_in, uint32_t a,
                         const fe* __restrict__ e_grp, const fe* __restrict__ pts, fe* cdev, fe* prev,
                         DevSha* t, fe* polys, fe* rs, fe* m_out, fe* d_out,
-                        const uint32_t* __restrict__ kw, fe* wfold, CoopCtl ctl, HostOut ho) {
+                        const uint32_t* __restrict__ kw, fe* wfold, CoopCtl ctl, HostOut ho,
+                        const fe* __restrict__ xc_part, uint32_t xc_nb) {
   MLH_COOP_EDGE(0);
   extern __shared__ fe eq_tail_lds[];
   const uint32_t JA = a < 6 ? a : 6, JB = a - JA, QA = 1u << (a - JA);
@@ -1898,6 +1901,14 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
       v[u] = x < S0 ? fe_load(Tin + x) : fe_zero();
     }
   }
+  // xc_part (optional, the tail launch): group A's corner sums as xc_nb (a
+  // few) partials per corner, written by the fold that produced Tin
+  // (fold_group_eq_kernel's JN path with e = e_grp): the corner-sum phase
+  // below is skipped.  (The head's terms -- 64 per corner from the corner-sum
+  // pass -- summed here measured slower than that phase.)
+  fe xcv = fe_zero();
+  if (xc_part && threadIdx.x < (1u << JA))
+    for (uint32_t bb = 0; bb < xc_nb; ++bb) xcv = fe_add(xcv, fe_load(xc_part + threadIdx.x * xc_nb + bb));
   // wave 0 rehearses a half-block transcript round NOW, while the loads above
   // are in flight (its inputs are not loaded yet: garbage in, result
   // discarded -- it only brings the code into the instruction cache), instead
@@ -1934,10 +1945,11 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
     for (uint32_t u = 0; u < 3; ++u) rin[u] = u < Jin ? fe_load(rs_in + u) : fe_zero();
     for (uint32_t x = threadIdx.x; x < S0; x += blockDim.x) lm[x] = fold_corners_n(Jin, Tin + x, S0, rin);
   }
+  if (xc_part && threadIdx.x < (1u << JA)) S.xc[threadIdx.x] = xcv;
   __syncthreads();
   MLH_COOP_TS(9, 11);
   // group A's corner sums: 2^JA corners x QA entries, G = 256 / 2^JA threads per corner
-  {
+  if (!xc_part) {
     const uint32_t G = kRedThreads >> JA, c = threadIdx.x / G, j = threadIdx.x % G;
     const fe* e = le;  // e_{JA-1}: QA entries
     sacc q;
@@ -1950,15 +1962,15 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
     } else {  // G = 128 or 256 (JA <= 1): 2 or 4 waves per corner
       if (lane == 0) S.red[wave][0] = x;
     }
+    __syncthreads();
+    if ((kRedThreads >> JA) > 64 && threadIdx.x < (1u << JA)) {
+      const uint32_t per = (kRedThreads >> JA) / 64;
+      fe y = fe_zero();
+      for (uint32_t w = 0; w < per; ++w) y = fe_add(y, S.red[threadIdx.x * per + w][0]);
+      S.xc[threadIdx.x] = y;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if ((kRedThreads >> JA) > 64 && threadIdx.x < (1u << JA)) {
-    const uint32_t per = (kRedThreads >> JA) / 64;
-    fe x = fe_zero();
-    for (uint32_t w = 0; w < per; ++w) x = fe_add(x, S.red[threadIdx.x * per + w][0]);
-    S.xc[threadIdx.x] = x;
-  }
-  __syncthreads();
   MLH_COOP_EDGE(1);
 #ifdef MLH_COOP_PROF
   if (lane == 0) g_coop_ts[9][20 + wave] = __builtin_amdgcn_s_getreg(4 | (31 << 11));  // HW_ID: SIMD in bits 5:4
@@ -2153,13 +2165,15 @@ hipError_t launch_sumcheck_round(const fe* partials, uint32_t nparts, fe* prev, 
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
-                                   CoopCtl ctl, const uint32_t* kw, HostOut ho) {
-  if (a == 0 || a > kTailLogMax || Jin > 3) return hipErrorInvalidValue;
+                                   CoopCtl ctl, const uint32_t* kw, HostOut ho, const fe* xc_part,
+                                   uint32_t xc_nb) {
+  if (a == 0 || a > kTailLogMax || Jin > 3 || (xc_part && (Jin || a < 6 || xc_nb == 0)))
+    return hipErrorInvalidValue;
   const uint32_t JA = a < 6 ? a : 6, S0 = 1u << a;
   const size_t lds = ((1ull << a) + (1ull << (a - JA))) * sizeof(fe);  // m + e_{JA-1}
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Tin, Jin, rs_in,
                      a, ets + (S0 - (S0 >> (JA - 1))), pts, c, prev, t, polys, rs, m_out, d_out, kw,
-                     (fe*)nullptr, ctl, ho);
+                     (fe*)nullptr, ctl, ho, xc_part, xc_nb);
   return hipGetLastError();
 }
 
@@ -2229,7 +2243,7 @@ hipError_t launch_sumcheck_eq_head(const fe* Y, uint32_t B, const fe* e_grp, con
   const size_t lds = ((1ull << B) + (1ull << (B - JA))) * sizeof(fe);
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Y, 0u,
                      (const fe*)nullptr, B, e_grp, pts, c, prev, t, polys, rs, (fe*)nullptr,
-                     (fe*)nullptr, kw, wfold, ctl, HostOut{});
+                     (fe*)nullptr, kw, wfold, ctl, HostOut{}, (const fe*)nullptr, 0u);
   return hipGetLastError();
 }
 

@@ -73,10 +73,13 @@ struct HostOut {
   uint8_t* dst = nullptr;
   uint32_t bytes = 0;
 };
+// xc_part (a >= 6, Jin = 0, optional): group A's corner sums sum_i Tin[c 2^(a-6) + i] e_{5}[i]
+// as xc_nb partials per corner (c xc_nb + b), from the fold that wrote Tin.
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
-                                   CoopCtl ctl, const uint32_t* kw = nullptr, HostOut ho = {});
+                                   CoopCtl ctl, const uint32_t* kw = nullptr, HostOut ho = {},
+                                   const fe* xc_part = nullptr, uint32_t xc_nb = 0);
 // The first B <= 12 rounds of an eq-factored sumcheck of 2^(B + a) entries in
 // one launch each for their corner sums and their rounds: Y[c] = sum_i T[c 2^a
 // + i] lo[i] (the B-variable corner sums, lo = eq of the last a points), then
