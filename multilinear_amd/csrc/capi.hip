@@ -1712,6 +1712,9 @@ static mlh_status sumcheck_fold_dr(mlh_ctx* ctx, fe* m, fe* d, uint64_t S, const
 #ifndef MLH_TAIL_XC
 #define MLH_TAIL_XC 1  // 0: the tail launch sums its group-A corners itself
 #endif
+#ifndef MLH_TAIL_RSUF
+#define MLH_TAIL_RSUF 1  // 0: the tail launch computes its suffix products itself
+#endif
 struct EqSumcheck {
   static constexpr uint32_t kEqLo = 12;  // = sumcheck_tail_rounds' LDS limit
   mlh_ctx* ctx;
@@ -1725,6 +1728,7 @@ struct EqSumcheck {
   fe* wts = nullptr;       // eq weights of the last finished group's challenges (its fold)
   uint32_t tail_xc_nb = 0; // head_rounds: the tail's group-A corner sums are in ctx->partials
   bool tail_tables = false; // Hs filled (init's want_tail)
+  fe* rsuf = nullptr;       // the tail's suffix products (want_tail; eq_setup_kernel)
   explicit EqSumcheck(mlh_ctx* c_) : ctx(c_), buf(c_) {}
 
   // matrix: round 0's table; work (2^(L-1) entries, optional) receives the
@@ -1741,8 +1745,8 @@ struct EqSumcheck {
     tail_tables = want_tail;
     a = L < kEqLo ? L : kEqLo;
     B = L - a;
-    // c | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1] | pts[L] | kw[64 L words] | wts[64]
-    MLH_TRY(buf.alloc(16 * (1 + 3 * (1ull << a) + (1ull << B) + L + 16ull * L + 64)));
+    // c | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1] | pts[L] | kw[64 L words] | wts[64] | rsuf
+    MLH_TRY(buf.alloc(16 * (1 + 3 * (1ull << a) + (1ull << B) + L + 16ull * L + 64 + kEqTailRsuf)));
     c = buf.as<fe>();
     lo = c + 1;
     d = B ? lo + (1ull << a) : lo;  // B == 0: delta is the whole eq table
@@ -1751,6 +1755,7 @@ struct EqSumcheck {
     pts = Hs + (1ull << a);
     kw = sha ? reinterpret_cast<uint32_t*>(pts + L) : nullptr;
     wts = pts + L + 16ull * L;
+    rsuf = MLH_TAIL_RSUF && want_tail ? wts + 64 : nullptr;
     EqSetupArgs args{};
     if (L) memcpy(args.pts, host_points, 16ull * L);
     if (sha) memcpy(&args.sha, sha, sizeof(DevSha));
@@ -1758,7 +1763,7 @@ struct EqSumcheck {
     args.L = L;
     args.B = B;
     HIP_TRY(ctx, launch_eq_setup(args, pts, c, lo, H, want_tail ? Hs : nullptr, dt_out, prev_out,
-                                 ctx->stream, kw));
+                                 ctx->stream, kw, rsuf));
     return MLH_OK;
   }
   const fe* Hk(uint32_t k) const { return H + ((1ull << B) - (1ull << (B - k))); }
@@ -1905,7 +1910,8 @@ mlh_status mlh_sumcheck_prove_eq(mlh_ctx* ctx, const void* dev_evals, void* dev_
                                        es.kw ? es.kw + 64 * es.B : nullptr,
                                        HostOut{reinterpret_cast<const uint8_t*>(polys), ctx->pinned,
                                                (uint32_t)(48ull * L + 16)},
-                                       es.tail_xc_nb ? ctx->partials : nullptr, es.tail_xc_nb));
+                                       es.tail_xc_nb ? ctx->partials : nullptr, es.tail_xc_nb,
+                                       es.rsuf));
   HIP_TRY(ctx, prove_wait(ctx));
   MLH_TRY(device_check(ctx));
   std::vector<uint8_t> host(ctx->pinned, ctx->pinned + 48ull * L + 16);

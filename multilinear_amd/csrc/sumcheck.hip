@@ -762,26 +762,60 @@ hipError_t launch_fold(fe* m, fe* d, uint64_t S, fe r, hipStream_t st, const fe*
 // H (2^B - 1, as eq_suffix_kernel over p_0..p_{B-1}), the tail suffix tables
 // Hs (2^a - 1, over p_B..p_{L-1}; optional); thread 0 also writes the points,
 // c_0 = 1 and (optional) the transcript state and the claim.
+#ifndef MLH_SETUP_TREE
+#define MLH_SETUP_TREE 1
+#endif
+#ifndef MLH_TAIL_DMA
+#define MLH_TAIL_DMA 1  // sumcheck_eq_tail_kernel: wave 3 copies the table by LDS-DMA (xc_part launches)
+#endif
 __global__ void __launch_bounds__(256)
 eq_setup_kernel(const EqSetupArgs args, fe* __restrict__ pts_out, fe* __restrict__ c_out,
                 fe* __restrict__ lo, fe* __restrict__ H, fe* __restrict__ Hs, DevSha* dt_out,
-                fe* prev_out, uint32_t* __restrict__ kw) {
+                fe* prev_out, uint32_t* __restrict__ kw, fe* __restrict__ rsuf) {
   const uint32_t L = args.L, B = args.B, a = L - B;
   const uint64_t NL = 1ull << a, NH = (1ull << B) - 1, NS = Hs ? NL - 1 : 0;
   uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // kw: per round k whose absorb of (c1, c2) empties the buffer, the padding
-  // block's K + W table (the transcript then grows 32 bytes per round)
-  if (kw && x >= NL + NH + NS && x < NL + NH + NS + L) {
-    const uint32_t k = (uint32_t)(x - (NL + NH + NS));
-    const uint64_t len = args.sha.len + 32ull * (k + 1);
-    if ((len & 63) == 0) sha256_pad_kw(len, kw + 64 * k);
+  // after the tables, from a wave boundary (so no table wave also runs these
+  // paths): one wave of copies -- lane i < L point i, lane 40 c_0, lane 41 the
+  // claim, lanes 48.. the transcript state's words -- then kw: per round k
+  // whose absorb of (c1, c2) empties the buffer, the padding block's K + W
+  // table (the transcript then grows 32 bytes per round)
+  const uint64_t NT = (NL + NH + NS + 63) & ~63ull;
+  if (x >= NT) {
+    const uint32_t y = (uint32_t)(x - NT);
+    if (y < 64) {
+      if (y < L) pts_out[y] = args.pts[y];
+      if (y == 40) *c_out = fe_one();
+      if (y == 41 && prev_out) *prev_out = args.sum;
+      constexpr uint32_t SW = sizeof(DevSha) / 8;
+      static_assert(sizeof(DevSha) % 8 == 0 && SW <= 16, "DevSha copy");
+      if (dt_out && y >= 48 && y < 48 + SW)
+        reinterpret_cast<uint2*>(dt_out)[y - 48] = reinterpret_cast<const uint2*>(&args.sha)[y - 48];
+    } else if (y < 128) {
+      if (kw && y - 64 < L) {
+        const uint32_t k = y - 64;
+        const uint64_t len = args.sha.len + 32ull * (k + 1);
+        if ((len & 63) == 0) sha256_pad_kw(len, kw + 64 * k);
+      }
+    } else if (rsuf && y - 128 < kEqTailRsuf) {
+      // the eq tail's suffix products (its prologue's suffix_products, moved
+      // off the tail launch's critical path): group g = 0 over p_B..
+      // p_{B+JA-1}, g = 1 over the next JB points; rs[u][c] = prod_{u<v<J}
+      // (bit J-1-v of c ? p_v : 1 - p_v)
+      const uint32_t z = y - 128, g = z / 384, u = (z % 384) / 64, c = z % 64;
+      const uint32_t JA = a < 6 ? a : 6, J = g ? a - JA : JA;
+      if (u < J) {
+        const fe* pv = args.pts + B + (g ? JA : 0);
+        const fe one = fe_one();
+        fe acc = one;
+        for (uint32_t v = J - 1; v > u; --v) {
+          const fe p = fe_vgpr(pv[v]);
+          acc = fe_mul_s(acc, ((c >> (J - 1 - v)) & 1u) ? p : fe_sub(one, p));
+        }
+        fe_store(rsuf + z, acc);
+      }
+    }
     return;
-  }
-  if (x == 0) {
-    for (uint32_t i = 0; i < L; ++i) pts_out[i] = args.pts[i];
-    *c_out = fe_one();
-    if (dt_out) *dt_out = args.sha;
-    if (prev_out) *prev_out = args.sum;
   }
   // entry j of an eq suffix family over points q[0..n): the table of index k
   // (2^(n-1-k) entries at offset 2^n - 2^(n-k)) = prod_{i < n-1-k} (bit_i(j) ?
@@ -805,22 +839,49 @@ eq_setup_kernel(const EqSetupArgs args, fe* __restrict__ pts_out, fe* __restrict
   }
   // (the chain of products is the launch's critical path, one thread per
   // entry: the generated asm multiply, operands in VGPRs)
+#if MLH_SETUP_TREE
+  // the first 12 factors as a product tree (depth 4 instead of a chain of up
+  // to 12: one wave per SIMD here, so the products' latency is the launch's
+  // time), the rest (cnt > 12: heads of more than 13 variables) chained on
+  const fe one = fe_one();
+  fe f[12];
+#pragma unroll
+  for (uint32_t i = 0; i < 12; ++i) {
+    f[i] = one;
+    if (i < cnt) {
+      const fe p = fe_vgpr(q[n - 1 - i]);
+      f[i] = ((j >> i) & 1) ? p : fe_sub(one, p);
+    }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < 6; ++i) f[i] = fe_mul_s(f[2 * i], f[2 * i + 1]);
+#pragma unroll
+  for (uint32_t i = 0; i < 3; ++i) f[i] = fe_mul_s(f[2 * i], f[2 * i + 1]);
+  fe acc = fe_mul_s(fe_mul_s(f[0], f[1]), f[2]);
+  for (uint32_t i = 12; i < cnt; ++i) {
+    const fe p = fe_vgpr(q[n - 1 - i]);
+    acc = fe_mul_s(acc, ((j >> i) & 1) ? p : fe_sub(one, p));
+  }
+#else
   fe acc = fe_one();
   for (uint32_t i = 0; i < cnt; ++i) {
     const fe p = fe_vgpr(q[n - 1 - i]);
     acc = fe_mul_s(acc, ((j >> i) & 1) ? p : fe_sub(fe_one(), p));
   }
+#endif
   fe_store(out, acc);
 }
 
 hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* lo, fe* H, fe* Hs,
-                           DevSha* dt_out, fe* prev_out, hipStream_t st, uint32_t* kw) {
+                           DevSha* dt_out, fe* prev_out, hipStream_t st, uint32_t* kw,
+                           fe* rsuf_out) {
   if (args.L == 0 || args.L > 40 || args.B > args.L || args.L - args.B > kTailLogMax)
     return hipErrorInvalidValue;
   const uint64_t NL = 1ull << (args.L - args.B);
-  const uint64_t total = NL + (1ull << args.B) - 1 + (Hs ? NL - 1 : 0) + (kw ? args.L : 0);
+  const uint64_t total = ((NL + (1ull << args.B) - 1 + (Hs ? NL - 1 : 0) + 63) & ~63ull) + 128 +
+                         (rsuf_out ? kEqTailRsuf : 0);
   hipLaunchKernelGGL(eq_setup_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, args,
-                     pts_out, c_out, lo, H, Hs, dt_out, prev_out, kw);
+                     pts_out, c_out, lo, H, Hs, dt_out, prev_out, kw, rsuf_out);
   return hipGetLastError();
 }
 
@@ -1868,10 +1929,15 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
                         const fe* __restrict__ e_grp, const fe* __restrict__ pts, fe* cdev, fe* prev,
                         DevSha* t, fe* polys, fe* rs, fe* m_out, fe* d_out,
                         const uint32_t* __restrict__ kw, fe* wfold, CoopCtl ctl, HostOut ho,
-                        const fe* __restrict__ xc_part, uint32_t xc_nb) {
+                        const fe* __restrict__ xc_part, uint32_t xc_nb, const fe* __restrict__ rsuf) {
   MLH_COOP_EDGE(0);
   extern __shared__ fe eq_tail_lds[];
   const uint32_t JA = a < 6 ? a : 6, JB = a - JA, QA = 1u << (a - JA);
+  // tdma: with the corner sums from xc_part, the table is read only by wave
+  // 3's fold levels (and, after them, the corner wave's group B): wave 3
+  // copies it HBM -> LDS itself (LDS-DMA, no registers) once the roles start,
+  // so the prologue waits for neither the table nor e
+  const bool tdma = MLH_TAIL_DMA && xc_part && JB && Jin == 0;
   fe claim0 = fe_zero(), cs0 = fe_zero();
   if ((threadIdx.x >> 6) == 1) {  // the coefficient wave's inputs, early
     claim0 = fe_load(prev);
@@ -1894,7 +1960,7 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
   const PadKw pkw = pad_kw_load(kw, 64 * a);
   constexpr uint32_t PER = (1u << kTailLogMax) / kRedThreads;
   fe v[PER];
-  if (Jin == 0) {
+  if (Jin == 0 && !tdma) {
 #pragma unroll
     for (uint32_t u = 0; u < PER; ++u) {
       const uint32_t x = u * kRedThreads + threadIdx.x;
@@ -1923,17 +1989,33 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
   if (threadIdx.x < a) S.pg[threadIdx.x] = pgv;
   pad_kw_store(pkw, kwl);
   if (Jin == 0) {
-    // plain copies: the groups' suffix products (their points' loads too),
-    // then the LDS stores
-    const fe ev = threadIdx.x < QA ? fe_load(e_grp + threadIdx.x) : fe_zero();
-    if (wave == 2) suffix_products(JA, pts, S.rsuf);
-    if (wave == 3 && JB) suffix_products(JB, pts + JA, S.rsufB);
+    // plain copies: the groups' suffix products (their points' loads too, or
+    // the precomputed products), then the LDS stores
+    const fe ev = !xc_part && threadIdx.x < QA ? fe_load(e_grp + threadIdx.x) : fe_zero();
+    if (rsuf) {
+      const uint32_t J = wave == 2 ? JA : JB;
+      if (wave == 2 || wave == 3) {
+        fe (*dst)[64] = wave == 2 ? S.rsuf : S.rsufB;
+        fe t[6];
 #pragma unroll
-    for (uint32_t u = 0; u < PER; ++u) {
-      const uint32_t x = u * kRedThreads + threadIdx.x;
-      if (x < S0) lm[x] = v[u];
+        for (uint32_t u = 0; u < 6; ++u)
+          if (u < J) t[u] = fe_load(rsuf + (wave - 2) * 384 + u * 64 + lane);
+#pragma unroll
+        for (uint32_t u = 0; u < 6; ++u)
+          if (u < J) dst[u][lane] = t[u];
+      }
+    } else {
+      if (wave == 2) suffix_products(JA, pts, S.rsuf);
+      if (wave == 3 && JB) suffix_products(JB, pts + JA, S.rsufB);
     }
-    if (threadIdx.x < QA) le[threadIdx.x] = ev;
+    if (!tdma) {
+#pragma unroll
+      for (uint32_t u = 0; u < PER; ++u) {
+        const uint32_t x = u * kRedThreads + threadIdx.x;
+        if (x < S0) lm[x] = v[u];
+      }
+    }
+    if (!xc_part && threadIdx.x < QA) le[threadIdx.x] = ev;
     MLH_COOP_TS(9, 10);
   } else {
     // the groups' suffix products (from the points in HBM) while the tables load
@@ -1989,9 +2071,16 @@ sumcheck_eq_tail_kernel(const fe* Tin, uint32_t Jin, const fe* __restrict__ rs_i
     // fold m in place over variables 0, 1, 2 as r_0, r_1, r_2 come out, so
     // that lm[d QA + x] (d: the bits of variables 3, 4, 5) is group B's split
     // table well before the corner wave's round-6 transition needs it.
+    if (tdma) {  // the table, HBM -> LDS (1 KiB per instruction; waited for below)
+      for (uint32_t i = 0; i < S0; i += 64)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(Tin + i + lane),
+                                         (__attribute__((address_space(3))) void*)(lm + i),
+                                         16, 0, 0);
+    }
     if (MLH_REH == 1) transcript_rehearsal(S, s, kwx, true);
     if (MLH_REH != 0) transcript_rehearsal(S, s, kwx, false);
     MLH_COOP_TS(9, 1);
+    if (tdma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (JB) {
       uint32_t n = 1u << a;
       for (uint32_t u = 0; u < 3; ++u) {
@@ -2166,14 +2255,15 @@ hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
                                    CoopCtl ctl, const uint32_t* kw, HostOut ho, const fe* xc_part,
-                                   uint32_t xc_nb) {
-  if (a == 0 || a > kTailLogMax || Jin > 3 || (xc_part && (Jin || a < 6 || xc_nb == 0)))
+                                   uint32_t xc_nb, const fe* rsuf) {
+  if (a == 0 || a > kTailLogMax || Jin > 3 || (xc_part && (Jin || a < 6 || xc_nb == 0)) ||
+      (rsuf && Jin))
     return hipErrorInvalidValue;
   const uint32_t JA = a < 6 ? a : 6, S0 = 1u << a;
   const size_t lds = ((1ull << a) + (1ull << (a - JA))) * sizeof(fe);  // m + e_{JA-1}
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Tin, Jin, rs_in,
                      a, ets + (S0 - (S0 >> (JA - 1))), pts, c, prev, t, polys, rs, m_out, d_out, kw,
-                     (fe*)nullptr, ctl, ho, xc_part, xc_nb);
+                     (fe*)nullptr, ctl, ho, xc_part, xc_nb, rsuf);
   return hipGetLastError();
 }
 
@@ -2243,7 +2333,7 @@ hipError_t launch_sumcheck_eq_head(const fe* Y, uint32_t B, const fe* e_grp, con
   const size_t lds = ((1ull << B) + (1ull << (B - JA))) * sizeof(fe);
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Y, 0u,
                      (const fe*)nullptr, B, e_grp, pts, c, prev, t, polys, rs, (fe*)nullptr,
-                     (fe*)nullptr, kw, wfold, ctl, HostOut{}, (const fe*)nullptr, 0u);
+                     (fe*)nullptr, kw, wfold, ctl, HostOut{}, (const fe*)nullptr, 0u, (const fe*)nullptr);
   return hipGetLastError();
 }
 

@@ -75,11 +75,14 @@ struct HostOut {
 };
 // xc_part (a >= 6, Jin = 0, optional): group A's corner sums sum_i Tin[c 2^(a-6) + i] e_{5}[i]
 // as xc_nb partials per corner (c xc_nb + b), from the fold that wrote Tin.
+// rsuf (Jin = 0, optional): the two groups' suffix products of pts as
+// eq_setup_kernel writes them (rsuf_out) instead of computed in the prologue.
 hipError_t launch_sumcheck_eq_tail(const fe* Tin, uint32_t Jin, const fe* rs_in, uint32_t a,
                                    const fe* ets, const fe* pts, fe* c, fe* prev, DevSha* t,
                                    fe* polys, fe* rs, fe* m_out, fe* d_out, hipStream_t st,
                                    CoopCtl ctl, const uint32_t* kw = nullptr, HostOut ho = {},
-                                   const fe* xc_part = nullptr, uint32_t xc_nb = 0);
+                                   const fe* xc_part = nullptr, uint32_t xc_nb = 0,
+                                   const fe* rsuf = nullptr);
 // The first B <= 12 rounds of an eq-factored sumcheck of 2^(B + a) entries in
 // one launch each for their corner sums and their rounds: Y[c] = sum_i T[c 2^a
 // + i] lo[i] (the B-variable corner sums, lo = eq of the last a points), then
@@ -103,9 +106,13 @@ struct EqSetupArgs {
 };
 // kw (optional, 64 L words): per round k whose (c1, c2) absorb leaves the
 // transcript buffer empty (len + 32 (k + 1) = 0 mod 64), the padding block's
-// K + W table at kw + 64 k.
+// K + W table at kw + 64 k.  rsuf_out (optional, kEqTailRsuf entries): the eq
+// tail's two corner groups' suffix products over p_B.. (group g, variable u,
+// corner c at g 384 + u 64 + c; sumcheck_eq_tail_kernel's S.rsuf / S.rsufB).
+constexpr uint32_t kEqTailRsuf = 2 * 6 * 64;
 hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* lo, fe* H, fe* Hs,
-                           DevSha* dt_out, fe* prev_out, hipStream_t st, uint32_t* kw = nullptr);
+                           DevSha* dt_out, fe* prev_out, hipStream_t st, uint32_t* kw = nullptr,
+                           fe* rsuf_out = nullptr);
 // PCS rounds (sumcheck.hip "PCS rounds off the transcript kernel"): the
 // running claim, eq scale and last polynomial (e0, c1, c2) in HBM.
 struct PcsRoundState {
