@@ -1745,8 +1745,9 @@ struct EqSumcheck {
     tail_tables = want_tail;
     a = L < kEqLo ? L : kEqLo;
     B = L - a;
-    // c | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1] | pts[L] | kw[64 L words] | wts[64] | rsuf
-    MLH_TRY(buf.alloc(16 * (1 + 3 * (1ull << a) + (1ull << B) + L + 16ull * L + 64 + kEqTailRsuf)));
+    // c | lo[2^a] | d[2^a] | H[2^B - 1] | Hs[2^a - 1] | pts[L] | kw[64 L words] | wts[64] |
+    // rsuf[2 kEqTailRsuf] (tail, head)
+    MLH_TRY(buf.alloc(16 * (1 + 3 * (1ull << a) + (1ull << B) + L + 16ull * L + 64 + 2 * kEqTailRsuf)));
     c = buf.as<fe>();
     lo = c + 1;
     d = B ? lo + (1ull << a) : lo;  // B == 0: delta is the whole eq table
@@ -1818,7 +1819,8 @@ struct EqSumcheck {
       const uint32_t JA = B < 6 ? B : 6, JB = B - JA;
       HIP_TRY(ctx, launch_corner_sums_lo(src, B, a, lo, Y, ctx->stream));
       HIP_TRY(ctx, launch_sumcheck_eq_head(Y, B, Hk(JA - 1), pts, c, prev, dt, polys, rs, wf,
-                                           ctx->stream, coop_ctl(ctx), kw));
+                                           ctx->stream, coop_ctl(ctx), kw,
+                                           rsuf ? rsuf + kEqTailRsuf : nullptr));
       // the last fold also sums the tail's group-A corners (JN = 6 over its
       // 2^12 outputs, e = Hs_5, H = H_{B-1} = [1]): the tail launch then skips
       // that phase of its prologue (tail_xc_nb partials per corner in

@@ -797,22 +797,26 @@ eq_setup_kernel(const EqSetupArgs args, fe* __restrict__ pts_out, fe* __restrict
         const uint64_t len = args.sha.len + 32ull * (k + 1);
         if ((len & 63) == 0) sha256_pad_kw(len, kw + 64 * k);
       }
-    } else if (rsuf && y - 128 < kEqTailRsuf) {
-      // the eq tail's suffix products (its prologue's suffix_products, moved
-      // off the tail launch's critical path): group g = 0 over p_B..
-      // p_{B+JA-1}, g = 1 over the next JB points; rs[u][c] = prod_{u<v<J}
-      // (bit J-1-v of c ? p_v : 1 - p_v)
-      const uint32_t z = y - 128, g = z / 384, u = (z % 384) / 64, c = z % 64;
-      const uint32_t JA = a < 6 ? a : 6, J = g ? a - JA : JA;
+    } else if (rsuf && y - 128 < 2 * kEqTailRsuf) {
+      // the suffix products of the eq tail's (h = 0: points p_B..) and the
+      // eq head's (h = 1: p_0..p_{B-1}, when B <= 12) corner groups, moved
+      // off those launches' critical paths (their prologue's
+      // suffix_products): group g = 0 over the first JA = min(n, 6) points,
+      // g = 1 over the next n - JA; rs[u][c] = prod_{u<v<J} (bit J-1-v of c
+      // ? p_v : 1 - p_v)
+      const uint32_t h = (y - 128) / kEqTailRsuf, z = (y - 128) % kEqTailRsuf;
+      const uint32_t g = z / 384, u = (z % 384) / 64, c = z % 64;
+      const uint32_t n = h ? (B <= 12 ? B : 0) : a;
+      const uint32_t JA = n < 6 ? n : 6, J = g ? n - JA : JA;
       if (u < J) {
-        const fe* pv = args.pts + B + (g ? JA : 0);
+        const fe* pv = args.pts + (h ? 0 : B) + (g ? JA : 0);
         const fe one = fe_one();
         fe acc = one;
         for (uint32_t v = J - 1; v > u; --v) {
           const fe p = fe_vgpr(pv[v]);
           acc = fe_mul_s(acc, ((c >> (J - 1 - v)) & 1u) ? p : fe_sub(one, p));
         }
-        fe_store(rsuf + z, acc);
+        fe_store(rsuf + (y - 128), acc);
       }
     }
     return;
@@ -879,7 +883,7 @@ hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* 
     return hipErrorInvalidValue;
   const uint64_t NL = 1ull << (args.L - args.B);
   const uint64_t total = ((NL + (1ull << args.B) - 1 + (Hs ? NL - 1 : 0) + 63) & ~63ull) + 128 +
-                         (rsuf_out ? kEqTailRsuf : 0);
+                         (rsuf_out ? 2 * kEqTailRsuf : 0);
   hipLaunchKernelGGL(eq_setup_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, args,
                      pts_out, c_out, lo, H, Hs, dt_out, prev_out, kw, rsuf_out);
   return hipGetLastError();
@@ -2327,13 +2331,13 @@ hipError_t launch_corner_sums_lo(const fe* T, uint32_t B, uint32_t a, const fe* 
 
 hipError_t launch_sumcheck_eq_head(const fe* Y, uint32_t B, const fe* e_grp, const fe* pts, fe* c,
                                    fe* prev, DevSha* t, fe* polys, fe* rs, fe* wfold,
-                                   hipStream_t st, CoopCtl ctl, const uint32_t* kw) {
+                                   hipStream_t st, CoopCtl ctl, const uint32_t* kw, const fe* rsuf) {
   if (B == 0 || B > kTailLogMax || !wfold) return hipErrorInvalidValue;
   const uint32_t JA = B < 6 ? B : 6;
   const size_t lds = ((1ull << B) + (1ull << (B - JA))) * sizeof(fe);
   hipLaunchKernelGGL(sumcheck_eq_tail_kernel, dim3(1), dim3(kRedThreads), lds, st, Y, 0u,
                      (const fe*)nullptr, B, e_grp, pts, c, prev, t, polys, rs, (fe*)nullptr,
-                     (fe*)nullptr, kw, wfold, ctl, HostOut{}, (const fe*)nullptr, 0u, (const fe*)nullptr);
+                     (fe*)nullptr, kw, wfold, ctl, HostOut{}, (const fe*)nullptr, 0u, rsuf);
   return hipGetLastError();
 }
 

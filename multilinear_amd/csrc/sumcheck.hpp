@@ -93,7 +93,8 @@ hipError_t launch_corner_sums_lo(const fe* T, uint32_t B, uint32_t a, const fe* 
                                  hipStream_t st);
 hipError_t launch_sumcheck_eq_head(const fe* Y, uint32_t B, const fe* e_grp, const fe* pts, fe* c,
                                    fe* prev, DevSha* t, fe* polys, fe* rs, fe* wfold,
-                                   hipStream_t st, CoopCtl ctl, const uint32_t* kw = nullptr);
+                                   hipStream_t st, CoopCtl ctl, const uint32_t* kw = nullptr,
+                                   const fe* rsuf = nullptr);
 // Setup of the eq-factored sumcheck in one launch (arguments by value): the
 // points, c_0 = 1, lo = eq(p_B..p_{L-1}), head suffix tables H (over
 // p_0..p_{B-1}), tail suffix tables Hs (optional), transcript state and claim
@@ -106,9 +107,10 @@ struct EqSetupArgs {
 };
 // kw (optional, 64 L words): per round k whose (c1, c2) absorb leaves the
 // transcript buffer empty (len + 32 (k + 1) = 0 mod 64), the padding block's
-// K + W table at kw + 64 k.  rsuf_out (optional, kEqTailRsuf entries): the eq
-// tail's two corner groups' suffix products over p_B.. (group g, variable u,
-// corner c at g 384 + u 64 + c; sumcheck_eq_tail_kernel's S.rsuf / S.rsufB).
+// K + W table at kw + 64 k.  rsuf_out (optional, 2 kEqTailRsuf entries): the
+// eq tail's two corner groups' suffix products over p_B.. (group g, variable
+// u, corner c at g 384 + u 64 + c; sumcheck_eq_tail_kernel's S.rsuf /
+// S.rsufB), then the eq head's over p_0..p_{B-1} (B <= 12).
 constexpr uint32_t kEqTailRsuf = 2 * 6 * 64;
 hipError_t launch_eq_setup(const EqSetupArgs& args, fe* pts_out, fe* c_out, fe* lo, fe* H, fe* Hs,
                            DevSha* dt_out, fe* prev_out, hipStream_t st, uint32_t* kw = nullptr,
